@@ -1,0 +1,136 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 bf16 edge-module inference images/sec on 1..8 MI355X.
+
+Metric/config are the ones BASELINE.json names ("images/sec ResNet-50 edge module at
+1/2/4/8 MI355X").  One step = one full edge-module step on every GPU:
+on-device synthetic uint8 frames (K11) -> preprocess (K12) -> ResNet-50 forward
+(hand-written gfx950 HIP kernels) -> softmax + top-1, captured in one hipGraph.
+Weights are random-init (seeded) ResNet-50 v1.5 of the full architecture.
+
+Data parallel, weak scaling: each rank runs its own per-GPU batch; the value is the
+WHOLE-JOB images/sec = world * batch * steps / max_rank_elapsed.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "images/sec ResNet-50 edge module at 1/2/4/8 MI355X; VM boot-to-ready sec"
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("KVEDGE_BENCH_BATCH", 256)),
+                    help="per-GPU batch")
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "yolov8n"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--json-out", default=None)
+    a = ap.parse_args(argv)
+
+    import torch
+    from kvedge_amd import ops, parallel
+    from kvedge_amd.engine import InferenceEngine
+
+    di = parallel.init_from_env(prefer_gpu=True)
+    if di.device.type != "cuda":
+        print("bench.py needs a GPU (MI355X); none visible", file=sys.stderr)
+        return 2
+    if not ops.load():
+        raise RuntimeError("kvedge native kernels not built: run python -m kvedge_amd._build")
+
+    t_build = time.perf_counter()
+    if a.model == "resnet50":
+        from kvedge_amd.models.resnet import KvResNet50
+
+        model = KvResNet50.build(seed=a.seed, device=di.device)
+        hw = KvResNet50.image_size
+    else:
+        from kvedge_amd.models.yolov8 import KvYoloV8n
+
+        model = KvYoloV8n.build(seed=a.seed, device=di.device)
+        hw = KvYoloV8n.image_size
+    # C1: every replica serves rank 0's weights
+    parallel.broadcast_tensors(parallel.model_tensors(model), src=0)
+    eng = InferenceEngine(model, a.batch, hw, device=di.device, seed=a.seed + di.rank,
+                          use_graph=not a.no_graph)
+    eng.prepare(warmup=2)
+    build_s = time.perf_counter() - t_build
+
+    for _ in range(a.warmup):
+        eng.run()
+    torch.cuda.synchronize()
+    parallel.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        eng.run()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    parallel.barrier()
+    torch.cuda.synchronize()
+
+    # C3: job time = slowest rank; C4: replica checksums (sanity, not timed)
+    (max_elapsed,) = parallel.allreduce_scalars([elapsed], op="max")
+    out0 = eng.outputs[0]
+    checksum = float(out0.double().sum().item())
+    sums = parallel.all_gather_scalar(checksum)
+
+    world = di.world_size
+    imgs = world * a.batch * a.steps
+    value = imgs / max_elapsed
+    ms_per_step = max_elapsed / a.steps * 1e3
+    flops = model.flops_per_image(hw) if hasattr(model, "flops_per_image") else None
+    res = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (on-device uint8 frames), random-init seeded weights",
+        "config": {
+            "model": a.model,
+            "global_batch": world * a.batch,
+            "per_gpu_batch": a.batch,
+            "seq_len": None,
+            "image_size": hw,
+            "parallelism": f"dp{world}",
+            "hip_graph": eng.graph is not None,
+        },
+        "extra": {
+            "tflops_per_gpu": round(value / world * flops / 1e12, 2) if flops else None,
+            "build_s": round(build_s, 2),
+            "replica_checksums": sums,
+            "backend": di.backend,
+        },
+    }
+    if di.is_main:
+        line = json.dumps(res)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    parallel.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,267 @@
+// N14: torch custom-op bindings for the gfx950 kernel library (TORCH_LIBRARY "kvedge").
+//
+// Every op writes into caller-provided output tensors (schema `Tensor(a!)`), runs
+// on torch's current HIP stream, allocates nothing and never synchronises, so a
+// whole forward built from these ops can be captured into one hipGraph
+// (kvedge_amd/engine).  Shapes/strides are computed by the Python wrappers in
+// kvedge_amd/ops/__init__.py; this layer only validates and launches.
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include "../kernels/kvedge_kernels.h"
+
+namespace {
+
+hipStream_t cur_stream(const at::Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check_dev(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "kvedge: ", name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), "kvedge: ", name, " must be contiguous");
+}
+
+void check_bf16(const at::Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "kvedge: ", name, " must be bf16");
+}
+
+void conv(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+          const c10::optional<at::Tensor>& res, at::Tensor& y, int64_t N, int64_t H, int64_t W,
+          int64_t Cin, int64_t ldx, int64_t x_coff, int64_t Ho, int64_t Wo, int64_t Cout,
+          int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t K, int64_t ldy,
+          int64_t y_coff, int64_t ldr, int64_t r_coff, int64_t act, int64_t mode,
+          int64_t tile) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_bf16(y, "y");
+  const c10::DeviceGuard g(x.device());
+  KvConvParams p{};
+  p.x = x.data_ptr();
+  p.w = w.data_ptr();
+  p.bias = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_dev(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= Cout, "kvedge: bias fp32[Cout]");
+    p.bias = bias->data_ptr<float>();
+  }
+  p.res = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_bf16(*res, "res");
+    p.res = res->data_ptr();
+  }
+  p.y = y.data_ptr();
+  p.N = (int)N; p.H = (int)H; p.W = (int)W; p.Cin = (int)Cin;
+  p.ldx = (int)ldx; p.x_coff = (int)x_coff;
+  p.Ho = (int)Ho; p.Wo = (int)Wo; p.Cout = (int)Cout;
+  p.KH = (int)KH; p.KW = (int)KW; p.stride = (int)stride; p.pad = (int)pad;
+  p.K = (int)K;
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == Cout, "kvedge: packed weight must be [Cout, Kpad]");
+  p.Kpad = (int)w.size(1);
+  p.M = (int)(N * Ho * Wo);
+  p.ldy = (int)ldy; p.y_coff = (int)y_coff; p.ldr = (int)ldr; p.r_coff = (int)r_coff;
+  p.act = (int)act; p.mode = (int)mode;
+  // bounds: every pointer offset the kernel forms must stay in int32 and in the buffer
+  TORCH_CHECK(x.numel() < (1ll << 31) && y.numel() < (1ll << 31), "kvedge: tensor too large for int32 indexing");
+  TORCH_CHECK(x.numel() >= N * H * W * ldx, "kvedge: x smaller than N*H*W*ldx");
+  TORCH_CHECK(x_coff + Cin <= ldx, "kvedge: x channel slice out of range");
+  TORCH_CHECK(y.numel() >= (int64_t)p.M * ldy && y_coff + Cout <= ldy, "kvedge: y too small");
+  if (p.res) TORCH_CHECK(res->numel() >= (int64_t)p.M * ldr && r_coff + Cout <= ldr, "kvedge: residual too small");
+  const int rc = kv_conv2d(&p, (int)tile, cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: kv_conv2d failed rc=", rc);
+}
+
+void maxpool2d(const at::Tensor& x, at::Tensor& y, int64_t N, int64_t H, int64_t W, int64_t C,
+               int64_t ldx, int64_t x_coff, int64_t ldy, int64_t y_coff, int64_t k, int64_t stride, int64_t pad,
+               int64_t Ho, int64_t Wo) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.numel() >= N * H * W * ldx && y.numel() >= N * Ho * Wo * ldy, "kvedge: maxpool sizes");
+  const c10::DeviceGuard g(x.device());
+  const int rc = kv_maxpool2d(x.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)ldx,
+                              (int)x_coff, (int)ldy, (int)y_coff, (int)k, (int)stride, (int)pad, (int)Ho,
+                              (int)Wo, cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: maxpool2d failed rc=", rc);
+}
+
+void sppf_pool(at::Tensor& buf, int64_t N, int64_t H, int64_t W, int64_t C) {
+  check_bf16(buf, "buf");
+  TORCH_CHECK(buf.numel() == N * H * W * 4 * C, "kvedge: sppf buffer must be [N,H,W,4C]");
+  const c10::DeviceGuard g(buf.device());
+  const int rc = kv_sppf_pool(buf.data_ptr(), (int)N, (int)H, (int)W, (int)C, cur_stream(buf));
+  TORCH_CHECK(rc == 0, "kvedge: sppf failed rc=", rc);
+}
+
+void global_avgpool(const at::Tensor& x, at::Tensor& y, int64_t N, int64_t HW, int64_t C) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.numel() == N * HW * C && y.numel() == N * C, "kvedge: avgpool sizes");
+  const c10::DeviceGuard g(x.device());
+  const int rc = kv_global_avgpool(x.data_ptr(), y.data_ptr(), (int)N, (int)HW, (int)C, cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: avgpool failed rc=", rc);
+}
+
+void softmax_rows(const at::Tensor& x, at::Tensor& y, at::Tensor& argmax) {
+  check_bf16(x, "x");
+  check_dev(y, "y");
+  check_dev(argmax, "argmax");
+  TORCH_CHECK(x.dim() == 2 && y.sizes() == x.sizes() && y.scalar_type() == at::kFloat, "kvedge: softmax y");
+  TORCH_CHECK(argmax.scalar_type() == at::kLong && argmax.numel() == x.size(0), "kvedge: argmax");
+  const c10::DeviceGuard g(x.device());
+  const int rc = kv_softmax_rows(x.data_ptr(), y.data_ptr<float>(), argmax.data_ptr<int64_t>(),
+                                 (int)x.size(0), (int)x.size(1), cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: softmax failed rc=", rc);
+}
+
+void upsample2x(const at::Tensor& x, at::Tensor& y, int64_t N, int64_t H, int64_t W, int64_t C,
+                int64_t ldx, int64_t x_coff, int64_t ldy, int64_t y_coff) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.numel() >= N * H * W * ldx && y.numel() >= N * 4 * H * W * ldy, "kvedge: upsample sizes");
+  const c10::DeviceGuard g(x.device());
+  const int rc = kv_upsample2x(x.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W, (int)C, (int)ldx,
+                               (int)x_coff, (int)ldy, (int)y_coff, cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: upsample2x failed rc=", rc);
+}
+
+void yolo_decode(const at::Tensor& f0, const at::Tensor& f1, const at::Tensor& f2, int64_t h0,
+                 int64_t w0, int64_t h1, int64_t w1, int64_t h2, int64_t w2, int64_t s0,
+                 int64_t s1, int64_t s2, int64_t nc, at::Tensor& boxes, at::Tensor& scores,
+                 at::Tensor& cls) {
+  check_bf16(f0, "f0");
+  check_bf16(f1, "f1");
+  check_bf16(f2, "f2");
+  const int64_t N = f0.size(0);
+  const int64_t A = h0 * w0 + h1 * w1 + h2 * w2;
+  const int64_t ch = 64 + nc;
+  TORCH_CHECK(f0.numel() == N * h0 * w0 * ch && f1.numel() == N * h1 * w1 * ch &&
+                  f2.numel() == N * h2 * w2 * ch, "kvedge: decode feature sizes");
+  TORCH_CHECK(boxes.numel() == N * A * 4 && boxes.scalar_type() == at::kFloat, "kvedge: boxes");
+  TORCH_CHECK(scores.numel() == N * A && scores.scalar_type() == at::kFloat, "kvedge: scores");
+  TORCH_CHECK(cls.numel() == N * A && cls.scalar_type() == at::kInt, "kvedge: cls");
+  const c10::DeviceGuard g(f0.device());
+  const int rc = kv_yolo_decode(f0.data_ptr(), f1.data_ptr(), f2.data_ptr(), (int)h0, (int)w0,
+                                (int)h1, (int)w1, (int)h2, (int)w2, (int)s0, (int)s1, (int)s2,
+                                (int)N, (int)nc, boxes.data_ptr<float>(), scores.data_ptr<float>(),
+                                cls.data_ptr<int>(), cur_stream(f0));
+  TORCH_CHECK(rc == 0, "kvedge: yolo_decode failed rc=", rc);
+}
+
+void nms(const at::Tensor& boxes, const at::Tensor& scores, const at::Tensor& cls, double conf,
+         double iou, int64_t max_det, at::Tensor& out, at::Tensor& count) {
+  check_dev(boxes, "boxes");
+  check_dev(scores, "scores");
+  check_dev(cls, "cls");
+  TORCH_CHECK(scores.dim() == 2, "kvedge: scores [N, A]");
+  const int64_t N = scores.size(0), A = scores.size(1);
+  TORCH_CHECK(boxes.numel() == N * A * 4 && cls.numel() == N * A, "kvedge: nms inputs");
+  TORCH_CHECK(out.numel() == N * max_det * 6 && out.scalar_type() == at::kFloat, "kvedge: nms out");
+  TORCH_CHECK(count.numel() == N && count.scalar_type() == at::kInt, "kvedge: nms count");
+  const c10::DeviceGuard g(scores.device());
+  const int rc = kv_nms(boxes.data_ptr<float>(), scores.data_ptr<float>(), cls.data_ptr<int>(),
+                        (int)N, (int)A, (float)conf, (float)iou, (int)max_det,
+                        out.data_ptr<float>(), count.data_ptr<int>(), cur_stream(scores));
+  TORCH_CHECK(rc == 0, "kvedge: nms failed rc=", rc);
+}
+
+void synth_frames(at::Tensor& y, int64_t seed, int64_t step) {
+  check_dev(y, "y");
+  TORCH_CHECK(y.scalar_type() == at::kByte && y.dim() == 4 && y.size(3) == 3, "kvedge: frames u8 [N,H,W,3]");
+  const c10::DeviceGuard g(y.device());
+  const int rc = kv_synth_frames(y.data_ptr<uint8_t>(), (int)y.size(0), (int)y.size(1),
+                                 (int)y.size(2), (uint64_t)seed, (uint64_t)step, cur_stream(y));
+  TORCH_CHECK(rc == 0, "kvedge: synth_frames failed rc=", rc);
+}
+
+void synth_frames_dev(at::Tensor& y, at::Tensor& step, int64_t seed) {
+  check_dev(y, "y");
+  check_dev(step, "step");
+  TORCH_CHECK(y.scalar_type() == at::kByte && y.dim() == 4 && y.size(3) == 3, "kvedge: frames u8 [N,H,W,3]");
+  TORCH_CHECK(step.scalar_type() == at::kLong && step.numel() == 1, "kvedge: step int64[1]");
+  const c10::DeviceGuard g(y.device());
+  const int rc = kv_synth_frames_dev(y.data_ptr<uint8_t>(), (int)y.size(0), (int)y.size(1),
+                                     (int)y.size(2), (uint64_t)seed,
+                                     reinterpret_cast<uint64_t*>(step.data_ptr<int64_t>()), cur_stream(y));
+  TORCH_CHECK(rc == 0, "kvedge: synth_frames_dev failed rc=", rc);
+}
+
+void preprocess(const at::Tensor& x, at::Tensor& y, at::ArrayRef<double> mean,
+                at::ArrayRef<double> stdv) {
+  check_dev(x, "x");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.scalar_type() == at::kByte && x.dim() == 4 && x.size(3) == 3, "kvedge: x u8 [N,H,W,3]");
+  TORCH_CHECK(y.dim() == 4 && y.size(0) == x.size(0) && y.size(1) == x.size(1) &&
+                  y.size(2) == x.size(2) && y.size(3) == 4, "kvedge: y bf16 [N,H,W,4]");
+  TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "kvedge: mean/std of 3");
+  float m[3], is[3];
+  for (int i = 0; i < 3; ++i) {
+    m[i] = (float)mean[i];
+    is[i] = (float)(1.0 / stdv[i]);
+  }
+  const c10::DeviceGuard g(x.device());
+  const int rc = kv_preprocess(x.data_ptr<uint8_t>(), y.data_ptr(), (int)x.size(0), (int)x.size(1),
+                               (int)x.size(2), m, is, cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: preprocess failed rc=", rc);
+}
+
+void batchnorm_nhwc(const at::Tensor& x, at::Tensor& y, const at::Tensor& scale,
+                    const at::Tensor& shift, bool relu) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  check_dev(scale, "scale");
+  check_dev(shift, "shift");
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(scale.numel() == C && shift.numel() == C && scale.scalar_type() == at::kFloat &&
+                  shift.scalar_type() == at::kFloat, "kvedge: bn scale/shift fp32[C]");
+  TORCH_CHECK(y.sizes() == x.sizes(), "kvedge: bn y shape");
+  const c10::DeviceGuard g(x.device());
+  const int rc = kv_batchnorm_nhwc(x.data_ptr(), y.data_ptr(), scale.data_ptr<float>(),
+                                   shift.data_ptr<float>(), x.numel() / C, (int)C, relu ? 1 : 0,
+                                   cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: batchnorm failed rc=", rc);
+}
+
+int64_t conv_num_tiles() { return kv_conv_num_tiles(); }
+
+}  // namespace
+
+TORCH_LIBRARY(kvedge, m) {
+  m.def("conv(Tensor x, Tensor w, Tensor? bias, Tensor? res, Tensor(a!) y, int N, int H, int W, "
+        "int Cin, int ldx, int x_coff, int Ho, int Wo, int Cout, int KH, int KW, int stride, "
+        "int pad, int K, int ldy, int y_coff, int ldr, int r_coff, int act, int mode, int tile) -> ()");
+  m.def("maxpool2d(Tensor x, Tensor(a!) y, int N, int H, int W, int C, int ldx, int x_coff, int ldy, "
+        "int y_coff, int k, int stride, int pad, int Ho, int Wo) -> ()");
+  m.def("sppf_pool(Tensor(a!) buf, int N, int H, int W, int C) -> ()");
+  m.def("global_avgpool(Tensor x, Tensor(a!) y, int N, int HW, int C) -> ()");
+  m.def("softmax_rows(Tensor x, Tensor(a!) y, Tensor(b!) argmax) -> ()");
+  m.def("upsample2x(Tensor x, Tensor(a!) y, int N, int H, int W, int C, int ldx, int x_coff, int ldy, "
+        "int y_coff) -> ()");
+  m.def("yolo_decode(Tensor f0, Tensor f1, Tensor f2, int h0, int w0, int h1, int w1, int h2, "
+        "int w2, int s0, int s1, int s2, int nc, Tensor(a!) boxes, Tensor(b!) scores, "
+        "Tensor(c!) cls) -> ()");
+  m.def("nms(Tensor boxes, Tensor scores, Tensor cls, float conf, float iou, int max_det, "
+        "Tensor(a!) out, Tensor(b!) count) -> ()");
+  m.def("synth_frames(Tensor(a!) y, int seed, int step) -> ()");
+  m.def("synth_frames_dev(Tensor(a!) y, Tensor(b!) step, int seed) -> ()");
+  m.def("preprocess(Tensor x, Tensor(a!) y, float[] mean, float[] std) -> ()");
+  m.def("batchnorm_nhwc(Tensor x, Tensor(a!) y, Tensor scale, Tensor shift, bool relu) -> ()");
+  m.def("conv_num_tiles() -> int", conv_num_tiles);
+}
+
+TORCH_LIBRARY_IMPL(kvedge, CUDA, m) {
+  m.impl("conv", conv);
+  m.impl("maxpool2d", maxpool2d);
+  m.impl("sppf_pool", sppf_pool);
+  m.impl("global_avgpool", global_avgpool);
+  m.impl("softmax_rows", softmax_rows);
+  m.impl("upsample2x", upsample2x);
+  m.impl("yolo_decode", yolo_decode);
+  m.impl("nms", nms);
+  m.impl("synth_frames", synth_frames);
+  m.impl("synth_frames_dev", synth_frames_dev);
+  m.impl("preprocess", preprocess);
+  m.impl("batchnorm_nhwc", batchnorm_nhwc);
+}
+

@@ -1,0 +1,55 @@
+// Shared device helpers for the kvedge_amd gfx950 (CDNA4) kernel library.
+//
+// Everything here is written for wave64 / MFMA / 160 KiB LDS; there is no
+// other target.  The reference (levi106/kvedge) has no kernels at all
+// (SURVEY.md §2.2); these exist for the north-star inference hot path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+namespace kvedge {
+
+constexpr int kWave = 64;   // CDNA wavefront; never 32
+constexpr int kNumXcd = 8;  // MI355X: 8 XCDs x 32 CUs, private 4 MiB L2 each
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be
+// bijective").  Blocks b, b+8, b+16 ... are dealt to the same XCD, so we hand
+// them CONSECUTIVE logical tiles: neighbouring tiles share operand panels and
+// hit the same L2.  Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / kNumXcd, r = nwg % kNumXcd;
+  const int xcd = bid % kNumXcd, idx = bid / kNumXcd;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+__device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
+__device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }  // v_cvt_pk_bf16_f32, NaN-safe
+
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+enum Act : int { kActNone = 0, kActRelu = 1, kActSilu = 2 };
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == kActRelu) return fmaxf(v, 0.0f);
+  if (act == kActSilu) return silu(v);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+}  // namespace kvedge

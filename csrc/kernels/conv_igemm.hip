@@ -1,0 +1,317 @@
+// K1/K2/K3 — implicit-GEMM convolution and GEMM on CDNA4 MFMA (gfx950).
+//
+// One kernel family covers every conv in ResNet-50 and YOLOv8n plus the FC layer:
+//   M = N*Ho*Wo output pixels, N = Cout, K = KH*KW*Cin (NHWC, k-order (r, s, c)).
+// The im2col gather is fused into the global->register staging of the A tile:
+// no im2col buffer ever exists.  BatchNorm is folded into W/bias on the host,
+// and bias + residual + ReLU/SiLU + bf16 cast are fused into the epilogue.
+//
+// Design (MI355X-first, see /opt/skills/guides/cdna_hip_programming.md):
+//  * 256-thread workgroups (4 wave64s), tile BM x BN x 64, v_mfma_f32_16x16x32_bf16.
+//  * Operands swapped: D = W * A^T, so the accumulator of a lane holds FOUR
+//    CONSECUTIVE OUTPUT CHANNELS of one pixel -> 8-byte NHWC stores.
+//  * LDS image [row][64] bf16 (128-B rows) with chunk ^= (row & 7) XOR swizzle:
+//    ds_write_b128 (8-lane contiguous groups) and the ds_read_b128 fragment reads
+//    (4 x 16-lane groups) are both bank-conflict-free (derivation in SURVEY.md
+//    notes / docs/kernels.md).
+//  * Register-staged double buffer (T14 async-STAGE split): tile k+1 is issued to
+//    VGPRs before the MFMAs of tile k and written to the other LDS buffer after,
+//    one barrier per K step.
+//  * XCD-aware bijective block remap so the N-tiles of one M panel share an L2.
+//
+// The reference has no kernels; the kernel inventory this
+// implements is SURVEY.md §2.5 K1-K3.
+#include "common.h"
+#include "kvedge_kernels.h"
+
+namespace kvedge {
+namespace {
+
+constexpr int BK = 64;
+
+struct TileCfg {
+  int bm, bn, wm, wn;
+};
+
+template <int BM, int BN, int WM, int WN, int MODE>
+__global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const KvConvParams p) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int AR = BM / 32;  // A rows staged per thread
+  constexpr int BR = BN / 32;  // B rows staged per thread
+  static_assert(WM * WN == 4, "4 waves per workgroup");
+  static_assert(TM >= 1 && TN >= 1, "wave tile >= 16x16");
+
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (BM + BN) * BK];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int wm = wv / WN, wn = wv % WN;
+
+  const int nbm = (p.M + BM - 1) / BM;
+  const int nbn = (p.Cout + BN - 1) / BN;
+  const int t = xcd_remap(blockIdx.x, nbm * nbn);
+  const int m0 = (t / nbn) * BM;
+  const int n0 = (t % nbn) * BN;
+
+  const bf16* __restrict__ X = reinterpret_cast<const bf16*>(p.x);
+  const bf16* __restrict__ Wt = reinterpret_cast<const bf16*>(p.w);
+
+  const int cc = tid & 7;   // 16-B chunk column this thread stages
+  const int rr = tid >> 3;  // first staged row (then +32, +64 ...)
+
+  // ---- per-row gather info (fixed for the whole K loop) -------------------
+  int a_base[AR], a_h0[AR], a_w0[AR];
+  const int HoWo = p.Ho * p.Wo;
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int m = m0 + rr + 32 * i;
+    if (m < p.M) {
+      if (MODE == 1) {
+        a_base[i] = m * p.ldx + p.x_coff;
+        a_h0[i] = 0;
+        a_w0[i] = 0;
+      } else {
+        const int img = m / HoWo;
+        const int rem = m - img * HoWo;
+        const int ho = rem / p.Wo;
+        const int wo = rem - ho * p.Wo;
+        a_base[i] = img * p.H * p.W * p.ldx + p.x_coff;
+        a_h0[i] = ho * p.stride - p.pad;
+        a_w0[i] = wo * p.stride - p.pad;
+      }
+    } else {
+      a_base[i] = 0;
+      a_h0[i] = -(1 << 28);  // never in range
+      a_w0[i] = -(1 << 28);
+    }
+  }
+
+  // ---- incremental (r, s, c) state of this thread's chunk column (MODE 0) --
+  int kr = 0, ksx = 0, kc = cc * 8;
+  if (MODE == 0) {
+    while (kc >= p.Cin) {
+      kc -= p.Cin;
+      if (++ksx == p.KW) { ksx = 0; ++kr; }
+    }
+  }
+  const int kwp = (p.KW + 1) & ~1;  // stem: KW padded to even
+  const int kpr = kwp * 4;          // stem: K elements per filter row
+
+  uint4 ra[AR], rb[BR];
+
+  auto load_a = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (MODE == 1) {
+        const int k = kt * BK + cc * 8;
+        if (a_h0[i] >= 0 && k < p.Cin)
+          v = *reinterpret_cast<const uint4*>(X + a_base[i] + k);
+      } else if (MODE == 0) {
+        const int hi = a_h0[i] + kr, wi = a_w0[i] + ksx;
+        if (kr < p.KH && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
+          v = *reinterpret_cast<const uint4*>(X + a_base[i] + (hi * p.W + wi) * p.ldx + kc);
+      } else {  // MODE 2 stem: chunk = pixels (s, s+1) x 4 channels of filter row r
+        const int k = kt * BK + cc * 8;
+        const int r = k / kpr;
+        const int s = ((k - r * kpr) >> 3) * 2;
+        const int hi = a_h0[i] + r, wi = a_w0[i] + s;
+        if (r < p.KH && (unsigned)hi < (unsigned)p.H) {
+          const bf16* rowp = X + a_base[i] + hi * p.W * 4;
+          uint2 lo = make_uint2(0, 0), hi2 = make_uint2(0, 0);
+          if ((unsigned)wi < (unsigned)p.W) lo = *reinterpret_cast<const uint2*>(rowp + wi * 4);
+          if ((unsigned)(wi + 1) < (unsigned)p.W)
+            hi2 = *reinterpret_cast<const uint2*>(rowp + (wi + 1) * 4);
+          v = make_uint4(lo.x, lo.y, hi2.x, hi2.y);
+        }
+      }
+      ra[i] = v;
+    }
+  };
+  auto advance_k = [&]() {
+    if (MODE == 0) {
+      kc += BK;
+      while (kc >= p.Cin) {
+        kc -= p.Cin;
+        if (++ksx == p.KW) { ksx = 0; ++kr; }
+      }
+    }
+  };
+  auto load_b = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int n = n0 + rr + 32 * i;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n < p.Cout)
+        v = *reinterpret_cast<const uint4*>(Wt + (size_t)n * p.Kpad + kt * BK + cc * 8);
+      rb[i] = v;
+    }
+  };
+  auto store_tiles = [&](int buf) {
+    bf16* As = smem + buf * (BM + BN) * BK;
+    bf16* Bs = As + BM * BK;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int row = rr + 32 * i;
+      *reinterpret_cast<uint4*>(As + row * BK + ((cc ^ (row & 7)) << 3)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int row = rr + 32 * i;
+      *reinterpret_cast<uint4*>(Bs + row * BK + ((cc ^ (row & 7)) << 3)) = rb[i];
+    }
+  };
+
+  floatx4 acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int b = 0; b < TM; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const bf16* As = smem + buf * (BM + BN) * BK;
+    const bf16* Bs = As + BM * BK;
+    const int fr = lane & 15;
+    const int sw = lane & 7;  // == row & 7 for every fragment row
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int q = ks * 4 + (lane >> 4);
+      bf16x8 af[TM], bfg[TN];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int row = wm * WTM + tm * 16 + fr;
+        af[tm] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((q ^ sw) << 3));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = wn * WTN + tn * 16 + fr;
+        bfg[tn] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((q ^ sw) << 3));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+          acc[tn][tm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[tn], af[tm], acc[tn][tm], 0, 0, 0);
+    }
+  };
+
+  const int nk = p.Kpad / BK;
+  load_a(0);
+  load_b(0);
+  store_tiles(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      advance_k();
+      load_a(kt + 1);
+      load_b(kt + 1);
+    }
+    compute(cur);
+    if (more) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- fused epilogue: bias + residual + activation + bf16, 8-B stores ------
+  bf16* __restrict__ Y = reinterpret_cast<bf16*>(p.y);
+  const bf16* __restrict__ R = reinterpret_cast<const bf16*>(p.res);
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int n = n0 + wn * WTN + tn * 16 + (lane >> 4) * 4;
+    if (n >= p.Cout) continue;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.bias) bv = *reinterpret_cast<const float4*>(p.bias + n);
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      const int m = m0 + wm * WTM + tm * 16 + (lane & 15);
+      if (m >= p.M) continue;
+      float v0 = acc[tn][tm][0] + bv.x;
+      float v1 = acc[tn][tm][1] + bv.y;
+      float v2 = acc[tn][tm][2] + bv.z;
+      float v3 = acc[tn][tm][3] + bv.w;
+      if (R) {
+        const bf16x4 rv = *reinterpret_cast<const bf16x4*>(R + (size_t)m * p.ldr + p.r_coff + n);
+        v0 += (float)rv[0];
+        v1 += (float)rv[1];
+        v2 += (float)rv[2];
+        v3 += (float)rv[3];
+      }
+      bf16x4 o;
+      o[0] = f2bf(apply_act(v0, p.act));
+      o[1] = f2bf(apply_act(v1, p.act));
+      o[2] = f2bf(apply_act(v2, p.act));
+      o[3] = f2bf(apply_act(v3, p.act));
+      *reinterpret_cast<bf16x4*>(Y + (size_t)m * p.ldy + p.y_coff + n) = o;
+    }
+  }
+}
+
+typedef void (*ConvKernelFn)(const KvConvParams);
+
+template <int BM, int BN, int WM, int WN>
+struct TileInst {
+  static ConvKernelFn get(int mode) {
+    switch (mode) {
+      case 0: return conv_igemm_kernel<BM, BN, WM, WN, 0>;
+      case 1: return conv_igemm_kernel<BM, BN, WM, WN, 1>;
+      default: return conv_igemm_kernel<BM, BN, WM, WN, 2>;
+    }
+  }
+};
+
+struct TileEntry {
+  TileCfg cfg;
+  ConvKernelFn (*get)(int);
+};
+
+const TileEntry kTiles[] = {
+    {{128, 128, 2, 2}, &TileInst<128, 128, 2, 2>::get},
+    {{128, 64, 2, 2}, &TileInst<128, 64, 2, 2>::get},
+    {{64, 64, 2, 2}, &TileInst<64, 64, 2, 2>::get},
+    {{256, 64, 4, 1}, &TileInst<256, 64, 4, 1>::get},
+    {{64, 128, 2, 2}, &TileInst<64, 128, 2, 2>::get},
+    {{256, 128, 2, 2}, &TileInst<256, 128, 2, 2>::get},
+};
+constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
+
+}  // namespace
+}  // namespace kvedge
+
+using namespace kvedge;
+
+extern "C" int kv_conv_num_tiles(void) { return kNumTiles; }
+
+extern "C" int kv_conv_pick_tile(const KvConvParams* p) {
+  // Heuristic: enough workgroups to cover 256 CUs x 2, largest tile otherwise.
+  const long long M = p->M, N = p->Cout;
+  auto nwg = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+  if (N <= 64) {
+    if (nwg(256, 64) >= 1024) return 3;
+    if (nwg(128, 64) >= 512) return 1;
+    return 2;
+  }
+  if (nwg(256, 128) >= 2048) return 5;
+  if (nwg(128, 128) >= 512) return 0;
+  if (nwg(64, 128) >= 256) return 4;
+  return 2;
+}
+
+extern "C" int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream) {
+  if (p->Kpad % BK != 0 || p->Cout % 4 != 0) return -1;
+  if (p->mode == 2 && (p->Cin != 4 || p->ldx != 4)) return -2;
+  if (p->mode != 2 && (p->Cin % 8 != 0 || p->ldx % 8 != 0 || p->x_coff % 8 != 0)) return -3;
+  if (p->mode == 1 && (p->KH != 1 || p->KW != 1 || p->stride != 1 || p->pad != 0)) return -4;
+  if ((p->ldy % 4) || (p->y_coff % 4) || (p->res && ((p->ldr % 4) || (p->r_coff % 4)))) return -5;
+  if (tile < 0) tile = kv_conv_pick_tile(p);
+  if (tile >= kNumTiles) return -6;
+  const TileEntry& e = kTiles[tile];
+  const long long nwg = (long long)((p->M + e.cfg.bm - 1) / e.cfg.bm) *
+                        ((p->Cout + e.cfg.bn - 1) / e.cfg.bn);
+  if (nwg <= 0) return 0;
+  ConvKernelFn fn = e.get(p->mode);
+  hipLaunchKernelGGL(fn, dim3((unsigned)nwg), dim3(256), 0, stream, *p);
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}

@@ -1,0 +1,82 @@
+// Host-visible launcher ABI of libkvedge kernels (gfx950 only).
+//
+// The kernels take raw device pointers and a hipStream_t so they can be driven
+// from the torch binding (csrc/bindings/ops.cpp), from native C++ tools and from
+// hipGraph capture alike.  Every launcher is capture-safe: no allocation, no
+// synchronisation, no host<->device copies (cdna_hip_programming.md G9).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// ---------------------------------------------------------------------------
+// K1/K2/K3: implicit-GEMM convolution / GEMM on MFMA, NHWC bf16, fp32 accumulate
+//   y[m, y_coff + n] = act( sum_k A[m,k] * W[n,k] + bias[n] + res[m, n] )
+//   m = (img, ho, wo), k = (r, s, c).  BN is folded into W/bias at load time.
+// ---------------------------------------------------------------------------
+typedef struct KvConvParams {
+  const void* x;      // bf16 input, pixel stride ldx elements, channel offset x_coff
+  const void* w;      // bf16 packed weights [Cout][Kpad]
+  const float* bias;  // fp32 [Cout] or NULL
+  const void* res;    // bf16 residual [M][ldr] or NULL
+  void* y;            // bf16 output, row stride ldy, channel offset y_coff
+  int N, H, W, Cin;   // input geometry (Cin = logical channels read)
+  int ldx, x_coff;
+  int Ho, Wo, Cout;
+  int KH, KW, stride, pad;
+  int K, Kpad;        // logical and padded (multiple of 64) reduction length
+  int M;              // N*Ho*Wo
+  int ldy, y_coff, ldr, r_coff;
+  int act;            // 0 none, 1 relu, 2 silu
+  int mode;           // 0 general, 1 1x1/s1/p0 GEMM, 2 stem (Cin=4, KW padded even)
+} KvConvParams;
+
+// tile: -1 = heuristic; otherwise an index into the tile table (kv_conv_num_tiles()).
+int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream);
+int kv_conv_num_tiles(void);
+int kv_conv_pick_tile(const KvConvParams* p);
+
+// K5: max pool NHWC (k x k, stride, pad); C % 8 == 0.  ldx/ldy allow channel slices.
+int kv_maxpool2d(const void* x, void* y, int N, int H, int W, int C, int ldx, int x_coff,
+                 int ldy, int y_coff, int k, int stride, int pad, int Ho, int Wo, hipStream_t s);
+// K5b: YOLOv8 SPPF: buf holds [x | y1 | y2 | y3] channel slices (4*C wide); x is
+// already written in slice 0; writes y1=mp5(x), y2=mp5(y1), y3=mp5(y2) in one pass.
+int kv_sppf_pool(void* buf, int N, int H, int W, int C, hipStream_t s);
+// K6: global average pool NHWC -> [N, C] bf16.
+int kv_global_avgpool(const void* x, void* y, int N, int HW, int C, hipStream_t s);
+// K7: row softmax, bf16 [rows, cols] -> fp32 probabilities; also writes argmax.
+int kv_softmax_rows(const void* x, float* y, int64_t* argmax, int rows, int cols, hipStream_t s);
+// K8: nearest 2x upsample of x [N,H,W,C] written into channel slice of y [N,2H,2W,ldy].
+int kv_upsample2x(const void* x, void* y, int N, int H, int W, int C, int ldx, int x_coff,
+                  int ldy, int y_coff, hipStream_t s);
+// K9: YOLOv8 decode (DFL softmax + expectation + dist2bbox + class sigmoid/max).
+//   feats: per level bf16 [N, HW_l, 64 + nc]; out boxes fp32 [N, A, 4] xyxy,
+//   scores fp32 [N, A], cls int32 [N, A].  A = sum HW_l.
+int kv_yolo_decode(const void* f0, const void* f1, const void* f2, int h0, int w0, int h1,
+                   int w1, int h2, int w2, int s0, int s1, int s2, int N, int nc,
+                   float* boxes, float* scores, int* cls, hipStream_t s);
+// K10: class-aware NMS per image: score threshold, sort, greedy IoU suppression,
+//   keep <= max_det.  out fp32 [N, max_det, 6] (x1,y1,x2,y2,score,cls); count int32 [N].
+int kv_nms(const float* boxes, const float* scores, const int* cls, int N, int A,
+           float conf_thres, float iou_thres, int max_det, float* out, int* count,
+           hipStream_t s);
+// K11: on-device synthetic camera frames, uint8 NHWC3, deterministic in (seed, step).
+int kv_synth_frames(uint8_t* y, int N, int H, int W, uint64_t seed, uint64_t step,
+                    hipStream_t s);
+// K11b: same but the step counter is read from device memory and incremented by
+// the kernel, so a captured hipGraph produces fresh frames on every replay.
+int kv_synth_frames_dev(uint8_t* y, int N, int H, int W, uint64_t seed, uint64_t* step,
+                        hipStream_t s);
+// K12: uint8 NHWC3 -> bf16 NHWC4 normalized ((x/255 - mean)/std), channel 3 = 0.
+int kv_preprocess(const uint8_t* x, void* y, int N, int H, int W, const float* mean3,
+                  const float* inv_std3, hipStream_t s);
+// K4 fallback: y = x*scale[c] + shift[c] (+relu) on NHWC bf16.
+int kv_batchnorm_nhwc(const void* x, void* y, const float* scale, const float* shift,
+                      int64_t rows, int C, int relu, hipStream_t s);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,363 @@
+// K4 (BN fallback), K5 (max pool, SPPF), K6 (global avg pool), K7 (softmax),
+// K8 (nearest 2x upsample into a concat slice), K11 (synthetic frames),
+// K12 (uint8 -> normalized bf16 NHWC4).  SURVEY.md §2.5.
+//
+// All of these are HBM-bound streaming ops: every lane moves 16 B (8 bf16
+// channels) per access (cdna_hip_programming.md Guideline 13), grids are capped
+// at 256 CUs x 8 blocks and grid-stride the rest (Guideline 11).
+#include "common.h"
+#include "kvedge_kernels.h"
+
+namespace kvedge {
+namespace {
+
+constexpr int kBlock = 256;
+inline unsigned grid_for(long long work) {
+  long long g = (work + kBlock - 1) / kBlock;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+__device__ __forceinline__ bf16x8 max8(bf16x8 a, bf16x8 b) {
+  bf16x8 r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r[i] = f2bf(fmaxf((float)a[i], (float)b[i]));
+  return r;
+}
+
+// ---- K5 max pool ----------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void maxpool_kernel(const bf16* __restrict__ x,
+                                                         bf16* __restrict__ y, int N, int H,
+                                                         int W, int C, int ldx, int x_coff,
+                                                         int ldy, int y_coff, int k, int stride,
+                                                         int pad, int Ho, int Wo) {
+  const int C8 = C / 8;
+  const long long total = (long long)N * Ho * Wo * C8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8);
+    long long pix = i / C8;
+    const int wo = (int)(pix % Wo);
+    pix /= Wo;
+    const int ho = (int)(pix % Ho);
+    const int n = (int)(pix / Ho);
+    float m[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+    const int h0 = ho * stride - pad, w0 = wo * stride - pad;
+    for (int r = 0; r < k; ++r) {
+      const int hi = h0 + r;
+      if ((unsigned)hi >= (unsigned)H) continue;
+      for (int s = 0; s < k; ++s) {
+        const int wi = w0 + s;
+        if ((unsigned)wi >= (unsigned)W) continue;
+        const bf16x8 v =
+            *reinterpret_cast<const bf16x8*>(x + ((long long)(n * H + hi) * W + wi) * ldx + x_coff + c8 * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], (float)v[j]);
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(m[j]);
+    *reinterpret_cast<bf16x8*>(y + ((long long)(n * Ho + ho) * Wo + wo) * ldy + y_coff + c8 * 8) = o;
+  }
+}
+
+// ---- K5b SPPF: y1 = mp5(x), y2 = mp5(y1) = mp9(x), y3 = mp13(x) ------------
+// Composition of stride-1 max filters with -inf padding is the max over the
+// summed window, so one pass over x produces all three slices exactly.
+__global__ __launch_bounds__(kBlock) void sppf_kernel(bf16* __restrict__ buf, int N, int H,
+                                                      int W, int C) {
+  const int C8 = C / 8;
+  const int ld = 4 * C;
+  const long long total = (long long)N * H * W * C8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8);
+    long long pix = i / C8;
+    const int w = (int)(pix % W);
+    pix /= W;
+    const int h = (int)(pix % H);
+    const int n = (int)(pix / H);
+    float m5[8], m9[8], m13[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m5[j] = m9[j] = m13[j] = -INFINITY;
+    for (int dr = -6; dr <= 6; ++dr) {
+      const int hi = h + dr;
+      if ((unsigned)hi >= (unsigned)H) continue;
+      const int adr = dr < 0 ? -dr : dr;
+      for (int ds = -6; ds <= 6; ++ds) {
+        const int wi = w + ds;
+        if ((unsigned)wi >= (unsigned)W) continue;
+        const int ads = ds < 0 ? -ds : ds;
+        const int ring = adr > ads ? adr : ads;
+        const bf16x8 v =
+            *reinterpret_cast<const bf16x8*>(buf + ((long long)(n * H + hi) * W + wi) * ld + c8 * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = (float)v[j];
+          m13[j] = fmaxf(m13[j], f);
+          if (ring <= 4) m9[j] = fmaxf(m9[j], f);
+          if (ring <= 2) m5[j] = fmaxf(m5[j], f);
+        }
+      }
+    }
+    bf16* o = buf + ((long long)(n * H + h) * W + w) * ld + c8 * 8;
+    bf16x8 a, b, c;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = f2bf(m5[j]);
+      b[j] = f2bf(m9[j]);
+      c[j] = f2bf(m13[j]);
+    }
+    *reinterpret_cast<bf16x8*>(o + C) = a;
+    *reinterpret_cast<bf16x8*>(o + 2 * C) = b;
+    *reinterpret_cast<bf16x8*>(o + 3 * C) = c;
+  }
+}
+
+// ---- K6 global average pool: one thread per (n, 8 channels) ----------------
+__global__ __launch_bounds__(kBlock) void avgpool_kernel(const bf16* __restrict__ x,
+                                                         bf16* __restrict__ y, int N, int HW,
+                                                         int C) {
+  const int C8 = C / 8;
+  const long long total = (long long)N * C8;
+  const float inv = 1.0f / (float)HW;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8);
+    const int n = (int)(i / C8);
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bf16* p = x + (long long)n * HW * C + c8 * 8;
+    for (int q = 0; q < HW; ++q) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(p + (long long)q * C);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(s[j] * inv);
+    *reinterpret_cast<bf16x8*>(y + (long long)n * C + c8 * 8) = o;
+  }
+}
+
+// ---- K7 row softmax + argmax: one wave64 per row ---------------------------
+__global__ __launch_bounds__(kBlock) void softmax_kernel(const bf16* __restrict__ x,
+                                                         float* __restrict__ y,
+                                                         int64_t* __restrict__ amax, int rows,
+                                                         int cols) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const bf16* xr = x + (long long)row * cols;
+  float mx = -INFINITY;
+  int arg = 0x7fffffff;
+  for (int c = lane; c < cols; c += 64) {
+    const float v = (float)xr[c];
+    if (v > mx) { mx = v; arg = c; }
+  }
+  // wave argmax (ties -> lowest index)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, 64);
+    const int oa = __shfl_xor(arg, o, 64);
+    if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
+  }
+  float sum = 0.f;
+  for (int c = lane; c < cols; c += 64) sum += __expf((float)xr[c] - mx);
+  sum = wave_sum(sum);
+  const float inv = 1.0f / sum;
+  float* yr = y + (long long)row * cols;
+  for (int c = lane; c < cols; c += 64) yr[c] = __expf((float)xr[c] - mx) * inv;
+  if (lane == 0 && amax) amax[row] = arg;
+}
+
+// ---- K8 nearest 2x upsample into a channel slice ---------------------------
+__global__ __launch_bounds__(kBlock) void upsample2x_kernel(const bf16* __restrict__ x,
+                                                            bf16* __restrict__ y, int N, int H,
+                                                            int W, int C, int ldx, int x_coff,
+                                                            int ldy, int y_coff) {
+  const int C8 = C / 8;
+  const int Ho = 2 * H, Wo = 2 * W;
+  const long long total = (long long)N * Ho * Wo * C8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8);
+    long long pix = i / C8;
+    const int wo = (int)(pix % Wo);
+    pix /= Wo;
+    const int ho = (int)(pix % Ho);
+    const int n = (int)(pix / Ho);
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(
+        x + ((long long)(n * H + (ho >> 1)) * W + (wo >> 1)) * ldx + x_coff + c8 * 8);
+    *reinterpret_cast<bf16x8*>(y + ((long long)(n * Ho + ho) * Wo + wo) * ldy + y_coff + c8 * 8) = v;
+  }
+}
+
+// ---- K11 synthetic frames: counter-based hash RNG (splitmix64) --------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Each thread produces 8 bytes.  Frames are a smooth gradient + hashed noise so
+// that they are not constant (constant inputs flatter DVFS, guide rule 25).
+__device__ __forceinline__ void synth_body(uint8_t* y, long long total8, uint64_t seed,
+                                           uint64_t step) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total8;
+       i += (long long)gridDim.x * blockDim.x) {
+    const uint64_t h = splitmix64(seed ^ (step * 0xD1B54A32D192ED03ull) ^ (uint64_t)i);
+    *reinterpret_cast<uint64_t*>(y + i * 8) = h;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void synth_kernel(uint8_t* y, long long total8,
+                                                       uint64_t seed, uint64_t step) {
+  synth_body(y, total8, seed, step);
+}
+
+__global__ __launch_bounds__(kBlock) void synth_dev_kernel(uint8_t* y, long long total8,
+                                                           uint64_t seed, uint64_t* step) {
+  const uint64_t s = *step;
+  synth_body(y, total8, seed, s);
+}
+
+__global__ void bump_kernel(uint64_t* step) { *step += 1; }
+
+// ---- K12 uint8 NHWC3 -> bf16 NHWC4 normalized ------------------------------
+__global__ __launch_bounds__(kBlock) void preprocess_kernel(const uint8_t* __restrict__ x,
+                                                            bf16* __restrict__ y, long long pix,
+                                                            float m0, float m1, float m2,
+                                                            float s0, float s1, float s2) {
+  // two pixels per thread: 6 input bytes -> 16 output bytes
+  const long long pairs = pix / 2;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < pairs;
+       i += (long long)gridDim.x * blockDim.x) {
+    const uint8_t* p = x + i * 6;
+    bf16x8 o;
+    o[0] = f2bf(((float)p[0] * (1.f / 255.f) - m0) * s0);
+    o[1] = f2bf(((float)p[1] * (1.f / 255.f) - m1) * s1);
+    o[2] = f2bf(((float)p[2] * (1.f / 255.f) - m2) * s2);
+    o[3] = f2bf(0.f);
+    o[4] = f2bf(((float)p[3] * (1.f / 255.f) - m0) * s0);
+    o[5] = f2bf(((float)p[4] * (1.f / 255.f) - m1) * s1);
+    o[6] = f2bf(((float)p[5] * (1.f / 255.f) - m2) * s2);
+    o[7] = f2bf(0.f);
+    *reinterpret_cast<bf16x8*>(y + i * 8) = o;
+  }
+}
+
+// ---- K4 fallback BN / affine ------------------------------------------------
+__global__ __launch_bounds__(kBlock) void bn_kernel(const bf16* __restrict__ x,
+                                                    bf16* __restrict__ y,
+                                                    const float* __restrict__ sc,
+                                                    const float* __restrict__ sh,
+                                                    long long total8, int C, int relu) {
+  const int C8 = C / 8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total8;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C8) * 8;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + i * 8);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float f = (float)v[j] * sc[c + j] + sh[c + j];
+      if (relu) f = fmaxf(f, 0.f);
+      o[j] = f2bf(f);
+    }
+    *reinterpret_cast<bf16x8*>(y + i * 8) = o;
+  }
+}
+
+}  // namespace
+}  // namespace kvedge
+
+using namespace kvedge;
+
+#define KV_CHECK_LAUNCH() return hipGetLastError() == hipSuccess ? 0 : -100
+
+extern "C" int kv_maxpool2d(const void* x, void* y, int N, int H, int W, int C, int ldx,
+                            int x_coff, int ldy, int y_coff, int k, int stride, int pad, int Ho,
+                            int Wo, hipStream_t s) {
+  if (C % 8 || ldx % 8 || x_coff % 8 || ldy % 8 || y_coff % 8) return -1;
+  const long long work = (long long)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(maxpool_kernel, dim3(grid_for(work)), dim3(kBlock), 0, s,
+                     (const bf16*)x, (bf16*)y, N, H, W, C, ldx, x_coff, ldy, y_coff, k, stride,
+                     pad, Ho, Wo);
+  KV_CHECK_LAUNCH();
+}
+
+extern "C" int kv_sppf_pool(void* buf, int N, int H, int W, int C, hipStream_t s) {
+  if (C % 8) return -1;
+  const long long work = (long long)N * H * W * (C / 8);
+  hipLaunchKernelGGL(sppf_kernel, dim3(grid_for(work)), dim3(kBlock), 0, s, (bf16*)buf, N, H, W,
+                     C);
+  KV_CHECK_LAUNCH();
+}
+
+extern "C" int kv_global_avgpool(const void* x, void* y, int N, int HW, int C, hipStream_t s) {
+  if (C % 8) return -1;
+  const long long work = (long long)N * (C / 8);
+  hipLaunchKernelGGL(avgpool_kernel, dim3(grid_for(work)), dim3(kBlock), 0, s, (const bf16*)x,
+                     (bf16*)y, N, HW, C);
+  KV_CHECK_LAUNCH();
+}
+
+extern "C" int kv_softmax_rows(const void* x, float* y, int64_t* argmax, int rows, int cols,
+                               hipStream_t s) {
+  const unsigned g = (unsigned)((rows + 3) / 4);
+  if (g == 0) return 0;
+  hipLaunchKernelGGL(softmax_kernel, dim3(g), dim3(kBlock), 0, s, (const bf16*)x, y, argmax,
+                     rows, cols);
+  KV_CHECK_LAUNCH();
+}
+
+extern "C" int kv_upsample2x(const void* x, void* y, int N, int H, int W, int C, int ldx,
+                             int x_coff, int ldy, int y_coff, hipStream_t s) {
+  if (C % 8 || ldx % 8 || x_coff % 8 || ldy % 8 || y_coff % 8) return -1;
+  const long long work = (long long)N * 4 * H * W * (C / 8);
+  hipLaunchKernelGGL(upsample2x_kernel, dim3(grid_for(work)), dim3(kBlock), 0, s,
+                     (const bf16*)x, (bf16*)y, N, H, W, C, ldx, x_coff, ldy, y_coff);
+  KV_CHECK_LAUNCH();
+}
+
+extern "C" int kv_synth_frames(uint8_t* y, int N, int H, int W, uint64_t seed, uint64_t step,
+                               hipStream_t s) {
+  const long long bytes = (long long)N * H * W * 3;
+  if (bytes % 8) return -1;
+  hipLaunchKernelGGL(synth_kernel, dim3(grid_for(bytes / 8)), dim3(kBlock), 0, s, y, bytes / 8,
+                     seed, step);
+  KV_CHECK_LAUNCH();
+}
+
+extern "C" int kv_synth_frames_dev(uint8_t* y, int N, int H, int W, uint64_t seed,
+                                   uint64_t* step, hipStream_t s) {
+  const long long bytes = (long long)N * H * W * 3;
+  if (bytes % 8) return -1;
+  hipLaunchKernelGGL(synth_dev_kernel, dim3(grid_for(bytes / 8)), dim3(kBlock), 0, s, y,
+                     bytes / 8, seed, step);
+  hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(1), 0, s, step);
+  KV_CHECK_LAUNCH();
+}
+
+extern "C" int kv_preprocess(const uint8_t* x, void* y, int N, int H, int W, const float* mean3,
+                             const float* inv_std3, hipStream_t s) {
+  const long long pix = (long long)N * H * W;
+  if (pix % 2) return -1;
+  hipLaunchKernelGGL(preprocess_kernel, dim3(grid_for(pix / 2)), dim3(kBlock), 0, s, x, (bf16*)y,
+                     pix, mean3[0], mean3[1], mean3[2], inv_std3[0], inv_std3[1], inv_std3[2]);
+  KV_CHECK_LAUNCH();
+}
+
+extern "C" int kv_batchnorm_nhwc(const void* x, void* y, const float* scale, const float* shift,
+                                 int64_t rows, int C, int relu, hipStream_t s) {
+  if (C % 8) return -1;
+  const long long total8 = rows * (long long)C / 8;
+  hipLaunchKernelGGL(bn_kernel, dim3(grid_for(total8)), dim3(kBlock), 0, s, (const bf16*)x,
+                     (bf16*)y, scale, shift, total8, C, relu);
+  KV_CHECK_LAUNCH();
+}

@@ -1,0 +1,241 @@
+// K9 YOLOv8 decode and K10 class-aware NMS for gfx950.  SURVEY.md §2.5, §7.3(2).
+//
+// Decode: one thread per anchor; DFL (softmax over 16 bins, expectation) for the
+// four box sides, dist2bbox against the anchor grid, class max (sigmoid is
+// monotonic so sigmoid(max logit) == max sigmoid).
+//
+// NMS: one workgroup per image (latency-bound by nature):
+//   1. compaction of candidates with score > conf into an LDS key array
+//      key = score_bits << 32 | ~index  (descending key = score desc, index asc)
+//   2. bitonic sort of up to 16384 keys in LDS (128 KiB of the CU's 160 KiB)
+//   3. greedy suppression in chunks of 64 candidates, ONE WAVE64 LANE PER BOX:
+//      each lane tests its box against the kept list, then the 64x64 in-chunk
+//      IoU matrix is resolved with 64-bit lane masks and readlane (no LDS), and
+//      survivors are appended in rank order with mbcnt.  Stops at max_det.
+#include "common.h"
+#include "kvedge_kernels.h"
+
+namespace kvedge {
+namespace {
+
+constexpr int kRegMax = 16;
+constexpr float kMaxWH = 7680.f;  // class offset for class-aware NMS
+constexpr int kMaxCand = 16384;
+
+__global__ __launch_bounds__(256) void yolo_decode_kernel(
+    const bf16* __restrict__ f0, const bf16* __restrict__ f1, const bf16* __restrict__ f2,
+    int h0, int w0, int h1, int w1, int h2, int w2, int s0, int s1, int s2, int N, int nc,
+    float* __restrict__ boxes, float* __restrict__ scores, int* __restrict__ cls) {
+  const int A0 = h0 * w0, A1 = h1 * w1, A2 = h2 * w2;
+  const int A = A0 + A1 + A2;
+  const long long total = (long long)N * A;
+  const int ch = 4 * kRegMax + nc;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int n = (int)(i / A);
+    int a = (int)(i % A);
+    const bf16* f;
+    int w, stride, local;
+    if (a < A0) {
+      f = f0; w = w0; stride = s0; local = a;
+      f += ((long long)n * A0 + local) * ch;
+    } else if (a < A0 + A1) {
+      f = f1; w = w1; stride = s1; local = a - A0;
+      f += ((long long)n * A1 + local) * ch;
+    } else {
+      f = f2; w = w2; stride = s2; local = a - A0 - A1;
+      f += ((long long)n * A2 + local) * ch;
+    }
+    const float ax = (float)(local % w) + 0.5f;
+    const float ay = (float)(local / w) + 0.5f;
+    float dist[4];
+#pragma unroll
+    for (int side = 0; side < 4; ++side) {
+      const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(f + side * 16);
+      const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(f + side * 16 + 8);
+      float x[16];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        x[j] = (float)v0[j];
+        x[8 + j] = (float)v1[j];
+      }
+      float mx = x[0];
+#pragma unroll
+      for (int j = 1; j < 16; ++j) mx = fmaxf(mx, x[j]);
+      float se = 0.f, sw = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float e = __expf(x[j] - mx);
+        se += e;
+        sw += e * (float)j;
+      }
+      dist[side] = sw / se;
+    }
+    const float sx = (float)stride;
+    float* b = boxes + i * 4;
+    b[0] = (ax - dist[0]) * sx;
+    b[1] = (ay - dist[1]) * sx;
+    b[2] = (ax + dist[2]) * sx;
+    b[3] = (ay + dist[3]) * sx;
+    float best = -INFINITY;
+    int bc = 0;
+    const bf16* fc = f + 4 * kRegMax;
+    for (int c = 0; c < nc; ++c) {
+      const float v = (float)fc[c];
+      if (v > best) { best = v; bc = c; }
+    }
+    scores[i] = sigmoidf_(best);
+    cls[i] = bc;
+  }
+}
+
+__device__ __forceinline__ float iou4(float ax1, float ay1, float ax2, float ay2, float bx1,
+                                      float by1, float bx2, float by2) {
+  const float iw = fmaxf(fminf(ax2, bx2) - fmaxf(ax1, bx1), 0.f);
+  const float ih = fmaxf(fminf(ay2, by2) - fmaxf(ay1, by1), 0.f);
+  const float inter = iw * ih;
+  const float aa = (ax2 - ax1) * (ay2 - ay1);
+  const float ab = (bx2 - bx1) * (by2 - by1);
+  return inter / fmaxf(aa + ab - inter, 1e-9f);
+}
+
+__global__ __launch_bounds__(256) void nms_kernel(const float* __restrict__ boxes,
+                                                  const float* __restrict__ scores,
+                                                  const int* __restrict__ cls, int A,
+                                                  float conf, float iou_thr, int max_det,
+                                                  float* __restrict__ out,
+                                                  int* __restrict__ count) {
+  __shared__ unsigned long long keys[kMaxCand];
+  __shared__ float kept[4 * 320];
+  __shared__ int ncand;
+  const int n = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (tid == 0) ncand = 0;
+  __syncthreads();
+  const float* sc = scores + (long long)n * A;
+  for (int a = tid; a < A; a += blockDim.x) {
+    const float s = sc[a];
+    if (s > conf) {
+      const int slot = atomicAdd(&ncand, 1);
+      if (slot < kMaxCand)
+        keys[slot] = ((unsigned long long)__float_as_uint(s) << 32) | (0xFFFFFFFFu - (unsigned)a);
+    }
+  }
+  __syncthreads();
+  const int cnt = min(ncand, kMaxCand);
+  int P = 64;
+  while (P < cnt) P <<= 1;
+  for (int i = cnt + tid; i < P; i += blockDim.x) keys[i] = 0ull;
+  __syncthreads();
+  // bitonic sort, descending
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < P; i += blockDim.x) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long a = keys[i], b = keys[ixj];
+          const bool desc = (i & k) == 0;
+          if (desc ? (a < b) : (a > b)) {
+            keys[i] = b;
+            keys[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  float* o = out + (long long)n * max_det * 6;
+  if (tid >= 64) {
+    return;  // greedy phase is one wave; no barriers follow
+  }
+  const int lane = tid;
+  const float* bx = boxes + (long long)n * A * 4;
+  const int* cl = cls + (long long)n * A;
+  int nk = 0;
+  for (int base = 0; base < cnt && nk < max_det; base += 64) {
+    const int ci = base + lane;
+    const bool valid = ci < cnt;
+    float x1 = 0, y1 = 0, x2 = 0, y2 = 0, s = 0;
+    int c = 0, idx = 0;
+    if (valid) {
+      const unsigned long long key = keys[ci];
+      idx = (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
+      s = __uint_as_float((unsigned)(key >> 32));
+      c = cl[idx];
+      const float off = (float)c * kMaxWH;
+      x1 = bx[idx * 4 + 0] + off;
+      y1 = bx[idx * 4 + 1] + off;
+      x2 = bx[idx * 4 + 2] + off;
+      y2 = bx[idx * 4 + 3] + off;
+    }
+    bool alive = valid;
+    for (int j = 0; j < nk && alive; ++j) {
+      if (iou4(x1, y1, x2, y2, kept[4 * j], kept[4 * j + 1], kept[4 * j + 2], kept[4 * j + 3]) >
+          iou_thr)
+        alive = false;
+    }
+    // row mask: which LATER lanes of this chunk this lane's box suppresses
+    unsigned long long row = 0ull;
+    for (int j = 0; j < 64; ++j) {
+      const float bx1 = __shfl(x1, j, 64), by1 = __shfl(y1, j, 64);
+      const float bx2 = __shfl(x2, j, 64), by2 = __shfl(y2, j, 64);
+      if (j > lane && iou4(x1, y1, x2, y2, bx1, by1, bx2, by2) > iou_thr) row |= 1ull << j;
+    }
+    unsigned long long live = __ballot(alive);
+    for (int j = 0; j < 64; ++j) {
+      const unsigned long long rj =
+          ((unsigned long long)__shfl((unsigned)(row >> 32), j, 64) << 32) |
+          (unsigned long long)__shfl((unsigned)row, j, 64);
+      if ((live >> j) & 1ull) live &= ~rj;
+    }
+    const bool keep = (live >> lane) & 1ull;
+    const int rank = __popcll(live & ((1ull << lane) - 1ull));
+    const int pos = nk + rank;
+    if (keep && pos < max_det) {
+      kept[4 * pos] = x1;
+      kept[4 * pos + 1] = y1;
+      kept[4 * pos + 2] = x2;
+      kept[4 * pos + 3] = y2;
+      const float off = (float)c * kMaxWH;
+      float* r = o + pos * 6;
+      r[0] = x1 - off;
+      r[1] = y1 - off;
+      r[2] = x2 - off;
+      r[3] = y2 - off;
+      r[4] = s;
+      r[5] = (float)c;
+    }
+    nk = min(nk + (int)__popcll(live), max_det);
+    __builtin_amdgcn_wave_barrier();
+  }
+  for (int i = nk * 6 + lane; i < max_det * 6; i += 64) o[i] = 0.f;
+  if (lane == 0) count[n] = nk;
+}
+
+}  // namespace
+}  // namespace kvedge
+
+using namespace kvedge;
+
+extern "C" int kv_yolo_decode(const void* f0, const void* f1, const void* f2, int h0, int w0,
+                              int h1, int w1, int h2, int w2, int s0, int s1, int s2, int N,
+                              int nc, float* boxes, float* scores, int* cls, hipStream_t s) {
+  if (nc % 8) return -1;
+  const long long total = (long long)N * (h0 * w0 + h1 * w1 + h2 * w2);
+  long long g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(yolo_decode_kernel, dim3((unsigned)g), dim3(256), 0, s, (const bf16*)f0,
+                     (const bf16*)f1, (const bf16*)f2, h0, w0, h1, w1, h2, w2, s0, s1, s2, N, nc,
+                     boxes, scores, cls);
+  return hipGetLastError() == hipSuccess ? 0 : -100;
+}
+
+extern "C" int kv_nms(const float* boxes, const float* scores, const int* cls, int N, int A,
+                      float conf_thres, float iou_thres, int max_det, float* out, int* count,
+                      hipStream_t s) {
+  if (max_det > 300 || max_det <= 0 || A > kMaxCand) return -1;
+  if (N <= 0) return 0;
+  hipLaunchKernelGGL(nms_kernel, dim3(N), dim3(256), 0, s, boxes, scores, cls, A, conf_thres,
+                     iou_thres, max_det, out, count);
+  return hipGetLastError() == hipSuccess ? 0 : -100;
+}

@@ -1,0 +1,121 @@
+"""N16 inference engine: static shapes, on-device synthetic frames, one hipGraph per forward.
+
+The whole edge-module step (K11 frame synthesis -> preprocess -> model -> softmax/
+top-1, or -> YOLO decode -> NMS) is captured once with ``torch.cuda.CUDAGraph``
+(which IS hipGraph on ROCm) and replayed per batch: launch overhead of ~60
+kernels collapses to one graph launch (MI355X_MICROARCH.md price row
+"graph-replay-floor").  The frame counter lives in device memory and is bumped
+inside the graph, so every replay sees fresh frames.
+
+On CPU the same engine runs the reference path eagerly (tests, no GPU).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+import torch
+
+from .. import ops
+
+
+@dataclass
+class StepTimes:
+    count: int = 0
+    total_s: float = 0.0
+    samples_ms: List[float] = field(default_factory=list)
+
+    def add(self, dt_s: float, keep: int = 4096):
+        self.count += 1
+        self.total_s += dt_s
+        if len(self.samples_ms) < keep:
+            self.samples_ms.append(dt_s * 1e3)
+
+    def percentile(self, q: float) -> float:
+        if not self.samples_ms:
+            return 0.0
+        s = sorted(self.samples_ms)
+        i = min(len(s) - 1, max(0, int(round(q / 100.0 * (len(s) - 1)))))
+        return s[i]
+
+
+class InferenceEngine:
+    """Runs ``model(frames_u8) -> outputs`` on static-shape batches.
+
+    model: any callable taking a uint8 NHWC3 frame batch (KvResNet50, KvYoloV8n).
+    """
+
+    def __init__(self, model: Callable, batch: int, image_size: int, device="cuda",
+                 seed: int = 0, use_graph: bool = True):
+        self.model = model
+        self.batch = batch
+        self.hw = image_size
+        self.device = torch.device(device)
+        self.seed = seed
+        self.use_graph = use_graph and self.device.type == "cuda"
+        self.frames = torch.empty(batch, image_size, image_size, 3, dtype=torch.uint8,
+                                  device=self.device)
+        self.step_ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.outputs = None
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.times = StepTimes()
+
+    # one full edge-module step: synthesize frames, run the model
+    def _step(self):
+        ops.synth_frames(self.frames, self.seed, self.step_ctr)
+        self.outputs = self.model(self.frames)
+        return self.outputs
+
+    def prepare(self, warmup: int = 2):
+        """Warm up (kernel code objects load, allocator pools fill), then capture."""
+        if not self.use_graph:
+            for _ in range(warmup):
+                self._step()
+            return self
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(max(1, warmup)):
+                self._step()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._step()
+        torch.cuda.synchronize(self.device)
+        return self
+
+    def run(self):
+        """Launch one step (async on GPU)."""
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._step()
+        return self.outputs
+
+    def run_timed(self, n: int) -> float:
+        """Run n steps, return elapsed seconds (device-synchronised)."""
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            self.run()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        dt = time.perf_counter() - t0
+        return dt
+
+    def measure_latency(self, n: int) -> StepTimes:
+        """Per-step latency with a sync after every step (p50/p99 telemetry)."""
+        st = StepTimes()
+        for _ in range(n):
+            dt = self.run_timed(1)
+            st.add(dt)
+        return st
+
+    def set_frames(self, frames_u8: torch.Tensor):
+        """Feed real frames instead of synthetic (disables the synthetic step)."""
+        self.frames.copy_(frames_u8)
+        self.outputs = self.model(self.frames)
+        return self.outputs

@@ -1,0 +1,87 @@
+"""Model-building blocks shared by ResNet-50 and YOLOv8n.
+
+A model is defined twice, on purpose:
+  * a plain ``torch.nn`` NCHW fp32 reference (random-init, seeded) that is the
+    numerics oracle and the source of the weights;
+  * a *deployed* form: BN folded into conv weight/bias (K4 one-shot fold), weights
+    packed [Cout, Kpad] bf16 for the implicit-GEMM kernel, activations NHWC bf16.
+The deployed forward calls only :mod:`kvedge_amd.ops` (HIP kernels on GPU).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..ops import ConvSpec
+
+
+def fold_bn(conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d]):
+    """Return (weight OIHW fp32, bias fp32) of conv followed by eval-mode BN."""
+    w = conv.weight.detach().float()
+    b = conv.bias.detach().float() if conv.bias is not None else torch.zeros(w.shape[0])
+    if bn is None:
+        return w.clone(), b.clone()
+    inv = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
+    wf = w * inv[:, None, None, None]
+    bf = (b - bn.running_mean.detach().float()) * inv + bn.bias.detach().float()
+    return wf, bf
+
+
+@dataclass
+class DeployedConv:
+    """A conv ready for the kernel: spec + packed bf16 weight + fp32 bias."""
+    spec: ConvSpec
+    w: torch.Tensor
+    b: torch.Tensor
+
+    @staticmethod
+    def from_modules(conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d], act: int,
+                     device="cpu") -> "DeployedConv":
+        wf, bf = fold_bn(conv, bn)
+        cout, cin, kh, kw = wf.shape
+        assert kh == kw and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
+        spec = ConvSpec.auto(cin, cout, kh, conv.stride[0], conv.padding[0], act)
+        return DeployedConv(spec, ops.pack_conv_weight(wf, spec).to(device),
+                            bf.contiguous().to(device))
+
+    def to(self, device) -> "DeployedConv":
+        return DeployedConv(self.spec, self.w.to(device), self.b.to(device))
+
+    def __call__(self, x, res=None, out=None, x_coff=0, y_coff=0, r_coff=0, tile=-1):
+        return ops.conv2d(x, self.spec, self.w, self.b, res=res, out=out, x_coff=x_coff,
+                          y_coff=y_coff, r_coff=r_coff, tile=tile)
+
+    @property
+    def flops_per_pixel(self) -> int:
+        s = self.spec
+        return 2 * s.kh * s.kw * s.cin * s.cout
+
+
+@torch.no_grad()
+def calibrate_bn(model: nn.Module, batches, momentum: Optional[float] = None) -> None:
+    """Set BN running stats from synthetic batches so a random-init network is
+    well conditioned (activations O(1) through all layers), like a trained one.
+    Uses cumulative averaging (momentum=None)."""
+    bns = [m for m in model.modules() if isinstance(m, nn.BatchNorm2d)]
+    saved = [(m.momentum) for m in bns]
+    for m in bns:
+        m.reset_running_stats()
+        m.momentum = momentum
+    model.train()
+    for x in batches:
+        model(x)
+    model.eval()
+    for m, mo in zip(bns, saved):
+        m.momentum = mo
+
+
+def frames_to_nchw(frames_u8: torch.Tensor, mean=ops.IMAGENET_MEAN,
+                   std=ops.IMAGENET_STD) -> torch.Tensor:
+    """uint8 NHWC3 frames -> normalized fp32 NCHW (reference path)."""
+    x = frames_u8.float() / 255.0
+    x = (x - torch.tensor(mean, device=x.device)) / torch.tensor(std, device=x.device)
+    return x.permute(0, 3, 1, 2).contiguous()

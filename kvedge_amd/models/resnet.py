@@ -1,0 +1,192 @@
+"""ResNet-50 v1.5 (torchvision layout) — reference NCHW module and deployed NHWC bf16 form.
+
+North-star flagship model (BASELINE.json config 2/3).  The
+reference repository has no model code; this is a new component.  Weights are
+random-init with a fixed seed (no checkpoints / no network), optionally with BN
+statistics calibrated on synthetic frames so activations stay well scaled.
+
+Deployed forward (all HIP kernels on GPU):
+  frames u8 NHWC3 -> K12 preprocess (bf16 NHWC4) -> K2 stem 7x7/2 (+BN+ReLU fused)
+  -> K5 maxpool 3x3/2 -> 16 bottlenecks of K3/K2 convs with bias+residual+ReLU
+  fused into the conv epilogue -> K6 global avgpool -> K1 FC GEMM -> K7 softmax+argmax.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from .layers import DeployedConv, calibrate_bn, frames_to_nchw
+
+ACT_NONE, ACT_RELU = ops.ACT_NONE, ops.ACT_RELU
+
+
+# ---------------------------------------------------------------------------
+# reference (NCHW fp32)
+# ---------------------------------------------------------------------------
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin: int, width: int, stride: int):
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride, 1, bias=False)  # v1.5: stride on 3x3
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(cout)
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False),
+                                            nn.BatchNorm2d(cout))
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        y = F.relu(self.bn1(self.conv1(x)))
+        y = F.relu(self.bn2(self.conv2(y)))
+        y = self.bn3(self.conv3(y))
+        return F.relu(y + idt)
+
+
+class ResNet50Ref(nn.Module):
+    layers_cfg = ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2))
+
+    def __init__(self, num_classes: int = 1000):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        blocks: List[nn.Module] = []
+        cin = 64
+        for width, n, stride in self.layers_cfg:
+            for i in range(n):
+                blocks.append(Bottleneck(cin, width, stride if i == 0 else 1))
+                cin = width * 4
+        self.blocks = nn.Sequential(*blocks)
+        self.fc = nn.Linear(2048, num_classes)
+        self.num_classes = num_classes
+
+    def forward(self, x):
+        x = F.relu(self.bn1(self.conv1(x)))
+        x = F.max_pool2d(x, 3, 2, 1)
+        x = self.blocks(x)
+        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        return self.fc(x)
+
+
+def init_resnet50(seed: int = 0, num_classes: int = 1000, calibrate: bool = True,
+                  calib_batch: int = 4, calib_hw: int = 224) -> ResNet50Ref:
+    """Seeded random init (torchvision scheme) + optional BN calibration on synthetic frames."""
+    g = torch.Generator().manual_seed(seed)
+    m = ResNet50Ref(num_classes)
+    for mod in m.modules():
+        if isinstance(mod, nn.Conv2d):
+            fan_out = mod.out_channels * mod.kernel_size[0] * mod.kernel_size[1]
+            with torch.no_grad():
+                mod.weight.normal_(0.0, (2.0 / fan_out) ** 0.5, generator=g)
+        elif isinstance(mod, nn.BatchNorm2d):
+            nn.init.ones_(mod.weight)
+            nn.init.zeros_(mod.bias)
+        elif isinstance(mod, nn.Linear):
+            bound = 1.0 / mod.in_features ** 0.5
+            with torch.no_grad():
+                mod.weight.uniform_(-bound, bound, generator=g)
+                mod.bias.uniform_(-bound, bound, generator=g)
+    if calibrate:
+        frames = torch.randint(0, 256, (calib_batch, calib_hw, calib_hw, 3), generator=g,
+                               dtype=torch.uint8)
+        calibrate_bn(m, [frames_to_nchw(frames)])
+    m.eval()
+    return m
+
+
+# ---------------------------------------------------------------------------
+# deployed (NHWC bf16, HIP kernels)
+# ---------------------------------------------------------------------------
+class DeployedBottleneck:
+    def __init__(self, b: Bottleneck, device):
+        self.c1 = DeployedConv.from_modules(b.conv1, b.bn1, ACT_RELU, device)
+        self.c2 = DeployedConv.from_modules(b.conv2, b.bn2, ACT_RELU, device)
+        # conv3: bias + residual + ReLU fused in the epilogue
+        self.c3 = DeployedConv.from_modules(b.conv3, b.bn3, ACT_RELU, device)
+        self.down = None
+        if b.downsample is not None:
+            self.down = DeployedConv.from_modules(b.downsample[0], b.downsample[1], ACT_NONE,
+                                                  device)
+
+    def __call__(self, x):
+        idt = x if self.down is None else self.down(x)
+        y = self.c1(x)
+        y = self.c2(y)
+        return self.c3(y, res=idt)
+
+    def convs(self):
+        return [c for c in (self.c1, self.c2, self.c3, self.down) if c is not None]
+
+
+class KvResNet50:
+    """Deployed ResNet-50: frames (u8 NHWC3) -> (probs fp32 [B,C], top1 int64 [B])."""
+
+    image_size = 224
+
+    def __init__(self, ref: ResNet50Ref, device="cuda"):
+        self.device = torch.device(device)
+        self.num_classes = ref.num_classes
+        self.stem = DeployedConv.from_modules(ref.conv1, ref.bn1, ACT_RELU, self.device)
+        self.blocks = [DeployedBottleneck(b, self.device) for b in ref.blocks]
+        fcw = ref.fc.weight.detach().float()[:, :, None, None]
+        fc_conv = nn.Conv2d(2048, ref.num_classes, 1, bias=True)
+        with torch.no_grad():
+            fc_conv.weight.copy_(fcw)
+            fc_conv.bias.copy_(ref.fc.bias.detach())
+        self.fc = DeployedConv.from_modules(fc_conv, None, ACT_NONE, self.device)
+
+    @staticmethod
+    def build(seed: int = 0, device="cuda", calibrate: bool = True) -> "KvResNet50":
+        return KvResNet50(init_resnet50(seed, calibrate=calibrate), device)
+
+    def convs(self) -> List[DeployedConv]:
+        out = [self.stem]
+        for b in self.blocks:
+            out += b.convs()
+        return out + [self.fc]
+
+    def flops_per_image(self, hw: int = 224) -> int:
+        """MAC-based FLOPs (2*MAC) of all convs + FC at input size hw."""
+        total = 0
+        h = hw
+        # walk spatial sizes
+        h = self.stem.spec.out_hw(h, h)[0]
+        total += self.stem.flops_per_pixel * h * h
+        h = (h + 2 - 3) // 2 + 1  # maxpool
+        for b in self.blocks:
+            total += b.c1.flops_per_pixel * h * h
+            h2 = b.c2.spec.out_hw(h, h)[0]
+            total += b.c2.flops_per_pixel * h2 * h2 + b.c3.flops_per_pixel * h2 * h2
+            if b.down is not None:
+                total += b.down.flops_per_pixel * h2 * h2
+            h = h2
+        return total + self.fc.flops_per_pixel
+
+    def features(self, x: torch.Tensor) -> torch.Tensor:
+        """x: preprocessed bf16 NHWC4 -> final feature map [B,7,7,2048] bf16."""
+        x = self.stem(x)
+        x = ops.maxpool2d(x, 3, 2, 1)
+        for b in self.blocks:
+            x = b(x)
+        return x
+
+    def logits(self, x: torch.Tensor) -> torch.Tensor:
+        f = self.features(x)
+        B = f.shape[0]
+        pooled = ops.global_avgpool(f).view(B, 1, 1, 2048)
+        return self.fc(pooled).view(B, self.num_classes)
+
+    def __call__(self, frames_u8: torch.Tensor, out: Optional[dict] = None):
+        x = ops.preprocess(frames_u8)
+        lg = self.logits(x)
+        probs, top1 = ops.softmax_rows(lg)
+        return probs, top1

@@ -1,0 +1,319 @@
+"""kvedge_amd.ops — Python face of the gfx950 HIP kernel library.
+
+Contract
+--------
+* GPU tensors ALWAYS go to the hand-written HIP kernels in ``kvedge_amd/_C.so``.
+  If the extension is missing on a GPU box the call raises — there is no silent
+  eager fallback on the device path.
+* CPU tensors go to :mod:`kvedge_amd.ops.reference`, a plain-PyTorch fp32
+  implementation of the *same* semantics (NHWC, packed weights, channel slices).
+  That path exists so the model/engine/module plumbing is testable without a GPU
+  and doubles as the numerics oracle for the kernel tests.
+
+Layout conventions (shared by kernels and reference):
+* activations: NHWC bf16, viewed as ``[N, H, W, ld]``; an op may read/write a
+  channel slice ``[coff, coff + C)`` of a wider buffer (concat-free YOLO neck).
+* conv weights: packed ``[Cout, Kpad]`` bf16, k-order ``(r, s, c)``; BN folded.
+  Stem mode (mode 2): input padded to 4 channels, KW padded to even,
+  k-order ``(r, s_padded, c4)`` so that each 8-element MFMA k-chunk is two
+  adjacent pixels (16 contiguous bytes).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import torch
+
+from . import reference as _ref
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C.so")
+_loaded = False
+_load_error: Optional[str] = None
+
+ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
+MODE_GENERAL, MODE_GEMM, MODE_STEM = 0, 1, 2
+BK = 64
+
+
+def load(build_if_missing: bool = False) -> bool:
+    """Load the native op library once. Returns True when available."""
+    global _loaded, _load_error
+    if _loaded:
+        return True
+    if not os.path.exists(_LIB_PATH) and build_if_missing:
+        from .. import _build
+
+        _build.build()
+    if not os.path.exists(_LIB_PATH):
+        _load_error = f"{_LIB_PATH} not built (run `python -m kvedge_amd._build`)"
+        return False
+    try:
+        torch.ops.load_library(_LIB_PATH)
+    except Exception as e:  # pragma: no cover - depends on build state
+        _load_error = f"failed to load {_LIB_PATH}: {e}"
+        return False
+    _check_single_hip_runtime()
+    _loaded = True
+    return True
+
+
+def _check_single_hip_runtime() -> None:
+    """Two libamdhip64 copies in one process (torch's + system) would split HIP state."""
+    try:
+        with open("/proc/self/maps") as f:
+            libs = {ln.split()[-1] for ln in f if "libamdhip64" in ln}
+    except OSError:
+        return
+    real = {os.path.realpath(p) for p in libs}
+    if len(real) > 1:
+        raise RuntimeError(f"kvedge: multiple HIP runtimes loaded: {sorted(real)}")
+
+
+def native_available() -> bool:
+    return load()
+
+
+def library_path() -> str:
+    return _LIB_PATH
+
+
+def _native():
+    if not load():
+        raise RuntimeError(
+            "kvedge_amd native kernels are required for GPU tensors but unavailable: "
+            f"{_load_error}")
+    return torch.ops.kvedge
+
+
+# ---------------------------------------------------------------------------
+# conv spec + weight packing
+# ---------------------------------------------------------------------------
+@dataclass
+class ConvSpec:
+    cin: int
+    cout: int
+    kh: int
+    kw: int
+    stride: int = 1
+    pad: int = 0
+    act: int = ACT_NONE
+    mode: int = MODE_GENERAL
+
+    @property
+    def cin_eff(self) -> int:
+        return 4 if self.mode == MODE_STEM else self.cin
+
+    @property
+    def kwp(self) -> int:
+        return (self.kw + 1) // 2 * 2
+
+    @property
+    def K(self) -> int:
+        if self.mode == MODE_STEM:
+            return self.kh * self.kwp * 4
+        return self.kh * self.kw * self.cin
+
+    @property
+    def Kpad(self) -> int:
+        return (self.K + BK - 1) // BK * BK
+
+    def out_hw(self, h: int, w: int):
+        return ((h + 2 * self.pad - self.kh) // self.stride + 1,
+                (w + 2 * self.pad - self.kw) // self.stride + 1)
+
+    @staticmethod
+    def auto(cin, cout, k, stride=1, pad=None, act=ACT_NONE) -> "ConvSpec":
+        if pad is None:
+            pad = k // 2
+        if cin < 8:
+            mode = MODE_STEM
+        elif k == 1 and stride == 1 and pad == 0:
+            mode = MODE_GEMM
+        else:
+            mode = MODE_GENERAL
+        return ConvSpec(cin, cout, k, k, stride, pad, act, mode)
+
+
+def pack_conv_weight(w: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
+    """torch OIHW fp32 -> packed [Cout, Kpad] bf16 (k-order (r, s, c))."""
+    assert w.shape == (spec.cout, spec.cin, spec.kh, spec.kw), (w.shape, spec)
+    w = w.detach().float()
+    if spec.mode == MODE_STEM:
+        wp = torch.zeros(spec.cout, spec.kh, spec.kwp, 4, dtype=torch.float32, device=w.device)
+        wp[:, :, :spec.kw, :spec.cin] = w.permute(0, 2, 3, 1)
+        flat = wp.reshape(spec.cout, -1)
+    else:
+        flat = w.permute(0, 2, 3, 1).reshape(spec.cout, -1)
+    out = torch.zeros(spec.cout, spec.Kpad, dtype=torch.float32, device=w.device)
+    out[:, :flat.shape[1]] = flat
+    return out.to(torch.bfloat16).contiguous()
+
+
+def unpack_conv_weight(wp: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
+    """Inverse of :func:`pack_conv_weight` -> OIHW fp32 (bf16-rounded values)."""
+    wf = wp.float()[:, :spec.K]
+    if spec.mode == MODE_STEM:
+        w4 = wf.reshape(spec.cout, spec.kh, spec.kwp, 4)[:, :, :spec.kw, :spec.cin]
+        return w4.permute(0, 3, 1, 2).contiguous()
+    return wf.reshape(spec.cout, spec.kh, spec.kw, spec.cin).permute(0, 3, 1, 2).contiguous()
+
+
+# ---------------------------------------------------------------------------
+# ops
+# ---------------------------------------------------------------------------
+def conv2d(x: torch.Tensor, spec: ConvSpec, w: torch.Tensor, bias: Optional[torch.Tensor],
+           res: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+           x_coff: int = 0, y_coff: int = 0, r_coff: int = 0, tile: int = -1) -> torch.Tensor:
+    """Fused conv + bias (+ residual) (+ act).  x: [N,H,W,ldx] bf16 -> out [N,Ho,Wo,ldy]."""
+    N, H, W, ldx = x.shape
+    Ho, Wo = spec.out_hw(H, W)
+    if out is None:
+        out = torch.empty(N, Ho, Wo, spec.cout, dtype=torch.bfloat16, device=x.device)
+    assert out.shape[:3] == (N, Ho, Wo), (out.shape, (N, Ho, Wo))
+    ldy = out.shape[3]
+    ldr = res.shape[-1] if res is not None else 0
+    if x.is_cuda:
+        _native().conv(x, w, bias, res, out, N, H, W, spec.cin_eff, ldx, x_coff, Ho, Wo,
+                       spec.cout, spec.kh, spec.kw, spec.stride, spec.pad, spec.K, ldy, y_coff,
+                       ldr, r_coff, spec.act, spec.mode, tile)
+    else:
+        _ref.conv2d(x, spec, w, bias, res, out, x_coff, y_coff, r_coff)
+    return out
+
+
+def maxpool2d(x: torch.Tensor, k: int, stride: int, pad: int, out: Optional[torch.Tensor] = None,
+              C: Optional[int] = None, x_coff: int = 0, y_coff: int = 0) -> torch.Tensor:
+    N, H, W, ldx = x.shape
+    C = C or (ldx - x_coff)
+    Ho = (H + 2 * pad - k) // stride + 1
+    Wo = (W + 2 * pad - k) // stride + 1
+    if out is None:
+        out = torch.empty(N, Ho, Wo, C, dtype=x.dtype, device=x.device)
+    if x.is_cuda:
+        _native().maxpool2d(x, out, N, H, W, C, ldx, x_coff, out.shape[3], y_coff, k, stride, pad,
+                            Ho, Wo)
+    else:
+        _ref.maxpool2d(x[..., x_coff:x_coff + C], out, C, k, stride, pad, y_coff)
+    return out
+
+
+def sppf_pool(buf: torch.Tensor, C: int) -> torch.Tensor:
+    """buf [N,H,W,4C] with x in slice 0 -> fills slices 1..3 with mp5/mp9/mp13."""
+    N, H, W, ld = buf.shape
+    assert ld == 4 * C
+    if buf.is_cuda:
+        _native().sppf_pool(buf, N, H, W, C)
+    else:
+        _ref.sppf_pool(buf, C)
+    return buf
+
+
+def global_avgpool(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    N, H, W, C = x.shape
+    if out is None:
+        out = torch.empty(N, C, dtype=x.dtype, device=x.device)
+    if x.is_cuda:
+        _native().global_avgpool(x, out, N, H * W, C)
+    else:
+        out.copy_(x.float().mean(dim=(1, 2)).to(out.dtype))
+    return out
+
+
+def softmax_rows(x: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 argmax: Optional[torch.Tensor] = None):
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    if argmax is None:
+        argmax = torch.empty(x.shape[0], dtype=torch.int64, device=x.device)
+    if x.is_cuda:
+        _native().softmax_rows(x, out, argmax)
+    else:
+        xf = x.float()
+        out.copy_(torch.softmax(xf, dim=1))
+        argmax.copy_(xf.argmax(dim=1))
+    return out, argmax
+
+
+def upsample2x(x: torch.Tensor, out: torch.Tensor, C: Optional[int] = None, x_coff: int = 0,
+               y_coff: int = 0):
+    N, H, W, ldx = x.shape
+    C = C or (ldx - x_coff)
+    if x.is_cuda:
+        _native().upsample2x(x, out, N, H, W, C, ldx, x_coff, out.shape[3], y_coff)
+    else:
+        up = x[..., x_coff:x_coff + C].repeat_interleave(2, dim=1).repeat_interleave(2, dim=2)
+        out[..., y_coff:y_coff + C] = up
+    return out
+
+
+def yolo_decode(feats: Sequence[torch.Tensor], strides: Sequence[int], nc: int,
+                boxes=None, scores=None, cls=None):
+    f0, f1, f2 = feats
+    N = f0.shape[0]
+    hw = [(f.shape[1], f.shape[2]) for f in feats]
+    A = sum(h * w for h, w in hw)
+    dev = f0.device
+    if boxes is None:
+        boxes = torch.empty(N, A, 4, dtype=torch.float32, device=dev)
+        scores = torch.empty(N, A, dtype=torch.float32, device=dev)
+        cls = torch.empty(N, A, dtype=torch.int32, device=dev)
+    if f0.is_cuda:
+        _native().yolo_decode(f0, f1, f2, hw[0][0], hw[0][1], hw[1][0], hw[1][1], hw[2][0],
+                              hw[2][1], strides[0], strides[1], strides[2], nc, boxes, scores, cls)
+    else:
+        _ref.yolo_decode(feats, strides, nc, boxes, scores, cls)
+    return boxes, scores, cls
+
+
+def nms(boxes, scores, cls, conf: float = 0.25, iou: float = 0.7, max_det: int = 300,
+        out=None, count=None):
+    N = scores.shape[0]
+    if out is None:
+        out = torch.empty(N, max_det, 6, dtype=torch.float32, device=scores.device)
+        count = torch.empty(N, dtype=torch.int32, device=scores.device)
+    if scores.is_cuda:
+        _native().nms(boxes, scores, cls, conf, iou, max_det, out, count)
+    else:
+        _ref.nms(boxes, scores, cls, conf, iou, max_det, out, count)
+    return out, count
+
+
+def synth_frames(out: torch.Tensor, seed: int, step) -> torch.Tensor:
+    """On-device synthetic uint8 NHWC3 frames.  ``step`` int or a device int64[1] counter."""
+    if out.is_cuda:
+        if isinstance(step, torch.Tensor):
+            _native().synth_frames_dev(out, step, seed)
+        else:
+            _native().synth_frames(out, seed, int(step))
+    else:
+        _ref.synth_frames(out, seed, step)
+    return out
+
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def preprocess(x: torch.Tensor, out: Optional[torch.Tensor] = None, mean=IMAGENET_MEAN,
+               std=IMAGENET_STD) -> torch.Tensor:
+    N, H, W, _ = x.shape
+    if out is None:
+        out = torch.empty(N, H, W, 4, dtype=torch.bfloat16, device=x.device)
+    if x.is_cuda:
+        _native().preprocess(x, out, list(mean), list(std))
+    else:
+        _ref.preprocess(x, out, mean, std)
+    return out
+
+
+def batchnorm_nhwc(x, scale, shift, relu=False, out=None):
+    if out is None:
+        out = torch.empty_like(x)
+    if x.is_cuda:
+        _native().batchnorm_nhwc(x, out, scale, shift, relu)
+    else:
+        y = x.float() * scale + shift
+        out.copy_((y.clamp_min(0) if relu else y).to(out.dtype))
+    return out

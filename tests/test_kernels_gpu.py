@@ -1,0 +1,182 @@
+"""Numerics of every HIP kernel vs the plain-PyTorch fp32 reference (SURVEY.md §4 T-kernel).
+
+Each test builds inputs on the CPU, runs the reference path (kvedge_amd.ops.reference)
+and the gfx950 kernel on the same bf16 inputs, and compares.  The GPU path must be
+the native library: tests assert it is loaded (no silent fallback).
+"""
+import pytest
+import torch
+
+from kvedge_amd import ops
+from kvedge_amd.ops import ConvSpec
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    assert ops.load(), "native kvedge library must be loaded on the GPU box"
+
+
+def _rand(shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).to(torch.bfloat16)
+
+
+def _conv_case(N, H, W, cin, cout, k, stride, pad, act, res=False, ldx_extra=0, x_coff=0,
+               ldy_extra=0, y_coff=0, tile=-1, seed=0):
+    spec = ConvSpec.auto(cin, cout, k, stride, pad, act)
+    cin_eff = spec.cin_eff
+    ldx = cin_eff + ldx_extra
+    x = _rand((N, H, W, ldx), seed)
+    if spec.mode == ops.MODE_STEM:
+        x[..., 3:] = 0
+    g = torch.Generator().manual_seed(seed + 1)
+    w = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    wp = ops.pack_conv_weight(w, spec)
+    Ho, Wo = spec.out_hw(H, W)
+    ldy = cout + ldy_extra
+    r = _rand((N, Ho, Wo, cout), seed + 2) if res else None
+    out_ref = torch.zeros(N, Ho, Wo, ldy, dtype=torch.bfloat16)
+    ops.conv2d(x, spec, wp, b, res=r, out=out_ref, x_coff=x_coff, y_coff=y_coff)
+    out_gpu = torch.zeros(N, Ho, Wo, ldy, dtype=torch.bfloat16, device="cuda")
+    ops.conv2d(x.cuda(), spec, wp.cuda(), b.cuda(), res=None if r is None else r.cuda(),
+               out=out_gpu, x_coff=x_coff, y_coff=y_coff, tile=tile)
+    torch.cuda.synchronize()
+    og = out_gpu.cpu().float()
+    orf = out_ref.float()
+    err = (og - orf).abs().max().item()
+    scale = orf.abs().max().item() + 1e-6
+    # untouched channels outside the output slice must stay zero
+    if ldy_extra:
+        mask = torch.ones(ldy, dtype=torch.bool)
+        mask[y_coff:y_coff + cout] = False
+        assert og[..., mask].abs().max().item() == 0.0
+    return err, scale
+
+
+@pytest.mark.parametrize("case", [
+    # (N, H, W, cin, cout, k, stride, pad, act)
+    (2, 56, 56, 64, 64, 1, 1, 0, ops.ACT_RELU),      # 1x1 GEMM mode
+    (2, 56, 56, 64, 256, 1, 1, 0, ops.ACT_NONE),
+    (2, 56, 56, 64, 64, 3, 1, 1, ops.ACT_RELU),      # 3x3 general
+    (2, 28, 28, 128, 128, 3, 2, 1, ops.ACT_RELU),    # 3x3 stride 2
+    (2, 56, 56, 256, 512, 1, 2, 0, ops.ACT_NONE),    # 1x1 stride-2 downsample
+    (1, 7, 7, 512, 512, 3, 1, 1, ops.ACT_RELU),      # tiny spatial tail
+    (2, 64, 64, 3, 16, 3, 2, 1, ops.ACT_SILU),       # YOLO stem (stem mode, KW=3)
+    (2, 224, 224, 3, 64, 7, 2, 3, ops.ACT_RELU),     # ResNet stem (stem mode, KW=7)
+    (2, 20, 20, 48, 32, 1, 1, 0, ops.ACT_SILU),      # Cin not multiple of 64
+    (2, 40, 40, 80, 80, 3, 1, 1, ops.ACT_SILU),      # Cin=80 (YOLO cls branch)
+    (2, 20, 20, 16, 16, 3, 1, 1, ops.ACT_SILU),      # Cin=16: 4 taps per 64-slab
+    (3, 1, 1, 2048, 1000, 1, 1, 0, ops.ACT_NONE),    # FC as GEMM, odd M
+])
+def test_conv_vs_reference(case):
+    err, scale = _conv_case(*case)
+    assert err <= 0.02 * scale + 0.02, (case, err, scale)
+
+
+def test_conv_residual_and_slices():
+    err, scale = _conv_case(2, 28, 28, 64, 128, 3, 1, 1, ops.ACT_RELU, res=True, ldx_extra=64,
+                            x_coff=32, ldy_extra=64, y_coff=32)
+    assert err <= 0.02 * scale + 0.02
+
+
+@pytest.mark.parametrize("tile", list(range(6)))
+def test_conv_every_tile(tile):
+    err, scale = _conv_case(2, 30, 30, 128, 192, 3, 1, 1, ops.ACT_RELU, res=True, tile=tile)
+    assert err <= 0.02 * scale + 0.02, (tile, err)
+
+
+def test_conv_identity_asymmetric():
+    """A = I-style check with an asymmetric B: catches a transposed C write."""
+    spec = ConvSpec.auto(64, 64, 1, 1, 0, ops.ACT_NONE)
+    x = torch.zeros(1, 8, 8, 64)
+    for p in range(64):
+        x.view(64, 64)[p, p] = 1.0
+    w = torch.arange(64 * 64, dtype=torch.float32).reshape(64, 64, 1, 1) % 17 - 8
+    wp = ops.pack_conv_weight(w, spec)
+    out = ops.conv2d(x.to(torch.bfloat16).cuda(), spec, wp.cuda(), None)
+    torch.cuda.synchronize()
+    # out[pixel p, n] = w[n, p]
+    ref = w.view(64, 64).t()
+    assert torch.equal(out.cpu().float().view(64, 64), ref)
+
+
+def test_maxpool_avgpool_softmax():
+    x = _rand((2, 112, 112, 64), 3)
+    y_ref = ops.maxpool2d(x, 3, 2, 1)
+    y = ops.maxpool2d(x.cuda(), 3, 2, 1)
+    assert torch.equal(y.cpu(), y_ref)
+    f = _rand((3, 7, 7, 2048), 4)
+    a = ops.global_avgpool(f.cuda()).cpu().float()
+    assert (a - f.float().mean((1, 2))).abs().max() < 0.02
+    lg = _rand((5, 1000), 5, 3.0)
+    p, am = ops.softmax_rows(lg.cuda())
+    pr = torch.softmax(lg.float(), 1)
+    assert (p.cpu() - pr).abs().max() < 1e-5
+    assert torch.equal(am.cpu(), lg.float().argmax(1))
+
+
+def test_sppf_and_upsample():
+    C = 32
+    buf = torch.zeros(2, 20, 20, 4 * C, dtype=torch.bfloat16)
+    buf[..., :C] = _rand((2, 20, 20, C), 6)
+    ref = ops.sppf_pool(buf.clone(), C)
+    got = ops.sppf_pool(buf.cuda(), C).cpu()
+    assert torch.equal(got, ref)
+    x = _rand((2, 10, 10, 48), 7)
+    out_ref = torch.zeros(2, 20, 20, 64, dtype=torch.bfloat16)
+    out = torch.zeros(2, 20, 20, 64, dtype=torch.bfloat16, device="cuda")
+    ops.upsample2x(x, out_ref, C=32, x_coff=16, y_coff=8)
+    ops.upsample2x(x.cuda(), out, C=32, x_coff=16, y_coff=8)
+    assert torch.equal(out.cpu(), out_ref)
+
+
+def test_synth_preprocess_bn():
+    fr = torch.empty(2, 16, 16, 3, dtype=torch.uint8)
+    ops.synth_frames(fr, 7, 3)
+    frg = torch.empty(2, 16, 16, 3, dtype=torch.uint8, device="cuda")
+    ops.synth_frames(frg, 7, 3)
+    assert torch.equal(frg.cpu(), fr)
+    ctr = torch.tensor([3], dtype=torch.int64, device="cuda")
+    ops.synth_frames(frg, 7, ctr)
+    assert torch.equal(frg.cpu(), fr) and int(ctr.item()) == 4
+    p_ref = ops.preprocess(fr)
+    p = ops.preprocess(fr.cuda()).cpu()
+    assert (p.float() - p_ref.float()).abs().max() <= 0.02
+    x = _rand((4, 5, 5, 64), 8)
+    sc = torch.rand(64) + 0.5
+    sh = torch.randn(64)
+    y_ref = ops.batchnorm_nhwc(x, sc, sh, relu=True)
+    y = ops.batchnorm_nhwc(x.cuda(), sc.cuda(), sh.cuda(), relu=True).cpu()
+    assert (y.float() - y_ref.float()).abs().max() <= 0.05
+
+
+def test_yolo_decode_and_nms():
+    nc = 80
+    feats = [_rand((2, h, h, 64 + nc), 10 + i, 2.0) for i, h in enumerate((16, 8, 4))]
+    b_ref, s_ref, c_ref = ops.yolo_decode(feats, (8, 16, 32), nc)
+    b, s, c = ops.yolo_decode([f.cuda() for f in feats], (8, 16, 32), nc)
+    assert (b.cpu() - b_ref).abs().max() < 1e-2
+    assert (s.cpu() - s_ref).abs().max() < 1e-5
+    assert torch.equal(c.cpu(), c_ref)
+    out_ref, cnt_ref = ops.nms(b_ref, s_ref, c_ref, conf=0.6, iou=0.5, max_det=100)
+    out, cnt = ops.nms(b_ref.cuda(), s_ref.cuda(), c_ref.cuda(), conf=0.6, iou=0.5, max_det=100)
+    assert torch.equal(cnt.cpu(), cnt_ref)
+    assert (out.cpu() - out_ref).abs().max() < 1e-4
+
+
+def test_nms_dense_overlaps():
+    """Many heavily-overlapping boxes of few classes: exercises in-chunk suppression."""
+    g = torch.Generator().manual_seed(11)
+    A = 700
+    ctr = torch.rand(1, A, 2, generator=g) * 100
+    wh = torch.rand(1, A, 2, generator=g) * 30 + 5
+    boxes = torch.cat([ctr - wh / 2, ctr + wh / 2], -1)
+    scores = torch.rand(1, A, generator=g)
+    cls = torch.randint(0, 3, (1, A), generator=g, dtype=torch.int32)
+    o_ref, n_ref = ops.nms(boxes, scores, cls, conf=0.1, iou=0.45, max_det=300)
+    o, n = ops.nms(boxes.cuda(), scores.cuda(), cls.cuda(), conf=0.1, iou=0.45, max_det=300)
+    assert torch.equal(n.cpu(), n_ref)
+    assert (o.cpu() - o_ref).abs().max() < 1e-4
