@@ -1,0 +1,62 @@
+"""CPU tests: BN folding, deployed ResNet-50 vs the fp32 module, engine plumbing."""
+import torch
+import torch.nn as nn
+
+from kvedge_amd import ops
+from kvedge_amd.engine import InferenceEngine
+from kvedge_amd.models.layers import DeployedConv, fold_bn, frames_to_nchw
+from kvedge_amd.models.resnet import KvResNet50, init_resnet50
+
+
+def test_fold_bn_exact():
+    torch.manual_seed(0)
+    conv = nn.Conv2d(8, 16, 3, 1, 1, bias=False)
+    bn = nn.BatchNorm2d(16)
+    bn.running_mean.uniform_(-1, 1)
+    bn.running_var.uniform_(0.5, 2)
+    bn.weight.data.uniform_(0.5, 1.5)
+    bn.bias.data.uniform_(-1, 1)
+    bn.eval()
+    x = torch.randn(2, 8, 10, 10)
+    w, b = fold_bn(conv, bn)
+    y = nn.functional.conv2d(x, w, b, 1, 1)
+    assert torch.allclose(y, bn(conv(x)), atol=1e-5)
+
+
+def test_deployed_conv_from_modules():
+    conv = nn.Conv2d(16, 32, 3, 2, 1, bias=False)
+    bn = nn.BatchNorm2d(16 * 2).eval()
+    d = DeployedConv.from_modules(conv, bn, ops.ACT_RELU)
+    assert d.spec.stride == 2 and d.spec.pad == 1 and d.w.shape == (32, d.spec.Kpad)
+    assert d.flops_per_pixel == 2 * 9 * 16 * 32
+
+
+def test_resnet50_cpu_deployed_vs_module():
+    ref = init_resnet50(seed=0)
+    kv = KvResNet50(ref, "cpu")
+    assert len(kv.convs()) == 1 + 16 * 3 + 4 + 1  # stem + bottleneck convs + downsamples + fc
+    assert abs(kv.flops_per_image() / 1e9 - 8.18) < 0.05
+    fr = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8,
+                       generator=torch.Generator().manual_seed(3))
+    with torch.no_grad():
+        lg = kv.logits(ops.preprocess(fr)).float()
+        lr = ref(frames_to_nchw(fr))
+    cos = nn.functional.cosine_similarity(lg.flatten(), lr.flatten(), dim=0)
+    assert cos > 0.98, float(cos)
+
+
+def test_engine_cpu_eager():
+    class Tiny:
+        def __call__(self, frames):
+            x = ops.preprocess(frames)
+            pooled = x.float().mean((1, 2))
+            return ops.softmax_rows(pooled.to(torch.bfloat16))
+
+    eng = InferenceEngine(Tiny(), 2, 16, device="cpu", seed=1).prepare(warmup=1)
+    assert eng.graph is None
+    p1 = eng.run()[0].clone()
+    p2 = eng.run()[0].clone()
+    assert p1.shape == (2, 4) and not torch.equal(p1, p2)
+    assert eng.run_timed(2) >= 0
+    st = eng.measure_latency(3)
+    assert st.count == 3 and st.percentile(50) >= 0
