@@ -215,37 +215,50 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const KvConvParams p
     __syncthreads();
   }
 
-  // ---- fused epilogue: bias + residual + activation + bf16, 8-B stores ------
-  bf16* __restrict__ Y = reinterpret_cast<bf16*>(p.y);
-  const bf16* __restrict__ R = reinterpret_cast<const bf16*>(p.res);
+  // ---- fused epilogue, staged through LDS for full-line 16-B stores ----------
+  // Phase 1: acc (+bias, +act when there is no residual) -> bf16 C tile in LDS,
+  //          row stride BN*2+16 B (ds_write_b64 at most 2-way, rows 16-B aligned).
+  // Phase 2: each lane moves 16 B (8 channels) of a row: residual read, act,
+  //          store — consecutive lanes cover consecutive bytes of a row, so a wave
+  //          writes whole 128-256 B row segments instead of 32-B pieces.
+  constexpr int CS = BN + 8;  // C-tile row stride in elements
+  static_assert(BM * CS <= 2 * (BM + BN) * BK, "C tile must fit the operand buffers");
+  const bool has_res = p.res != nullptr;
+  const int act1 = has_res ? kActNone : p.act;
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
-    const int n = n0 + wn * WTN + tn * 16 + (lane >> 4) * 4;
-    if (n >= p.Cout) continue;
+    const int nl = wn * WTN + tn * 16 + (lane >> 4) * 4;
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (p.bias) bv = *reinterpret_cast<const float4*>(p.bias + n);
+    if (p.bias && n0 + nl < p.Cout) bv = *reinterpret_cast<const float4*>(p.bias + n0 + nl);
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) {
-      const int m = m0 + wm * WTM + tm * 16 + (lane & 15);
-      if (m >= p.M) continue;
-      float v0 = acc[tn][tm][0] + bv.x;
-      float v1 = acc[tn][tm][1] + bv.y;
-      float v2 = acc[tn][tm][2] + bv.z;
-      float v3 = acc[tn][tm][3] + bv.w;
-      if (R) {
-        const bf16x4 rv = *reinterpret_cast<const bf16x4*>(R + (size_t)m * p.ldr + p.r_coff + n);
-        v0 += (float)rv[0];
-        v1 += (float)rv[1];
-        v2 += (float)rv[2];
-        v3 += (float)rv[3];
-      }
+      const int ml = wm * WTM + tm * 16 + (lane & 15);
       bf16x4 o;
-      o[0] = f2bf(apply_act(v0, p.act));
-      o[1] = f2bf(apply_act(v1, p.act));
-      o[2] = f2bf(apply_act(v2, p.act));
-      o[3] = f2bf(apply_act(v3, p.act));
-      *reinterpret_cast<bf16x4*>(Y + (size_t)m * p.ldy + p.y_coff + n) = o;
+      o[0] = f2bf(apply_act(acc[tn][tm][0] + bv.x, act1));
+      o[1] = f2bf(apply_act(acc[tn][tm][1] + bv.y, act1));
+      o[2] = f2bf(apply_act(acc[tn][tm][2] + bv.z, act1));
+      o[3] = f2bf(apply_act(acc[tn][tm][3] + bv.w, act1));
+      *reinterpret_cast<bf16x4*>(smem + ml * CS + nl) = o;
     }
+  }
+  __syncthreads();
+  bf16* __restrict__ Y = reinterpret_cast<bf16*>(p.y);
+  const bf16* __restrict__ R = reinterpret_cast<const bf16*>(p.res);
+  constexpr int CPR = BN / 8;               // 16-B chunks per tile row
+  constexpr int PER = BM * CPR / 256;       // chunks per thread
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int idx = tid + 256 * j;
+    const int ml = idx / CPR, ch = idx % CPR;
+    const int m = m0 + ml, n = n0 + ch * 8;
+    if (m >= p.M || n >= p.Cout) continue;
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + ml * CS + ch * 8);
+    if (has_res) {
+      const bf16x8 rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(apply_act((float)v[e] + (float)rv[e], p.act));
+    }
+    *reinterpret_cast<bf16x8*>(Y + (size_t)m * p.ldy + p.y_coff + n) = v;
   }
 }
 
@@ -300,11 +313,11 @@ extern "C" int kv_conv_pick_tile(const KvConvParams* p) {
 }
 
 extern "C" int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream) {
-  if (p->Kpad % BK != 0 || p->Cout % 4 != 0) return -1;
+  if (p->Kpad % BK != 0 || p->Cout % 8 != 0) return -1;
   if (p->mode == 2 && (p->Cin != 4 || p->ldx != 4)) return -2;
   if (p->mode != 2 && (p->Cin % 8 != 0 || p->ldx % 8 != 0 || p->x_coff % 8 != 0)) return -3;
   if (p->mode == 1 && (p->KH != 1 || p->KW != 1 || p->stride != 1 || p->pad != 0)) return -4;
-  if ((p->ldy % 4) || (p->y_coff % 4) || (p->res && ((p->ldr % 4) || (p->r_coff % 4)))) return -5;
+  if ((p->ldy % 8) || (p->y_coff % 8) || (p->res && ((p->ldr % 8) || (p->r_coff % 8)))) return -5;
   if (tile < 0) tile = kv_conv_pick_tile(p);
   if (tile >= kNumTiles) return -6;
   const TileEntry& e = kTiles[tile];

@@ -196,12 +196,11 @@ __global__ __launch_bounds__(256) void nms_kernel(const float* __restrict__ boxe
       kept[4 * pos + 1] = y1;
       kept[4 * pos + 2] = x2;
       kept[4 * pos + 3] = y2;
-      const float off = (float)c * kMaxWH;
-      float* r = o + pos * 6;
-      r[0] = x1 - off;
-      r[1] = y1 - off;
-      r[2] = x2 - off;
-      r[3] = y2 - off;
+      float* r = o + pos * 6;  // original (un-offset) coordinates: exact, no fp32 cancellation
+      r[0] = bx[idx * 4 + 0];
+      r[1] = bx[idx * 4 + 1];
+      r[2] = bx[idx * 4 + 2];
+      r[3] = bx[idx * 4 + 3];
       r[4] = s;
       r[5] = (float)c;
     }
