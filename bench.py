@@ -36,6 +36,7 @@ def main(argv=None):
                     help="per-GPU batch")
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "yolov8n"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-autotune", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
@@ -66,7 +67,7 @@ def main(argv=None):
     parallel.broadcast_tensors(parallel.model_tensors(model), src=0)
     eng = InferenceEngine(model, a.batch, hw, device=di.device, seed=a.seed + di.rank,
                           use_graph=not a.no_graph)
-    eng.prepare(warmup=2)
+    eng.prepare(warmup=2, autotune=not a.no_autotune)
     build_s = time.perf_counter() - t_build
 
     for _ in range(a.warmup):

@@ -223,8 +223,13 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const KvConvParams p
   //          writes whole 128-256 B row segments instead of 32-B pieces.
   constexpr int CS = BN + 8;  // C-tile row stride in elements
   static_assert(BM * CS <= 2 * (BM + BN) * BK, "C tile must fit the operand buffers");
+  // act bits: [1:0] activation, bit 2 = residual added AFTER the activation
+  // (YOLO Bottleneck: x + SiLU(conv)); otherwise act(conv + res) (ResNet).
   const bool has_res = p.res != nullptr;
-  const int act1 = has_res ? kActNone : p.act;
+  const int act_fn = p.act & 3;
+  const bool res_post = (p.act & 4) != 0;
+  const int act1 = (has_res && !res_post) ? kActNone : act_fn;
+  const int act2 = res_post ? kActNone : act_fn;
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) {
     const int nl = wn * WTN + tn * 16 + (lane >> 4) * 4;
@@ -256,7 +261,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const KvConvParams p
     if (has_res) {
       const bf16x8 rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = f2bf(apply_act((float)v[e] + (float)rv[e], p.act));
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(apply_act((float)v[e] + (float)rv[e], act2));
     }
     *reinterpret_cast<bf16x8*>(Y + (size_t)m * p.ldy + p.y_coff + n) = v;
   }

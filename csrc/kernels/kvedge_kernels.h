@@ -30,7 +30,7 @@ typedef struct KvConvParams {
   int K, Kpad;        // logical and padded (multiple of 64) reduction length
   int M;              // N*Ho*Wo
   int ldy, y_coff, ldr, r_coff;
-  int act;            // 0 none, 1 relu, 2 silu
+  int act;            // bits[1:0]: 0 none, 1 relu, 2 silu; bit 2: residual after act
   int mode;           // 0 general, 1 1x1/s1/p0 GEMM, 2 stem (Cin=4, KW padded even)
 } KvConvParams;
 

@@ -67,8 +67,15 @@ class InferenceEngine:
         self.outputs = self.model(self.frames)
         return self.outputs
 
-    def prepare(self, warmup: int = 2):
-        """Warm up (kernel code objects load, allocator pools fill), then capture."""
+    def prepare(self, warmup: int = 2, autotune: bool = True, verbose: bool = False):
+        """Autotune conv tiles for this batch, warm up (code objects load, allocator
+        pools fill), then capture the step into a hipGraph."""
+        self.tuning = {}
+        if autotune and self.device.type == "cuda":
+            from .autotune import autotune as _tune
+
+            ops.synth_frames(self.frames, self.seed, 0)
+            self.tuning = _tune(self.model, self.frames, verbose=verbose)
         if not self.use_graph:
             for _ in range(warmup):
                 self._step()

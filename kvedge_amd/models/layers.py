@@ -31,12 +31,31 @@ def fold_bn(conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d]):
     return wf, bf
 
 
+_RECORDER: Optional[list] = None
+
+
+class record_convs:
+    """Context manager: record every DeployedConv call (for the tile autotuner)."""
+
+    def __enter__(self):
+        global _RECORDER
+        _RECORDER = []
+        return _RECORDER
+
+    def __exit__(self, *exc):
+        global _RECORDER
+        _RECORDER = None
+
+
 @dataclass
 class DeployedConv:
-    """A conv ready for the kernel: spec + packed bf16 weight + fp32 bias."""
+    """A conv ready for the kernel: spec + packed bf16 weight + fp32 bias.
+
+    ``tile`` is the kernel tile index chosen by the autotuner (-1 = heuristic)."""
     spec: ConvSpec
     w: torch.Tensor
     b: torch.Tensor
+    tile: int = -1
 
     @staticmethod
     def from_modules(conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d], act: int,
@@ -49,11 +68,15 @@ class DeployedConv:
                             bf.contiguous().to(device))
 
     def to(self, device) -> "DeployedConv":
-        return DeployedConv(self.spec, self.w.to(device), self.b.to(device))
+        return DeployedConv(self.spec, self.w.to(device), self.b.to(device), self.tile)
 
-    def __call__(self, x, res=None, out=None, x_coff=0, y_coff=0, r_coff=0, tile=-1):
-        return ops.conv2d(x, self.spec, self.w, self.b, res=res, out=out, x_coff=x_coff,
-                          y_coff=y_coff, r_coff=r_coff, tile=tile)
+    def __call__(self, x, res=None, out=None, x_coff=0, y_coff=0, r_coff=0, tile=None):
+        out = ops.conv2d(x, self.spec, self.w, self.b, res=res, out=out, x_coff=x_coff,
+                         y_coff=y_coff, r_coff=r_coff, tile=self.tile if tile is None else tile)
+        if _RECORDER is not None:
+            _RECORDER.append((self, dict(x=x, res=res, out=out, x_coff=x_coff, y_coff=y_coff,
+                                         r_coff=r_coff)))
+        return out
 
     @property
     def flops_per_pixel(self) -> int:

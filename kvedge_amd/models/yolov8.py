@@ -1,0 +1,366 @@
+"""YOLOv8n detection model (ultralytics yolov8.yaml, scale n) — reference + deployed forms.
+
+BASELINE.json config 4 ("YOLOv8n detection edge module, conv + NMS CDNA4 HIP kernels").
+Architecture facts (depth 0.33, width 0.25, max 1024 ch, 80 classes, reg_max 16) are
+public model facts; no ultralytics code is used (the package is not installed and
+there is no network).  Weights are random-init, seeded; the Detect head biases use
+the usual prior (box 1.0, cls log(5/nc/(640/s)^2)) so random nets give sparse,
+realistic candidate counts for NMS.
+
+Deployed forward is CONCAT-FREE: every Concat / C2f split of the graph is a channel
+slice of one NHWC buffer; producers write their slice directly (conv y_coff, upsample
+y_coff) and consumers read slices (x_coff).  The two Detect branch stems that read
+the same level feature are merged into one conv (Cout 64+80).  Hot path kernels:
+K2/K3 convs with SiLU epilogue, K5b SPPF (3 pools in one pass), K8 upsample, K9
+decode, K10 NMS.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from .layers import DeployedConv, calibrate_bn
+
+ACT_SILU, ACT_NONE = ops.ACT_SILU, ops.ACT_NONE
+NC = 80
+REG_MAX = 16
+STRIDES = (8, 16, 32)
+
+
+# ---------------------------------------------------------------------------
+# reference modules (NCHW fp32)
+# ---------------------------------------------------------------------------
+class Conv(nn.Module):
+    def __init__(self, c1, c2, k=1, s=1):
+        super().__init__()
+        self.conv = nn.Conv2d(c1, c2, k, s, k // 2, bias=False)
+        self.bn = nn.BatchNorm2d(c2, eps=1e-3, momentum=0.03)
+
+    def forward(self, x):
+        return F.silu(self.bn(self.conv(x)))
+
+
+class Bottleneck(nn.Module):
+    def __init__(self, c1, c2, shortcut=True):
+        super().__init__()
+        self.cv1 = Conv(c1, c2, 3)
+        self.cv2 = Conv(c2, c2, 3)
+        self.add = shortcut and c1 == c2
+
+    def forward(self, x):
+        y = self.cv2(self.cv1(x))
+        return x + y if self.add else y
+
+
+class C2f(nn.Module):
+    def __init__(self, c1, c2, n=1, shortcut=False):
+        super().__init__()
+        self.c = c2 // 2
+        self.cv1 = Conv(c1, 2 * self.c, 1)
+        self.cv2 = Conv((2 + n) * self.c, c2, 1)
+        self.m = nn.ModuleList(Bottleneck(self.c, self.c, shortcut) for _ in range(n))
+
+    def forward(self, x):
+        y = list(self.cv1(x).chunk(2, 1))
+        for m in self.m:
+            y.append(m(y[-1]))
+        return self.cv2(torch.cat(y, 1))
+
+
+class SPPF(nn.Module):
+    def __init__(self, c1, c2, k=5):
+        super().__init__()
+        c_ = c1 // 2
+        self.cv1 = Conv(c1, c_, 1)
+        self.cv2 = Conv(c_ * 4, c2, 1)
+        self.k = k
+
+    def forward(self, x):
+        y = [self.cv1(x)]
+        for _ in range(3):
+            y.append(F.max_pool2d(y[-1], self.k, 1, self.k // 2))
+        return self.cv2(torch.cat(y, 1))
+
+
+class Detect(nn.Module):
+    def __init__(self, nc=NC, ch=(64, 128, 256)):
+        super().__init__()
+        self.nc = nc
+        c2 = max(16, ch[0] // 4, REG_MAX * 4)
+        c3 = max(ch[0], min(nc, 100))
+        self.cv2 = nn.ModuleList(
+            nn.Sequential(Conv(x, c2, 3), Conv(c2, c2, 3), nn.Conv2d(c2, 4 * REG_MAX, 1))
+            for x in ch)
+        self.cv3 = nn.ModuleList(
+            nn.Sequential(Conv(x, c3, 3), Conv(c3, c3, 3), nn.Conv2d(c3, nc, 1)) for x in ch)
+
+    def bias_init(self):
+        for a, b, s in zip(self.cv2, self.cv3, STRIDES):
+            a[-1].bias.data[:] = 1.0
+            b[-1].bias.data[:self.nc] = math.log(5 / self.nc / (640 / s) ** 2)
+
+    def forward(self, feats):
+        return [torch.cat([self.cv2[i](f), self.cv3[i](f)], 1) for i, f in enumerate(feats)]
+
+
+class YoloV8nRef(nn.Module):
+    """Returns the three raw Detect outputs [N, 64+nc, h, w] (strides 8/16/32)."""
+
+    def __init__(self, nc=NC):
+        super().__init__()
+        self.nc = nc
+        self.b0 = Conv(3, 16, 3, 2)
+        self.b1 = Conv(16, 32, 3, 2)
+        self.b2 = C2f(32, 32, 1, True)
+        self.b3 = Conv(32, 64, 3, 2)
+        self.b4 = C2f(64, 64, 2, True)
+        self.b5 = Conv(64, 128, 3, 2)
+        self.b6 = C2f(128, 128, 2, True)
+        self.b7 = Conv(128, 256, 3, 2)
+        self.b8 = C2f(256, 256, 1, True)
+        self.b9 = SPPF(256, 256, 5)
+        self.h12 = C2f(384, 128, 1, False)
+        self.h15 = C2f(192, 64, 1, False)
+        self.h16 = Conv(64, 64, 3, 2)
+        self.h18 = C2f(192, 128, 1, False)
+        self.h19 = Conv(128, 128, 3, 2)
+        self.h21 = C2f(384, 256, 1, False)
+        self.detect = Detect(nc, (64, 128, 256))
+
+    def forward(self, x):
+        x = self.b1(self.b0(x))
+        x = self.b2(x)
+        p3b = self.b4(self.b3(x))
+        p4b = self.b6(self.b5(p3b))
+        p5b = self.b9(self.b8(self.b7(p4b)))
+        up = lambda t: F.interpolate(t, scale_factor=2, mode="nearest")  # noqa: E731
+        h12 = self.h12(torch.cat([up(p5b), p4b], 1))
+        p3 = self.h15(torch.cat([up(h12), p3b], 1))
+        p4 = self.h18(torch.cat([self.h16(p3), h12], 1))
+        p5 = self.h21(torch.cat([self.h19(p4), p5b], 1))
+        return self.detect([p3, p4, p5])
+
+
+def init_yolov8n(seed: int = 0, calibrate: bool = True, calib_batch: int = 2,
+                 calib_hw: int = 320) -> YoloV8nRef:
+    torch.manual_seed(seed)
+    m = YoloV8nRef()
+    m.detect.bias_init()
+    if calibrate:
+        g = torch.Generator().manual_seed(seed)
+        fr = torch.randint(0, 256, (calib_batch, calib_hw, calib_hw, 3), generator=g,
+                           dtype=torch.uint8)
+        calibrate_bn(m, [fr.float().permute(0, 3, 1, 2) / 255.0])
+    m.eval()
+    return m
+
+
+def frames_to_yolo(frames_u8: torch.Tensor) -> torch.Tensor:
+    return (frames_u8.float() / 255.0).permute(0, 3, 1, 2).contiguous()
+
+
+# ---------------------------------------------------------------------------
+# deployed (NHWC bf16, concat-free)
+# ---------------------------------------------------------------------------
+def _dc(m: Conv, device) -> DeployedConv:
+    return DeployedConv.from_modules(m.conv, m.bn, ACT_SILU, device)
+
+
+class DC2f:
+    def __init__(self, m: C2f, device):
+        self.c = m.c
+        self.n = len(m.m)
+        self.cv1 = _dc(m.cv1, device)
+        self.cv2 = _dc(m.cv2, device)
+        self.m = []
+        for b in m.m:
+            c2 = _dc(b.cv2, device)
+            if b.add:  # x + SiLU(bn(conv)): residual after the activation
+                c2.spec.act |= ops.RES_AFTER_ACT
+            self.m.append((_dc(b.cv1, device), c2, b.add))
+
+    def __call__(self, x, x_coff=0, out=None, y_coff=0):
+        N, H, W, _ = x.shape
+        c, n = self.c, self.n
+        cat = torch.empty(N, H, W, (2 + n) * c, dtype=torch.bfloat16, device=x.device)
+        self.cv1(x, x_coff=x_coff, out=cat, y_coff=0)
+        for i, (b1, b2, add) in enumerate(self.m):
+            t = b1(cat, x_coff=(1 + i) * c)
+            b2(t, res=cat if add else None, r_coff=(1 + i) * c, out=cat, y_coff=(2 + i) * c)
+        return self.cv2(cat, out=out, y_coff=y_coff)
+
+    def convs(self):
+        out = [self.cv1, self.cv2]
+        for b1, b2, _ in self.m:
+            out += [b1, b2]
+        return out
+
+
+class DSPPF:
+    def __init__(self, m: SPPF, device):
+        self.cv1 = _dc(m.cv1, device)
+        self.cv2 = _dc(m.cv2, device)
+        self.c_ = m.cv1.conv.out_channels
+
+    def __call__(self, x, out=None, y_coff=0):
+        N, H, W, _ = x.shape
+        buf = torch.empty(N, H, W, 4 * self.c_, dtype=torch.bfloat16, device=x.device)
+        self.cv1(x, out=buf, y_coff=0)
+        ops.sppf_pool(buf, self.c_)
+        return self.cv2(buf, out=out, y_coff=y_coff)
+
+    def convs(self):
+        return [self.cv1, self.cv2]
+
+
+class DDetectLevel:
+    """One Detect level: merged branch stems (64 box + 80 cls) -> two 3x3 -> two 1x1
+    heads writing [box 64 | cls 80] slices of one [N,h,w,144] buffer."""
+
+    def __init__(self, d: Detect, i: int, device):
+        a, b = d.cv2[i], d.cv3[i]
+        wa, ba = _fold(a[0])
+        wb, bb = _fold(b[0])
+        merged = nn.Conv2d(wa.shape[1], wa.shape[0] + wb.shape[0], 3, 1, 1, bias=True)
+        with torch.no_grad():
+            merged.weight.copy_(torch.cat([wa, wb], 0))
+            merged.bias.copy_(torch.cat([ba, bb], 0))
+        self.stem = DeployedConv.from_modules(merged, None, ACT_SILU, device)
+        self.ca = wa.shape[0]
+        self.a1 = _dc(a[1], device)
+        self.b1 = _dc(b[1], device)
+        self.a2 = DeployedConv.from_modules(a[2], None, ACT_NONE, device)
+        self.b2 = DeployedConv.from_modules(b[2], None, ACT_NONE, device)
+        self.nc = d.nc
+
+    def __call__(self, p):
+        N, h, w, _ = p.shape
+        s = self.stem(p)
+        feat = torch.empty(N, h, w, 4 * REG_MAX + self.nc, dtype=torch.bfloat16, device=p.device)
+        ta = self.a1(s, x_coff=0)
+        self.a2(ta, out=feat, y_coff=0)
+        tb = self.b1(s, x_coff=self.ca)
+        self.b2(tb, out=feat, y_coff=4 * REG_MAX)
+        return feat
+
+    def convs(self):
+        return [self.stem, self.a1, self.b1, self.a2, self.b2]
+
+
+def _fold(m: Conv):
+    from .layers import fold_bn
+
+    return fold_bn(m.conv, m.bn)
+
+
+class KvYoloV8n:
+    """Deployed YOLOv8n: frames u8 [N,640,640,3] -> (dets fp32 [N,300,6], count int32 [N])."""
+
+    image_size = 640
+
+    def __init__(self, ref: YoloV8nRef, device="cuda", conf=0.25, iou=0.7, max_det=300):
+        self.device = torch.device(device)
+        self.nc = ref.nc
+        self.conf, self.iou, self.max_det = conf, iou, max_det
+        d = self.device
+        self.b0, self.b1, self.b3, self.b5, self.b7 = (_dc(m, d) for m in
+                                                        (ref.b0, ref.b1, ref.b3, ref.b5, ref.b7))
+        self.b2, self.b4, self.b6, self.b8 = (DC2f(m, d) for m in (ref.b2, ref.b4, ref.b6, ref.b8))
+        self.b9 = DSPPF(ref.b9, d)
+        self.h12, self.h15, self.h18, self.h21 = (DC2f(m, d) for m in
+                                                  (ref.h12, ref.h15, ref.h18, ref.h21))
+        self.h16, self.h19 = _dc(ref.h16, d), _dc(ref.h19, d)
+        self.levels = [DDetectLevel(ref.detect, i, d) for i in range(3)]
+
+    @staticmethod
+    def build(seed: int = 0, device="cuda", calibrate: bool = True) -> "KvYoloV8n":
+        return KvYoloV8n(init_yolov8n(seed, calibrate=calibrate), device)
+
+    def convs(self) -> List[DeployedConv]:
+        out = [self.b0, self.b1, self.b3, self.b5, self.b7, self.h16, self.h19]
+        for m in (self.b2, self.b4, self.b6, self.b8, self.b9, self.h12, self.h15, self.h18,
+                  self.h21):
+            out += m.convs()
+        for lv in self.levels:
+            out += lv.convs()
+        return out
+
+    def flops_per_image(self, hw: int = 640) -> int:
+        return int(self._flops(hw))
+
+    def _flops(self, hw):
+        total = 0
+        h = hw
+        def acc(c, hin):
+            nonlocal total
+            ho = c.spec.out_hw(hin, hin)[0]
+            total += c.flops_per_pixel * ho * ho
+            return ho
+        h = acc(self.b0, h); h = acc(self.b1, h)
+        for blk in (self.b2,):
+            for c in blk.convs():
+                acc(c, h)
+        h = acc(self.b3, h); h3 = h
+        for c in self.b4.convs():
+            acc(c, h)
+        h = acc(self.b5, h); h4 = h
+        for c in self.b6.convs():
+            acc(c, h)
+        h = acc(self.b7, h); h5 = h
+        for c in self.b8.convs() + self.b9.convs():
+            acc(c, h)
+        for c in self.h12.convs():
+            acc(c, h4)
+        for c in self.h15.convs():
+            acc(c, h3)
+        acc(self.h16, h3)
+        for c in self.h18.convs():
+            acc(c, h4)
+        acc(self.h19, h4)
+        for c in self.h21.convs():
+            acc(c, h5)
+        for lv, hl in zip(self.levels, (h3, h4, h5)):
+            for c in lv.convs():
+                acc(c, hl)
+        return total
+
+    def heads(self, x: torch.Tensor):
+        """x: preprocessed bf16 NHWC4 [N,640,640,4] -> three [N,h,w,144] head outputs."""
+        N = x.shape[0]
+        dev = x.device
+        bf = torch.bfloat16
+        x = self.b1(self.b0(x))                       # [N,160,160,32]
+        x = self.b2(x)
+        x = self.b3(x)                                # [N,80,80,64]
+        H3 = x.shape[1]
+        H4, H5 = H3 // 2, H3 // 4
+        cat14 = torch.empty(N, H3, H3, 192, dtype=bf, device=dev)   # [up(h12) 128 | p3b 64]
+        cat11 = torch.empty(N, H4, H4, 384, dtype=bf, device=dev)   # [up(p5b) 256 | p4b 128]
+        cat17 = torch.empty(N, H4, H4, 192, dtype=bf, device=dev)   # [h16 64 | h12 128]
+        cat20 = torch.empty(N, H5, H5, 384, dtype=bf, device=dev)   # [h19 128 | p5b 256]
+        self.b4(x, out=cat14, y_coff=128)                          # p3b
+        x = self.b5(cat14, x_coff=128)                             # [N,40,40,128]
+        self.b6(x, out=cat11, y_coff=256)                          # p4b
+        x = self.b7(cat11, x_coff=256)                             # [N,20,20,256]
+        x = self.b8(x)
+        self.b9(x, out=cat20, y_coff=128)                          # p5b
+        ops.upsample2x(cat20, cat11, C=256, x_coff=128, y_coff=0)
+        self.h12(cat11, out=cat17, y_coff=64)                      # h12
+        ops.upsample2x(cat17, cat14, C=128, x_coff=64, y_coff=0)
+        p3 = self.h15(cat14)                                       # [N,80,80,64]
+        self.h16(p3, out=cat17, y_coff=0)
+        p4 = self.h18(cat17)                                       # [N,40,40,128]
+        self.h19(p4, out=cat20, y_coff=0)
+        p5 = self.h21(cat20)                                       # [N,20,20,256]
+        return [lv(p) for lv, p in zip(self.levels, (p3, p4, p5))]
+
+    def __call__(self, frames_u8: torch.Tensor):
+        x = ops.preprocess(frames_u8, mean=(0.0, 0.0, 0.0), std=(1.0, 1.0, 1.0))
+        feats = self.heads(x)
+        boxes, scores, cls = ops.yolo_decode(feats, STRIDES, self.nc)
+        return ops.nms(boxes, scores, cls, self.conf, self.iou, self.max_det)

@@ -33,6 +33,7 @@ _loaded = False
 _load_error: Optional[str] = None
 
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
+RES_AFTER_ACT = 4  # flag: y = act(conv) + res  (default: y = act(conv + res))
 MODE_GENERAL, MODE_GEMM, MODE_STEM = 0, 1, 2
 BK = 64
 

@@ -30,9 +30,12 @@ def conv2d(x, spec, w, bias, res, out, x_coff=0, y_coff=0, r_coff=0):
     y = F.conv2d(xin.permute(0, 3, 1, 2), wt, None, spec.stride, spec.pad).permute(0, 2, 3, 1)
     if bias is not None:
         y = y + bias.float()
-    if res is not None:
+    act, post = spec.act & 3, bool(spec.act & 4)
+    if res is not None and not post:
         y = y + res[..., r_coff:r_coff + spec.cout].float()
-    y = _act(y, spec.act)
+    y = _act(y, act)
+    if res is not None and post:
+        y = y.to(out.dtype).float() + res[..., r_coff:r_coff + spec.cout].float()
     out[..., y_coff:y_coff + spec.cout] = y.to(out.dtype)
     return out
 

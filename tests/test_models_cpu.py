@@ -60,3 +60,38 @@ def test_engine_cpu_eager():
     assert eng.run_timed(2) >= 0
     st = eng.measure_latency(3)
     assert st.count == 3 and st.percentile(50) >= 0
+
+
+def test_yolov8n_cpu_structure_and_parity():
+    from kvedge_amd.models.yolov8 import KvYoloV8n, frames_to_yolo, init_yolov8n
+
+    ref = init_yolov8n(seed=0)
+    assert abs(sum(p.numel() for p in ref.parameters()) - 3_157_184) == 0
+    kv = KvYoloV8n(ref, "cpu")
+    assert abs(kv.flops_per_image() / 1e9 - 8.74) < 0.02
+    fr = torch.randint(0, 256, (1, 256, 256, 3), dtype=torch.uint8,
+                       generator=torch.Generator().manual_seed(2))
+    with torch.no_grad():
+        hk = kv.heads(ops.preprocess(fr, mean=(0, 0, 0), std=(1, 1, 1)))
+        hr = ref(frames_to_yolo(fr))
+    for k, r in zip(hk, hr):
+        assert k.shape == r.permute(0, 2, 3, 1).shape
+        cos = nn.functional.cosine_similarity(k.float().flatten(), r.permute(0, 2, 3, 1).flatten(),
+                                              dim=0)
+        assert cos > 0.995, float(cos)
+    dets, cnt = kv(fr)
+    assert dets.shape == (1, 300, 6) and 0 <= int(cnt[0]) <= 300
+
+
+def test_residual_after_activation_flag():
+    from kvedge_amd.ops import ConvSpec
+
+    spec = ConvSpec.auto(16, 16, 3, 1, 1, ops.ACT_SILU | ops.RES_AFTER_ACT)
+    x = torch.randn(1, 5, 5, 16).to(torch.bfloat16)
+    w = torch.randn(16, 16, 3, 3) * 0.1
+    r = torch.randn(1, 5, 5, 16).to(torch.bfloat16)
+    y = ops.conv2d(x, spec, ops.pack_conv_weight(w, spec), torch.zeros(16), res=r)
+    conv = nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.to(torch.bfloat16).float(),
+                                None, 1, 1).permute(0, 2, 3, 1)
+    ref = nn.functional.silu(conv) + r.float()
+    assert (y.float() - ref).abs().max() < 0.05

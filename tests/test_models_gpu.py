@@ -52,3 +52,45 @@ def test_resnet50_engine_graph(resnet):
     frames = eng.frames.clone()
     probs, _ = kv(frames)
     assert torch.allclose(probs, eng.outputs[0], atol=1e-6)
+
+
+@pytest.fixture(scope="module")
+def yolo():
+    from kvedge_amd.models.yolov8 import KvYoloV8n, init_yolov8n
+
+    ref = init_yolov8n(seed=0)
+    return ref, KvYoloV8n(ref, "cuda"), KvYoloV8n(ref, "cpu")
+
+
+def test_yolov8n_parity(yolo):
+    from kvedge_amd.models.yolov8 import frames_to_yolo
+
+    ref, kv, kv_cpu = yolo
+    fr = _frames(2, 5, hw=320)
+    with torch.no_grad():
+        hg = kv.heads(ops.preprocess(fr.cuda(), mean=(0, 0, 0), std=(1, 1, 1)))
+        hc = kv_cpu.heads(ops.preprocess(fr, mean=(0, 0, 0), std=(1, 1, 1)))
+        hr = ref(frames_to_yolo(fr))
+    for g, c, r in zip(hg, hc, hr):
+        g = g.float().cpu()
+        cos_dep = torch.nn.functional.cosine_similarity(g.flatten(), c.float().flatten(), dim=0)
+        cos_ref = torch.nn.functional.cosine_similarity(
+            g.flatten(), r.permute(0, 2, 3, 1).flatten(), dim=0)
+        assert cos_dep > 0.999 and cos_ref > 0.995, (float(cos_dep), float(cos_ref))
+
+
+def test_yolov8n_pipeline_graph(yolo):
+    _, kv, _ = yolo
+    eng = InferenceEngine(kv, 4, 640, device="cuda", seed=1).prepare(warmup=1)
+    dets, cnt = eng.run()
+    torch.cuda.synchronize()
+    assert dets.shape == (4, 300, 6) and cnt.shape == (4,)
+    assert int(cnt.max()) <= 300 and int(cnt.min()) >= 0
+    # NMS on the same decoded boxes: GPU kernel == CPU reference
+    frames = eng.frames.clone()
+    x = ops.preprocess(frames, mean=(0, 0, 0), std=(1, 1, 1))
+    b, s, c = ops.yolo_decode(kv.heads(x), (8, 16, 32), 80)
+    o_g, n_g = ops.nms(b, s, c, 0.05, 0.7, 300)
+    o_c, n_c = ops.nms(b.cpu(), s.cpu(), c.cpu(), 0.05, 0.7, 300)
+    assert torch.equal(n_g.cpu(), n_c)
+    assert (o_g.cpu() - o_c).abs().max() < 1e-3

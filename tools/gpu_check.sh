@@ -27,6 +27,7 @@ for s in $STEPS; do
     test)  run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python bench.py --steps 30 --warmup 5 --json-out $OUT/bench.json ;;
+    yolo)  run bench_yolo 400 python bench.py --model yolov8n --batch 64 --steps 20 --warmup 3 --json-out $OUT/bench_yolo.json ;;
     base)  run torch_base 400 python tools/torch_baseline.py --graph --batch 256 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 5 --warmup 2 ;;
     sweep) run sweep 600 python tools/batch_sweep.py ;;
