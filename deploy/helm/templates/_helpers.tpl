@@ -1,0 +1,146 @@
+{{/*
+kvedge chart helpers.  Resource names of replica 0 are exactly the reference's
+(levi106/kvedge _helper.tpl:6-8 naming rule: default .Chart.Name .Values.nameOverride,
+trunc 40, trimSuffix "-"); replica i>0 appends "-<i>".
+*/}}
+
+{{- define "kvedge.name" -}}
+{{- default .Chart.Name .Values.nameOverride | trunc 40 | trimSuffix "-" -}}
+{{- end -}}
+
+{{- define "kvedge.chart" -}}
+{{- printf "%s-%s" .Chart.Name .Chart.Version | replace "+" "_" | trunc 63 | trimSuffix "-" -}}
+{{- end -}}
+
+{{/* "" for replica 0, "-<i>" otherwise.  Context: (dict "root" $ "i" $i) */}}
+{{- define "kvedge.sfx" -}}
+{{- if gt (int .i) 0 }}-{{ .i }}{{ end -}}
+{{- end -}}
+
+{{/* Common labels (reference emitted version + managed-by; we add the chart label
+     the reference defined but never used, plus instance/part-of). */}}
+{{- define "kvedge.labels" -}}
+helm.sh/chart: {{ include "kvedge.chart" . }}
+{{- if .Chart.AppVersion }}
+app.kubernetes.io/version: {{ .Chart.AppVersion | quote }}
+{{- end }}
+app.kubernetes.io/managed-by: {{ .Release.Service }}
+app.kubernetes.io/instance: {{ .Release.Name }}
+app.kubernetes.io/part-of: kvedge
+{{- end -}}
+
+{{/* Bool-or-string flag, e.g. --set-string aziotEdgeVmEnableExternalSsh=true. */}}
+{{- define "kvedge.flag" -}}
+{{- if eq (lower (toString .)) "true" }}true{{ end -}}
+{{- end -}}
+
+{{/* Per-replica names.  Context: (dict "root" $ "i" $i) */}}
+{{- define "kvedge.vmName" -}}{{ include "kvedge.name" .root }}-linux{{ include "kvedge.sfx" . }}{{- end -}}
+{{- define "kvedge.dvName" -}}{{ include "kvedge.name" .root }}-linux-dv{{ include "kvedge.sfx" . }}{{- end -}}
+{{- define "kvedge.domain" -}}{{ include "kvedge.name" .root }}-vm{{ include "kvedge.sfx" . }}{{- end -}}
+{{- define "kvedge.svcName" -}}{{ include "kvedge.name" .root }}-vm-ssh-service{{ include "kvedge.sfx" . }}{{- end -}}
+{{- define "kvedge.cfgSecret" -}}{{ include "kvedge.name" .root }}-vm-aziotedgeconfig{{ include "kvedge.sfx" . }}{{- end -}}
+{{/* The reference names the cloud-init Secret from the RAW nameOverride (its TODO
+     at aziot-edge-vm.yaml:57).  Same name whenever nameOverride is set; falls back to
+     the truncated name instead of the invalid "-vm-cloudconfig" when it is empty. */}}
+{{- define "kvedge.ciSecret" -}}{{ default (include "kvedge.name" .root) .root.Values.nameOverride }}-vm-cloudconfig{{ include "kvedge.sfx" . }}{{- end -}}
+
+{{- define "kvedge.replicaConfig" -}}
+{{- $cfgs := .root.Values.replicaConfigs | default list -}}
+{{- if lt (int .i) (len $cfgs) }}{{ index $cfgs (int .i) }}{{ else }}{{ .root.Values.azIotEdgeConfig }}{{ end -}}
+{{- end -}}
+
+{{/* Secret-disk serial: the bootcmd mount and the VM disk must agree (reference
+     aziot-edge-vm.yaml:28 / _helper.tpl:64). */}}
+{{- define "kvedge.secretSerial" -}}D23YZ9W6WA5DJ487{{- end -}}
+
+{{/*
+cloud-init user-data (GPU-aware).  Context: (dict "root" $ "i" $i)
+ * same contract as the reference: secret disk (found by serial) mounted at
+   /mnt/app-secret, its `userdata` installed as /etc/aziot/config.toml, then
+   `iotedge config apply`;
+ * but idempotent on EVERY boot (systemd oneshot comparing contents), so a
+   `helm upgrade --set-file azIotEdgeConfig=...` + VM restart rotates the config;
+ * nothing is installed when the image is pre-baked (no apt on the boot path);
+ * waits for the passed-through MI355X (/dev/kfd, /dev/dri/renderD*) and records
+   boot-timing stamps for the boot-to-ready metric (kvedge_amd/utils/boottime.py).
+*/}}
+{{- define "kvedge.cloudinit" -}}
+{{- $v := .root.Values -}}
+#cloud-config
+hostname: {{ $v.guest.hostname }}{{ include "kvedge.sfx" . }}
+ssh_authorized_keys:
+  - {{ $v.publicSshKey }}
+{{- if not $v.image.prebaked }}
+apt:
+  sources:
+    microsoft-prod.list:
+      source: "deb [arch=amd64] https://packages.microsoft.com/ubuntu/{{ $v.guest.ubuntuVersion }}/prod {{ $v.guest.ubuntuCodename }} main"
+      keyid: BC528686B50D79E339D3721CEB3E94ADBE1229CF
+{{- end }}
+bootcmd:
+  - [sh, -c, "mkdir -p /mnt/app-secret /var/lib/kvedge && echo \"bootcmd $(date +%s.%N)\" >> /var/lib/kvedge/boot-timing"]
+  - [sh, -c, "mountpoint -q /mnt/app-secret || mount -o ro /dev/disk/by-id/virtio-{{ include "kvedge.secretSerial" . }} /mnt/app-secret || mount -o ro /dev/$(lsblk -dno NAME,SERIAL | awk '$2==\"{{ include "kvedge.secretSerial" . }}\"{print $1}') /mnt/app-secret"]
+write_files:
+  - path: /usr/local/sbin/kvedge-stamp
+    permissions: "0755"
+    content: |
+      #!/bin/sh
+      mkdir -p /var/lib/kvedge
+      echo "$1 $(date +%s.%N)" >> /var/lib/kvedge/boot-timing
+  - path: /usr/local/sbin/kvedge-apply-config
+    permissions: "0755"
+    content: |
+      #!/bin/sh
+      # Install /mnt/app-secret/userdata as /etc/aziot/config.toml when it changed,
+      # then `iotedge config apply`.  Safe to run on every boot.
+      set -eu
+      src=/mnt/app-secret/userdata
+      dst=/etc/aziot/config.toml
+      [ -s "$src" ] || { echo "kvedge: no config on secret disk"; exit 0; }
+      mkdir -p /etc/aziot
+      if [ ! -f "$dst" ] || ! cmp -s "$src" "$dst"; then
+        install -m 0600 "$src" "$dst"
+        if command -v iotedge >/dev/null 2>&1; then iotedge config apply -c "$dst"; fi
+      fi
+      /usr/local/sbin/kvedge-stamp config_applied
+  - path: /usr/local/sbin/kvedge-gpu-check
+    permissions: "0755"
+    content: |
+      #!/bin/sh
+      # Wait for the VFIO-passed MI355X to be bound by amdgpu inside the guest.
+      want=${1:-1}; wait_s=${2:-120}; t=0
+      while [ "$t" -lt "$wait_s" ]; do
+        n=$(ls /dev/dri/renderD* 2>/dev/null | wc -l)
+        if [ "$want" -eq 0 ] || { [ -e /dev/kfd ] && [ "$n" -ge "$want" ]; }; then
+          echo "{\"kfd\": $([ -e /dev/kfd ] && echo true || echo false), \"render_nodes\": $n, \"wanted\": $want, \"waited_s\": $t}" > /var/lib/kvedge/gpu.json
+          /usr/local/sbin/kvedge-stamp gpu_ready
+          exit 0
+        fi
+        sleep 1; t=$((t+1))
+      done
+      echo "{\"kfd\": false, \"render_nodes\": $n, \"wanted\": $want, \"waited_s\": $t, \"error\": \"timeout\"}" > /var/lib/kvedge/gpu.json
+      exit 1
+  - path: /etc/systemd/system/kvedge-config.service
+    content: |
+      [Unit]
+      Description=kvedge: apply IoT Edge config.toml from the secret disk
+      After=local-fs.target network-online.target
+      Wants=network-online.target
+      [Service]
+      Type=oneshot
+      ExecStart=/usr/local/sbin/kvedge-apply-config
+      RemainAfterExit=yes
+      [Install]
+      WantedBy=multi-user.target
+runcmd:
+{{- if not $v.image.prebaked }}
+  - [sh, -c, "apt-get update && apt-get install -y moby-engine && apt-get install -y aziot-edge"]
+{{- end }}
+  - [sh, -c, "getent group render >/dev/null && getent passwd iotedge >/dev/null && usermod -aG video,render iotedge || true"]
+  - [systemctl, daemon-reload]
+  - [systemctl, enable, --now, kvedge-config.service]
+  - [/usr/local/sbin/kvedge-gpu-check, "{{ $v.gpu.count }}", "{{ $v.guest.gpuWaitSeconds }}"]
+  - [/usr/local/sbin/kvedge-stamp, runcmd_done]
+final_message: "kvedge guest {{ $v.guest.hostname }}{{ include "kvedge.sfx" . }} up after $UPTIME s"
+{{- end -}}
