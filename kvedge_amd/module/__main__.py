@@ -1,0 +1,61 @@
+"""`python -m kvedge_amd.module` -- the IoT Edge module entry point (also bare-metal).
+
+Inside IoT Edge: --transport azure (twin/methods/outputs via edgeHub).  Outside:
+--transport stdout prints telemetry as JSON lines; CLI flags mirror the twin keys
+ and are overridden by the twin's desired properties.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import sys
+
+from .. import parallel
+from .app import ModuleApp
+from .config import ModuleConfig
+from .transport import make_transport
+
+
+def main(argv=None):
+    d = ModuleConfig()
+    ap = argparse.ArgumentParser(prog="kvedge-module")
+    ap.add_argument("--transport", default=os.environ.get("KVEDGE_TRANSPORT", "stdout"),
+                    choices=["stdout", "fake", "azure"])
+    ap.add_argument("--model", default=os.environ.get("KVEDGE_MODEL", d.model))
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("KVEDGE_BATCH", d.batch)))
+    ap.add_argument("--dtype", default=os.environ.get("KVEDGE_DTYPE", d.dtype))
+    ap.add_argument("--seed", type=int, default=d.seed)
+    ap.add_argument("--report-interval-s", type=float, default=d.report_interval_s)
+    ap.add_argument("--image-size", type=int, default=d.image_size)
+    ap.add_argument("--fps", type=float, default=d.fps)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--steps", type=int, default=None, help="stop after N steps")
+    ap.add_argument("--duration-s", type=float, default=None)
+    ap.add_argument("--state", default=os.environ.get("KVEDGE_STATE", "/var/lib/kvedge/module-state.json"))
+    a = ap.parse_args(argv)
+    di = parallel.init_from_env(prefer_gpu=True)
+    cfg = ModuleConfig(model=a.model, batch=a.batch, dtype=a.dtype, seed=a.seed,
+                       report_interval_s=a.report_interval_s, image_size=a.image_size,
+                       fps=a.fps, use_graph=not a.no_graph, world_size=di.world_size).validate()
+    app = ModuleApp(make_transport(a.transport), cfg, state_path=a.state)
+    stop = {"flag": False}
+    signal.signal(signal.SIGTERM, lambda *_: stop.update(flag=True))
+    app.start()
+    try:
+        n = 0
+        while not stop["flag"] and (a.steps is None or n < a.steps):
+            app.run(max_steps=1)
+            n += 1
+            if a.duration_s is not None and n and app.clock() - app._win_t0 > a.duration_s:
+                break
+        if app.engine is not None:
+            app.report()
+    finally:
+        app.stop()
+        parallel.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,192 @@
+"""IoT Edge module transport abstraction.
+
+The module talks to edgeHub (module twin, telemetry outputs, direct methods).
+Three implementations:
+  * AzureIoTTransport -- azure-iot-device's IoTHubModuleClient from the IoT Edge
+    environment (only inside a real edge runtime; the package is optional and is
+    not installed here, so it is imported lazily and fails with a clear message);
+  * FakeTransport     -- in-process hub for tests: records messages and reported
+    properties, lets tests push twin patches and invoke direct methods;
+  * StdoutTransport   -- JSON lines on stdout for bare-metal/bench runs.
+"""
+from __future__ import annotations
+
+import json
+import queue
+import sys
+import threading
+import time
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+TwinHandler = Callable[[Dict[str, Any]], None]
+MethodHandler = Callable[[str, Dict[str, Any]], Tuple[int, Dict[str, Any]]]
+
+
+class Transport:
+    def connect(self) -> None:
+        pass
+
+    def disconnect(self) -> None:
+        pass
+
+    def get_desired(self) -> Dict[str, Any]:
+        return {}
+
+    def patch_reported(self, props: Dict[str, Any]) -> None:
+        raise NotImplementedError
+
+    def send_message(self, output: str, payload: Dict[str, Any]) -> None:
+        raise NotImplementedError
+
+    def set_twin_patch_handler(self, cb: TwinHandler) -> None:
+        self._twin_cb = cb
+
+    def set_method_handler(self, cb: MethodHandler) -> None:
+        self._method_cb = cb
+
+    def poll(self) -> None:
+        """Deliver pending twin patches / method calls on the caller's thread."""
+
+
+class FakeTransport(Transport):
+    """In-process stand-in for edgeHub.  Thread-safe; events are delivered from
+    ``poll()`` so the module loop stays single-threaded (no races with the GPU)."""
+
+    def __init__(self, desired: Optional[Dict[str, Any]] = None):
+        self.desired: Dict[str, Any] = dict(desired or {})
+        self.reported: Dict[str, Any] = {}
+        self.messages: List[Tuple[str, Dict[str, Any]]] = []
+        self.method_results: List[Tuple[str, int, Dict[str, Any]]] = []
+        self.connected = False
+        self._events: "queue.Queue" = queue.Queue()
+        self._lock = threading.Lock()
+        self._twin_cb: Optional[TwinHandler] = None
+        self._method_cb: Optional[MethodHandler] = None
+
+    def connect(self):
+        self.connected = True
+
+    def disconnect(self):
+        self.connected = False
+
+    def get_desired(self):
+        with self._lock:
+            return dict(self.desired)
+
+    def patch_reported(self, props):
+        with self._lock:
+            self.reported.update(json.loads(json.dumps(props)))
+
+    def send_message(self, output, payload):
+        if not self.connected:
+            raise RuntimeError("transport not connected")
+        with self._lock:
+            self.messages.append((output, json.loads(json.dumps(payload))))
+
+    # --- test-side API ----------------------------------------------------
+    def push_twin_patch(self, patch: Dict[str, Any]):
+        with self._lock:
+            self.desired.update(patch)
+        self._events.put(("twin", patch))
+
+    def invoke_method(self, name: str, payload: Optional[Dict[str, Any]] = None):
+        self._events.put(("method", (name, payload or {})))
+
+    def poll(self):
+        while True:
+            try:
+                kind, data = self._events.get_nowait()
+            except queue.Empty:
+                return
+            if kind == "twin" and self._twin_cb:
+                self._twin_cb(data)
+            elif kind == "method" and self._method_cb:
+                status, res = self._method_cb(*data)
+                self.method_results.append((data[0], status, res))
+
+    def outputs(self, name: str) -> List[Dict[str, Any]]:
+        with self._lock:
+            return [p for o, p in self.messages if o == name]
+
+
+class StdoutTransport(Transport):
+    def __init__(self, desired: Optional[Dict[str, Any]] = None, stream=None):
+        self.desired = dict(desired or {})
+        self.stream = stream or sys.stdout
+
+    def get_desired(self):
+        return dict(self.desired)
+
+    def patch_reported(self, props):
+        self._emit({"reported": props})
+
+    def send_message(self, output, payload):
+        self._emit({"output": output, "payload": payload})
+
+    def _emit(self, obj):
+        self.stream.write(json.dumps(obj) + "\n")
+        self.stream.flush()
+
+
+class AzureIoTTransport(Transport):
+    """Real edgeHub connection via azure-iot-device (optional dependency)."""
+
+    def __init__(self):
+        try:
+            from azure.iot.device import IoTHubModuleClient, Message, MethodResponse  # noqa
+        except ImportError as e:  # pragma: no cover - not installed in CI
+            raise RuntimeError(
+                "azure-iot-device is not installed; install it in the module image or use "
+                "--transport stdout/fake") from e
+        self._Message, self._MethodResponse = Message, MethodResponse
+        self.client = IoTHubModuleClient.create_from_edge_environment()
+        self._events: "queue.Queue" = queue.Queue()
+        self._twin_cb: Optional[TwinHandler] = None
+        self._method_cb: Optional[MethodHandler] = None
+
+    def connect(self):  # pragma: no cover
+        self.client.connect()
+        self.client.on_twin_desired_properties_patch_received = \
+            lambda p: self._events.put(("twin", p))
+        self.client.on_method_request_received = lambda r: self._events.put(("method", r))
+
+    def disconnect(self):  # pragma: no cover
+        self.client.shutdown()
+
+    def get_desired(self):  # pragma: no cover
+        return self.client.get_twin().get("desired", {})
+
+    def patch_reported(self, props):  # pragma: no cover
+        self.client.patch_twin_reported_properties(props)
+
+    def send_message(self, output, payload):  # pragma: no cover
+        msg = self._Message(json.dumps(payload))
+        msg.content_type, msg.content_encoding = "application/json", "utf-8"
+        self.client.send_message_to_output(msg, output)
+
+    def poll(self):  # pragma: no cover
+        while True:
+            try:
+                kind, data = self._events.get_nowait()
+            except queue.Empty:
+                return
+            if kind == "twin" and self._twin_cb:
+                self._twin_cb(data)
+            elif kind == "method" and self._method_cb:
+                status, res = self._method_cb(data.name, data.payload or {})
+                self.client.send_method_response(
+                    self._MethodResponse.create_from_method_request(data, status, res))
+
+
+def make_transport(kind: str, desired: Optional[Dict[str, Any]] = None) -> Transport:
+    if kind == "fake":
+        return FakeTransport(desired)
+    if kind == "stdout":
+        return StdoutTransport(desired)
+    if kind == "azure":
+        return AzureIoTTransport()
+    raise ValueError(f"unknown transport {kind!r}")
+
+
+def now_iso() -> str:
+    return time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime()) + "Z"

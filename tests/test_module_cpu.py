@@ -1,0 +1,93 @@
+"""T-module: twin -> engine config, telemetry schema, direct methods,
+checkpoint/resume, all through the fake edgeHub transport on CPU."""
+import json
+
+import pytest
+
+from kvedge_amd.module.app import ModuleApp
+from kvedge_amd.module.config import ModuleConfig
+from kvedge_amd.module.transport import FakeTransport, StdoutTransport
+
+
+class Clock:
+    def __init__(self):
+        self.t = 0.0
+
+    def __call__(self):
+        self.t += 0.25
+        return self.t
+
+
+def test_config_patch_validation():
+    c = ModuleConfig()
+    c2 = c.apply_patch({"model": "yolov8n", "batch": "8", "$version": 3, "unknown": 1})
+    assert c2.model == "yolov8n" and c2.batch == 8 and c2.needs_rebuild(c)
+    assert not c2.apply_patch({"report_interval_s": 5}).needs_rebuild(c2)
+    assert c2.resolved_image_size() == 640 and c.resolved_image_size() == 224
+    for bad in ({"model": "vgg"}, {"batch": 0}, {"dtype": "fp32"}, {"image_size": 100},
+                {"conf": 2}):
+        with pytest.raises(ValueError):
+            c.apply_patch(bad)
+
+
+def test_simulated_temperature_module(tmp_path):
+    tr = FakeTransport({"model": "simulated-temperature", "send_interval_s": 1.0,
+                        "max_messages": 3})
+    app = ModuleApp(tr, device="cpu", state_path=str(tmp_path / "s.json"), clock=Clock()).start()
+    app.run(max_steps=40)
+    msgs = tr.outputs("temperatureOutput")
+    assert len(msgs) == 3  # capped like SimulatedTemperatureSensor's MessageCount
+    assert {"machine", "ambient", "timeCreated"} <= set(msgs[0])
+    assert tr.reported["config"]["model"] == "simulated-temperature"
+    app.stop()
+
+
+def test_resnet_module_twin_methods_resume(tmp_path):
+    state = str(tmp_path / "state.json")
+    tr = FakeTransport({"model": "resnet50", "batch": 1, "report_interval_s": 1.0,
+                        "image_size": 64})
+    app = ModuleApp(tr, device="cpu", state_path=state, clock=Clock()).start()
+    assert tr.reported["status"] == "running" and tr.reported["config"]["batch"] == 1
+    app.run(max_steps=6)
+    tel = tr.outputs("telemetry")
+    assert tel, "telemetry expected every report interval"
+    t = tel[-1]
+    assert {"images_per_s", "latency_ms", "total_images", "top1", "heartbeat"} <= set(t)
+    assert t["images_per_s"] > 0 and t["latency_ms"]["p99"] >= t["latency_ms"]["p50"]
+    # twin patch: invalid rejected, valid non-rebuild keeps engine, rebuild key rebuilds
+    eng = app.engine
+    tr.push_twin_patch({"batch": -5})
+    tr.push_twin_patch({"report_interval_s": 2.0})
+    app.run(max_steps=1)
+    assert "rejected" in tr.reported["lastError"] and app.engine is eng
+    tr.push_twin_patch({"batch": 2})
+    app.run(max_steps=1)
+    assert app.engine is not eng and app.cfg.batch == 2 and app.state["rebuilds"] == 1
+    # direct methods
+    tr.invoke_method("ping")
+    tr.invoke_method("benchmark", {"steps": 2, "warmup": 0})
+    tr.invoke_method("getStatus")
+    tr.invoke_method("nope")
+    app.run(max_steps=1)
+    res = {n: (s, r) for n, s, r in tr.method_results}
+    assert res["ping"][0] == 200 and res["benchmark"][0] == 200
+    assert res["benchmark"][1]["images_per_s"] > 0 and res["benchmark"][1]["batch"] == 2
+    assert res["getStatus"][1]["config"]["batch"] == 2 and res["nope"][0] == 404
+    total = app.state["total_images"]
+    app.stop()
+    saved = json.load(open(state))
+    assert saved["total_images"] == total and saved["config"]["batch"] == 2
+    # restart resumes counters from the persistent disk
+    tr2 = FakeTransport({"model": "resnet50", "batch": 1, "image_size": 64})
+    app2 = ModuleApp(tr2, device="cpu", state_path=state, clock=Clock()).start()
+    assert app2.state["restarts"] == 1 and app2.state["total_images"] == total
+    app2.stop()
+
+
+def test_stdout_transport(capsys):
+    tr = StdoutTransport({"model": "simulated-temperature"})
+    app = ModuleApp(tr, device="cpu", clock=Clock()).start()
+    app.run(max_steps=2)
+    lines = [json.loads(l) for l in capsys.readouterr().out.strip().splitlines()]
+    assert any("reported" in l for l in lines)
+    assert any(l.get("output") == "temperatureOutput" for l in lines)
