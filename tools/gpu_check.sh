@@ -31,6 +31,9 @@ for s in $STEPS; do
     base)  run torch_base 400 python tools/torch_baseline.py --graph --batch 256 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 5 --warmup 2 ;;
     sweep) run sweep 600 python tools/batch_sweep.py ;;
+    pmc)   run pmc 1000 bash tools/prof_layers.sh 256 ;;
+    rccl)  run rccl 300 ./kvedge_amd/bin/kv_rccl_bench 1024 268435456 10 bf16 ;;
+    layers64) run layers64 600 python tools/layer_bench.py --batch 64 --out $OUT/layer_bench_b64.md ;;
     layers) run layers 600 python tools/layer_bench.py ;;
   esac
 done
