@@ -192,8 +192,14 @@ void preprocess(const at::Tensor& x, at::Tensor& y, at::ArrayRef<double> mean,
   check_dev(x, "x");
   check_bf16(y, "y");
   TORCH_CHECK(x.scalar_type() == at::kByte && x.dim() == 4 && x.size(3) == 3, "kvedge: x u8 [N,H,W,3]");
-  TORCH_CHECK(y.dim() == 4 && y.size(0) == x.size(0) && y.size(1) == x.size(1) &&
-                  y.size(2) == x.size(2) && y.size(3) == 4, "kvedge: y bf16 [N,H,W,4]");
+  TORCH_CHECK(y.dim() == 4 && y.size(0) == x.size(0), "kvedge: y batch");
+  const bool s2d = y.size(3) == 16;
+  if (s2d) {
+    TORCH_CHECK(y.size(1) * 2 == x.size(1) && y.size(2) * 2 == x.size(2), "kvedge: y bf16 [N,H/2,W/2,16]");
+  } else {
+    TORCH_CHECK(y.size(1) == x.size(1) && y.size(2) == x.size(2) && y.size(3) == 4,
+                "kvedge: y bf16 [N,H,W,4] or [N,H/2,W/2,16]");
+  }
   TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "kvedge: mean/std of 3");
   float m[3], is[3];
   for (int i = 0; i < 3; ++i) {
@@ -201,8 +207,10 @@ void preprocess(const at::Tensor& x, at::Tensor& y, at::ArrayRef<double> mean,
     is[i] = (float)(1.0 / stdv[i]);
   }
   const c10::DeviceGuard g(x.device());
-  const int rc = kv_preprocess(x.data_ptr<uint8_t>(), y.data_ptr(), (int)x.size(0), (int)x.size(1),
-                               (int)x.size(2), m, is, cur_stream(x));
+  const int rc = s2d ? kv_preprocess_s2d(x.data_ptr<uint8_t>(), y.data_ptr(), (int)x.size(0),
+                                         (int)x.size(1), (int)x.size(2), m, is, cur_stream(x))
+                     : kv_preprocess(x.data_ptr<uint8_t>(), y.data_ptr(), (int)x.size(0),
+                                     (int)x.size(1), (int)x.size(2), m, is, cur_stream(x));
   TORCH_CHECK(rc == 0, "kvedge: preprocess failed rc=", rc);
 }
 

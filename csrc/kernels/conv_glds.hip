@@ -1,0 +1,309 @@
+// K1/K2/K3 v2 — implicit-GEMM conv with LDS-DMA (buffer_load ... lds) staging, gfx950.
+//
+// Second-generation main loop (the v1 register-staged kernel is conv_igemm.hip; the
+// autotuner picks per layer between both families).  What changes, and why (rocprof
+// PMC on v1: 2-3 VALU per MFMA on the 3x3 layers = VALU-issue-bound beside the
+// MFMAs, and 33-70 % of wave cycles parked on waits):
+//  * Operands go global -> LDS with buffer_load_dwordx4 ... lds: no staging VGPRs,
+//    no ds_write instructions, and the buffer descriptor's range check turns every
+//    out-of-image tap (conv padding, M/N/K tails) into zeros for free: an invalid lane
+//    just gets an offset past num_records.
+//  * Address work per K step is one scalar soffset (weights, 1x1 activations) or, for
+//    KxK convs with Cin % 64 == 0, a wave-uniform tap offset plus a per-row tap-valid
+//    bit (precomputed once): ~3 VALU per staged row instead of ~10.
+//  * v_mfma_f32_32x32x16_bf16: 32 cycles per MFMA leave 24 issue cycles for VALU/LDS
+//    (16x16x32 leaves 8), and half the LDS fragment bytes per FLOP.
+//  * LDS image [row][64] bf16, 16-B chunk c of row r stored at c ^ ((r >> 1) & 7):
+//    the DMA writes are lane-linear (swizzle applied on the SOURCE address, guide rule
+//    21) and both the 32x32x16 and 16x16x32 fragment reads are conflict-free under the
+//    ds_read_b128 lane grouping (derivation: docs/kernels.md).
+//  * 2-stage ring: K step k+1 is issued before the MFMAs of step k; one vmcnt(0) +
+//    barrier per step (guide §5.5 T3+T4 "minimum 2-phase").
+//  * Fused epilogue (bias, residual before/after act, ReLU/SiLU) staged through LDS for
+//    full-row 16-B stores, as in v1.
+#include "common.h"
+#include "kvedge_kernels.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace kvedge {
+namespace {
+
+constexpr int BK = 64;
+constexpr int kOOB = 0x7ffffff0;  // byte offset beyond every tensor: buffer load returns 0
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t rs, bf16* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      rs, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+
+// MODE 0: KxK (or strided 1x1) conv with Cin % 64 == 0 -> tap uniform per K step
+// MODE 1: 1x1 / stride 1 / pad 0 GEMM (A rows contiguous)
+// MODE 3: generic gather, Cin % 8 == 0 (per-lane tap tracking)
+template <int BM, int BN, int WM, int WN, int MODE>
+__global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p) {
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int A_INS = BM / 32;  // DMA instructions per wave per stage (8 rows each)
+  constexpr int B_INS = BN / 32;
+  constexpr int STAGE = (BM + BN) * BK;
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wv / WN, wn = wv % WN;
+  const int nbm = (p.M + BM - 1) / BM, nbn = (p.Cout + BN - 1) / BN;
+  const int t = xcd_remap(blockIdx.x, nbm * nbn);
+  const int m0 = (t / nbn) * BM, n0 = (t % nbn) * BN;
+
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, p.N * p.H * p.W * p.ldx * 2);
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w, p.Cout * p.Kpad * 2);
+
+  // ---- per-lane source descriptors (constant over the K loop) -------------
+  const int lrow = lane >> 3, pch = lane & 7;
+  int a_off[A_INS];   // MODE 0: pixel-row base offset (elements); MODE 1: full byte offset
+  unsigned a_msk[A_INS];
+  int a_lc[A_INS];
+  int a_h0[A_INS], a_w0[A_INS];  // MODE 3
+  const int HoWo = p.Ho * p.Wo;
+#pragma unroll
+  for (int i = 0; i < A_INS; ++i) {
+    const int row = (wv * A_INS + i) * 8 + lrow;
+    const int lc = pch ^ ((row >> 1) & 7);
+    a_lc[i] = lc;
+    const int m = m0 + row;
+    a_msk[i] = 0u;
+    a_h0[i] = -(1 << 28);
+    a_w0[i] = -(1 << 28);
+    if (MODE == 1) {
+      a_off[i] = m < p.M ? (m * p.ldx + p.x_coff + lc * 8) * 2 : kOOB;
+    } else {
+      a_off[i] = 0;
+      if (m < p.M) {
+        const int img = m / HoWo;
+        const int rem = m - img * HoWo;
+        const int ho = rem / p.Wo, wo = rem - (rem / p.Wo) * p.Wo;
+        const int h0 = ho * p.stride - p.pad, w0 = wo * p.stride - p.pad;
+        a_h0[i] = h0;
+        a_w0[i] = w0;
+        a_off[i] = ((img * p.H + h0) * p.W + w0) * p.ldx + p.x_coff + lc * 8;  // may be < 0
+        if (MODE == 0) {
+          unsigned msk = 0;
+          for (int r = 0; r < p.KH; ++r)
+            for (int s = 0; s < p.KW; ++s)
+              if ((unsigned)(h0 + r) < (unsigned)p.H && (unsigned)(w0 + s) < (unsigned)p.W)
+                msk |= 1u << (r * p.KW + s);
+          a_msk[i] = msk;
+        }
+      }
+    }
+  }
+  int b_off[B_INS];
+#pragma unroll
+  for (int i = 0; i < B_INS; ++i) {
+    const int row = (wv * B_INS + i) * 8 + lrow;
+    const int lc = pch ^ ((row >> 1) & 7);
+    const int n = n0 + row;
+    b_off[i] = n < p.Cout ? (n * p.Kpad + lc * 8) * 2 : kOOB;
+  }
+  // MODE 3 per-lane incremental tap state, one per A instruction (lc differs per row)
+  int g_tap[A_INS], g_c[A_INS];
+  if (MODE == 3) {
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i) {
+      int c = a_lc[i] * 8, tap = 0;
+      while (c >= p.Cin) { c -= p.Cin; ++tap; }
+      g_tap[i] = tap;
+      g_c[i] = c;
+    }
+  }
+
+  auto issue = [&](int stage, int kt) {
+    bf16* As = smem + stage * STAGE;
+    bf16* Bs = As + BM * BK;
+    if (MODE == 1) {
+      const int kbase = kt * BK;
+#pragma unroll
+      for (int i = 0; i < A_INS; ++i) {
+        const int v = (kbase + a_lc[i] * 8 < p.Cin) ? a_off[i] : kOOB;
+        glds16(rx, As + (wv * A_INS + i) * 512, v, kbase * 2);
+      }
+    } else if (MODE == 0) {
+      const int k0 = kt * BK;
+      const int tap = k0 / p.Cin;           // wave-uniform
+      const int c0 = k0 - tap * p.Cin;
+      const int r = tap / p.KW, s = tap - (tap / p.KW) * p.KW;
+      const int toff = (r * p.W + s) * p.ldx + c0;  // elements, wave-uniform
+#pragma unroll
+      for (int i = 0; i < A_INS; ++i) {
+        // a_off may be negative (top/left padding rows); only valid taps form an address
+        const bool ok = tap < p.KH * p.KW && ((a_msk[i] >> tap) & 1u);
+        const int v = ok ? (a_off[i] + toff) * 2 : kOOB;
+        glds16(rx, As + (wv * A_INS + i) * 512, v, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_INS; ++i) {
+        const int tap = g_tap[i];
+        const int r = tap / p.KW, s = tap - (tap / p.KW) * p.KW;
+        const int hi = a_h0[i] + r, wi = a_w0[i] + s;
+        const bool ok = tap < p.KH * p.KW && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
+        const int v = ok ? (a_off[i] - a_lc[i] * 8 + (r * p.W + s) * p.ldx + g_c[i]) * 2 : kOOB;
+        glds16(rx, As + (wv * A_INS + i) * 512, v, 0);
+        int c = g_c[i] + BK;
+        while (c >= p.Cin) { c -= p.Cin; ++g_tap[i]; }
+        g_c[i] = c;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i) glds16(rw, Bs + (wv * B_INS + i) * 512, b_off[i], kt * BK * 2);
+  };
+
+  floatx16 acc[TN][TM];
+#pragma unroll
+  for (int a = 0; a < TN; ++a)
+#pragma unroll
+    for (int b = 0; b < TM; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  const int fr = lane & 31, fh = lane >> 5;
+  auto compute = [&](int stage) {
+    const bf16* As = smem + stage * STAGE;
+    const bf16* Bs = As + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int q = ks * 2 + fh;
+      bf16x8 af[TM], bfg[TN];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int row = wm * WTM + tm * 32 + fr;
+        af[tm] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((q ^ ((row >> 1) & 7)) << 3));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = wn * WTN + tn * 32 + fr;
+        bfg[tn] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((q ^ ((row >> 1) & 7)) << 3));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+          acc[tn][tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfg[tn], af[tm], acc[tn][tm], 0, 0, 0);
+    }
+  };
+
+  const int nk = p.Kpad / BK;
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage `cur` landed for every wave; stage cur^1 no longer read
+    if (kt + 1 < nk) issue(cur ^ 1, kt + 1);
+    compute(cur);
+  }
+  __syncthreads();
+
+  // ---- fused epilogue through LDS (see conv_igemm.hip) ----------------------
+  constexpr int CS = BN + 8;
+  static_assert(BM * CS <= 2 * STAGE, "C tile fits");
+  const bool has_res = p.res != nullptr;
+  const int act_fn = p.act & 3;
+  const bool res_post = (p.act & 4) != 0;
+  const int act1 = (has_res && !res_post) ? kActNone : act_fn;
+  const int act2 = res_post ? kActNone : act_fn;
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int nl = wn * WTN + tn * 32 + g * 8 + fh * 4;
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p.bias && n0 + nl < p.Cout) bv = *reinterpret_cast<const float4*>(p.bias + n0 + nl);
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int ml = wm * WTM + tm * 32 + fr;
+        bf16x4 o;
+        o[0] = f2bf(apply_act(acc[tn][tm][4 * g + 0] + bv.x, act1));
+        o[1] = f2bf(apply_act(acc[tn][tm][4 * g + 1] + bv.y, act1));
+        o[2] = f2bf(apply_act(acc[tn][tm][4 * g + 2] + bv.z, act1));
+        o[3] = f2bf(apply_act(acc[tn][tm][4 * g + 3] + bv.w, act1));
+        *reinterpret_cast<bf16x4*>(smem + ml * CS + nl) = o;
+      }
+    }
+  }
+  __syncthreads();
+  bf16* __restrict__ Y = reinterpret_cast<bf16*>(p.y);
+  const bf16* __restrict__ R = reinterpret_cast<const bf16*>(p.res);
+  constexpr int CPR = BN / 8;
+  constexpr int PER = BM * CPR / 256;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int idx = tid + 256 * j;
+    const int ml = idx / CPR, ch = idx % CPR;
+    const int m = m0 + ml, n = n0 + ch * 8;
+    if (m >= p.M || n >= p.Cout) continue;
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + ml * CS + ch * 8);
+    if (has_res) {
+      const bf16x8 rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(apply_act((float)v[e] + (float)rv[e], act2));
+    }
+    *reinterpret_cast<bf16x8*>(Y + (size_t)m * p.ldy + p.y_coff + n) = v;
+  }
+}
+
+}  // namespace
+
+typedef void (*ConvKernelFn)(const KvConvParams);
+
+template <int BM, int BN, int WM, int WN>
+ConvKernelFn glds_get(int mode) {
+  switch (mode) {
+    case 0: return conv_glds_kernel<BM, BN, WM, WN, 0>;
+    case 1: return conv_glds_kernel<BM, BN, WM, WN, 1>;
+    default: return conv_glds_kernel<BM, BN, WM, WN, 3>;
+  }
+}
+
+struct GldsTile {
+  int bm, bn;
+  ConvKernelFn (*get)(int);
+};
+
+static const GldsTile kGldsTiles[] = {
+    {128, 128, &glds_get<128, 128, 2, 2>},
+    {128, 64, &glds_get<128, 64, 2, 2>},
+    {64, 64, &glds_get<64, 64, 2, 2>},
+    {256, 64, &glds_get<256, 64, 4, 1>},
+    {64, 128, &glds_get<64, 128, 2, 2>},
+    {256, 128, &glds_get<256, 128, 2, 2>},
+    {128, 256, &glds_get<128, 256, 2, 2>},
+};
+
+int glds_num_tiles() { return (int)(sizeof(kGldsTiles) / sizeof(kGldsTiles[0])); }
+
+// mode here is the caller's (0 general, 1 gemm); picks MODE 0 vs 3 by Cin and taps.
+int glds_launch(const KvConvParams* p, int tile, hipStream_t stream) {
+  if (tile < 0 || tile >= glds_num_tiles()) return -6;
+  int mode = p->mode;
+  if (mode == 2) return -8;  // legacy stem layout: v1 only
+  if (mode == 0 && (p->Cin % 64 != 0 || p->KH * p->KW > 32)) mode = 3;
+  const long long xb = (long long)p->N * p->H * p->W * p->ldx * 2;
+  const long long wb = (long long)p->Cout * p->Kpad * 2;
+  if (xb >= kOOB || wb >= kOOB) return -9;
+  const GldsTile& e = kGldsTiles[tile];
+  const long long nwg = (long long)((p->M + e.bm - 1) / e.bm) * ((p->Cout + e.bn - 1) / e.bn);
+  if (nwg <= 0) return 0;
+  hipLaunchKernelGGL(e.get(mode), dim3((unsigned)nwg), dim3(256), 0, stream, *p);
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
+int glds_tile_bm(int tile) { return kGldsTiles[tile].bm; }
+int glds_tile_bn(int tile) { return kGldsTiles[tile].bn; }
+
+}  // namespace kvedge

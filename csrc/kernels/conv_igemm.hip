@@ -300,7 +300,15 @@ constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
 using namespace kvedge;
 
-extern "C" int kv_conv_num_tiles(void) { return kNumTiles; }
+namespace kvedge {
+// v2 family (conv_glds.hip): tile indices kNumTiles .. kNumTiles + glds_num_tiles() - 1
+int glds_num_tiles();
+int glds_launch(const KvConvParams* p, int tile, hipStream_t stream);
+int glds_tile_bm(int tile);
+int glds_tile_bn(int tile);
+}  // namespace kvedge
+
+extern "C" int kv_conv_num_tiles(void) { return kNumTiles + glds_num_tiles(); }
 
 extern "C" int kv_conv_pick_tile(const KvConvParams* p) {
   // Heuristic: enough workgroups to cover 256 CUs x 2, largest tile otherwise.
@@ -324,7 +332,8 @@ extern "C" int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream) {
   if (p->mode == 1 && (p->KH != 1 || p->KW != 1 || p->stride != 1 || p->pad != 0)) return -4;
   if ((p->ldy % 8) || (p->y_coff % 8) || (p->res && ((p->ldr % 8) || (p->r_coff % 8)))) return -5;
   if (tile < 0) tile = kv_conv_pick_tile(p);
-  if (tile >= kNumTiles) return -6;
+  if (tile >= kNumTiles + glds_num_tiles()) return -6;
+  if (tile >= kNumTiles) return glds_launch(p, tile - kNumTiles, stream);
   const TileEntry& e = kTiles[tile];
   const long long nwg = (long long)((p->M + e.cfg.bm - 1) / e.cfg.bm) *
                         ((p->Cout + e.cfg.bn - 1) / e.cfg.bn);

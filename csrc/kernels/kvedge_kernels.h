@@ -73,6 +73,10 @@ int kv_synth_frames_dev(uint8_t* y, int N, int H, int W, uint64_t seed, uint64_t
 // K12: uint8 NHWC3 -> bf16 NHWC4 normalized ((x/255 - mean)/std), channel 3 = 0.
 int kv_preprocess(const uint8_t* x, void* y, int N, int H, int W, const float* mean3,
                   const float* inv_std3, hipStream_t s);
+// K12b: uint8 NHWC3 -> bf16 space-to-depth [N, H/2, W/2, 16] normalized
+//   (channel (dy*2+dx)*4 + c, c == 3 zero) for the stride-1 s2d stem conv.
+int kv_preprocess_s2d(const uint8_t* x, void* y, int N, int H, int W, const float* mean3,
+                      const float* inv_std3, hipStream_t s);
 // K4 fallback: y = x*scale[c] + shift[c] (+relu) on NHWC bf16.
 int kv_batchnorm_nhwc(const void* x, void* y, const float* scale, const float* shift,
                       int64_t rows, int C, int relu, hipStream_t s);

@@ -251,6 +251,41 @@ __global__ __launch_bounds__(kBlock) void preprocess_kernel(const uint8_t* __res
   }
 }
 
+// ---- K12b uint8 NHWC3 -> bf16 space-to-depth NHWC16 normalized ------------
+// y[n, by, bx, (dy*2+dx)*4 + c] = norm(x[n, 2by+dy, 2bx+dx, c]), c == 3 -> 0.
+// Turns a stride-2 KxK stem conv into a stride-1 ceil(K/2)-tap conv over 16
+// channels (kvedge_amd.models.layers.DeployedConv.stem_s2d): every MFMA k-chunk is
+// then one aligned 16-B load and the stem runs on the general implicit-GEMM path.
+__global__ __launch_bounds__(kBlock) void preprocess_s2d_kernel(
+    const uint8_t* __restrict__ x, bf16* __restrict__ y, int N, int H, int W, float m0,
+    float m1, float m2, float s0, float s1, float s2) {
+  const int Hs = H / 2, Ws = W / 2;
+  const long long total = (long long)N * Hs * Ws;
+  const float mm[3] = {m0, m1, m2}, ss[3] = {s0, s1, s2};
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int bx = (int)(i % Ws);
+    const long long t = i / Ws;
+    const int by = (int)(t % Hs);
+    const int n = (int)(t / Hs);
+    bf16x8 o[2];
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+      const uint8_t* p = x + (((long long)n * H + 2 * by + dy) * W + 2 * bx) * 3;
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          o[dy][dx * 4 + c] = f2bf(((float)p[dx * 3 + c] * (1.f / 255.f) - mm[c]) * ss[c]);
+        o[dy][dx * 4 + 3] = f2bf(0.f);
+      }
+    }
+    bf16x8* q = reinterpret_cast<bf16x8*>(y + i * 16);
+    q[0] = o[0];
+    q[1] = o[1];
+  }
+}
+
 // ---- K4 fallback BN / affine ------------------------------------------------
 __global__ __launch_bounds__(kBlock) void bn_kernel(const bf16* __restrict__ x,
                                                     bf16* __restrict__ y,
@@ -350,6 +385,16 @@ extern "C" int kv_preprocess(const uint8_t* x, void* y, int N, int H, int W, con
   if (pix % 2) return -1;
   hipLaunchKernelGGL(preprocess_kernel, dim3(grid_for(pix / 2)), dim3(kBlock), 0, s, x, (bf16*)y,
                      pix, mean3[0], mean3[1], mean3[2], inv_std3[0], inv_std3[1], inv_std3[2]);
+  KV_CHECK_LAUNCH();
+}
+
+extern "C" int kv_preprocess_s2d(const uint8_t* x, void* y, int N, int H, int W,
+                                 const float* mean3, const float* inv_std3, hipStream_t s) {
+  if (H % 2 || W % 2) return -1;
+  const long long work = (long long)N * (H / 2) * (W / 2);
+  hipLaunchKernelGGL(preprocess_s2d_kernel, dim3(grid_for(work)), dim3(kBlock), 0, s, x,
+                     (bf16*)y, N, H, W, mean3[0], mean3[1], mean3[2], inv_std3[0], inv_std3[1],
+                     inv_std3[2]);
   KV_CHECK_LAUNCH();
 }
 

@@ -67,6 +67,40 @@ class DeployedConv:
         return DeployedConv(spec, ops.pack_conv_weight(wf, spec).to(device),
                             bf.contiguous().to(device))
 
+    @staticmethod
+    def stem_s2d(conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d], act: int,
+                 device="cpu") -> "DeployedConv":
+        """Stride-2 KxK stem on RGB -> stride-1 ceil(K/2)... tap conv over the
+        space-to-depth input [N, H/2, W/2, 16] written by ops.preprocess(s2d=True).
+
+        out[ho] = sum_r w[r] x[2 ho - p + r].  With X'[by, dy] = x[2 by + dy] and
+        q = (p + 1) // 2:  r = 2a + dy + p - 2q, by = ho - q + a, a in [0, ka).
+        Taps with r outside [0, K) get zero weight.  Top/left pad q; bottom/right pad
+        ka - 1 - q keeps Ho = H/2.  Every 8-element MFMA k-chunk is then one aligned
+        16-B load (2 pixels x 4 channels), i.e. the general implicit-GEMM path."""
+        wf, bf = fold_bn(conv, bn)
+        cout, cin, k, _ = wf.shape
+        p, s = conv.padding[0], conv.stride[0]
+        assert s == 2 and cin <= 4 and conv.padding[0] == conv.padding[1]
+        q = (p + 1) // 2
+        ka = (k - 1 + 2 * q - p) // 2 + 1
+        w2 = torch.zeros(cout, 16, ka, ka)
+        for a in range(ka):
+            for dy in range(2):
+                r = 2 * a + dy + p - 2 * q
+                if not 0 <= r < k:
+                    continue
+                for b in range(ka):
+                    for dx in range(2):
+                        t = 2 * b + dx + p - 2 * q
+                        if not 0 <= t < k:
+                            continue
+                        ch = (dy * 2 + dx) * 4
+                        w2[:, ch:ch + cin, a, b] = wf[:, :, r, t]
+        spec = ConvSpec(16, cout, ka, ka, 1, q, act, ops.MODE_GENERAL, pad_b=ka - 1 - q)
+        return DeployedConv(spec, ops.pack_conv_weight(w2, spec).to(device),
+                            bf.contiguous().to(device))
+
     def to(self, device) -> "DeployedConv":
         return DeployedConv(self.spec, self.w.to(device), self.b.to(device), self.tile)
 
@@ -108,3 +142,27 @@ def frames_to_nchw(frames_u8: torch.Tensor, mean=ops.IMAGENET_MEAN,
     x = frames_u8.float() / 255.0
     x = (x - torch.tensor(mean, device=x.device)) / torch.tensor(std, device=x.device)
     return x.permute(0, 3, 1, 2).contiguous()
+
+
+def count_flops(module: nn.Module, input_shape) -> int:
+    """2*MAC FLOPs of every Conv2d/Linear for one forward of ``input_shape`` (NCHW),
+    evaluated on the meta device (no compute, no weights touched)."""
+    import copy
+
+    m = copy.deepcopy(module).to("meta").eval()
+    total = [0]
+
+    def hook(mod, inp, out):
+        if isinstance(mod, nn.Conv2d):
+            kh, kw = mod.kernel_size
+            total[0] += 2 * out.numel() * (mod.in_channels // mod.groups) * kh * kw
+        elif isinstance(mod, nn.Linear):
+            total[0] += 2 * out.numel() * mod.in_features
+
+    hs = [x.register_forward_hook(hook) for x in m.modules()
+          if isinstance(x, (nn.Conv2d, nn.Linear))]
+    with torch.no_grad():
+        m(torch.empty(*input_shape, device="meta"))
+    for h in hs:
+        h.remove()
+    return total[0] // input_shape[0]

@@ -19,7 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .layers import DeployedConv, calibrate_bn, frames_to_nchw
+from .layers import DeployedConv, calibrate_bn, count_flops, frames_to_nchw
 
 ACT_NONE, ACT_RELU = ops.ACT_NONE, ops.ACT_RELU
 
@@ -135,7 +135,10 @@ class KvResNet50:
     def __init__(self, ref: ResNet50Ref, device="cuda"):
         self.device = torch.device(device)
         self.num_classes = ref.num_classes
-        self.stem = DeployedConv.from_modules(ref.conv1, ref.bn1, ACT_RELU, self.device)
+        # stride-2 7x7 stem as a stride-1 4x4 conv over space-to-depth input (K12b)
+        self.stem = DeployedConv.stem_s2d(ref.conv1, ref.bn1, ACT_RELU, self.device)
+        self._flops = {}
+        self._ref = ref
         self.blocks = [DeployedBottleneck(b, self.device) for b in ref.blocks]
         fcw = ref.fc.weight.detach().float()[:, :, None, None]
         fc_conv = nn.Conv2d(2048, ref.num_classes, 1, bias=True)
@@ -155,24 +158,16 @@ class KvResNet50:
         return out + [self.fc]
 
     def flops_per_image(self, hw: int = 224) -> int:
-        """MAC-based FLOPs (2*MAC) of all convs + FC at input size hw."""
-        total = 0
-        h = hw
-        # walk spatial sizes
-        h = self.stem.spec.out_hw(h, h)[0]
-        total += self.stem.flops_per_pixel * h * h
-        h = (h + 2 - 3) // 2 + 1  # maxpool
-        for b in self.blocks:
-            total += b.c1.flops_per_pixel * h * h
-            h2 = b.c2.spec.out_hw(h, h)[0]
-            total += b.c2.flops_per_pixel * h2 * h2 + b.c3.flops_per_pixel * h2 * h2
-            if b.down is not None:
-                total += b.down.flops_per_pixel * h2 * h2
-            h = h2
-        return total + self.fc.flops_per_pixel
+        """Model FLOPs (2*MAC of all convs + FC) of the reference architecture."""
+        if hw not in self._flops:
+            self._flops[hw] = count_flops(self._ref, (1, 3, hw, hw))
+        return self._flops[hw]
+
+    def preprocess(self, frames_u8: torch.Tensor) -> torch.Tensor:
+        return ops.preprocess(frames_u8, s2d=True)
 
     def features(self, x: torch.Tensor) -> torch.Tensor:
-        """x: preprocessed bf16 NHWC4 -> final feature map [B,7,7,2048] bf16."""
+        """x: preprocessed bf16 s2d [B,112,112,16] -> final feature map [B,7,7,2048] bf16."""
         x = self.stem(x)
         x = ops.maxpool2d(x, 3, 2, 1)
         for b in self.blocks:
@@ -186,7 +181,7 @@ class KvResNet50:
         return self.fc(pooled).view(B, self.num_classes)
 
     def __call__(self, frames_u8: torch.Tensor, out: Optional[dict] = None):
-        x = ops.preprocess(frames_u8)
+        x = self.preprocess(frames_u8)
         lg = self.logits(x)
         probs, top1 = ops.softmax_rows(lg)
         return probs, top1

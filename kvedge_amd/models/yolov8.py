@@ -24,7 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .layers import DeployedConv, calibrate_bn
+from .layers import DeployedConv, calibrate_bn, count_flops
 
 ACT_SILU, ACT_NONE = ops.ACT_SILU, ops.ACT_NONE
 NC = 80
@@ -268,8 +268,10 @@ class KvYoloV8n:
         self.nc = ref.nc
         self.conf, self.iou, self.max_det = conf, iou, max_det
         d = self.device
-        self.b0, self.b1, self.b3, self.b5, self.b7 = (_dc(m, d) for m in
-                                                        (ref.b0, ref.b1, ref.b3, ref.b5, ref.b7))
+        self.b0 = DeployedConv.stem_s2d(ref.b0.conv, ref.b0.bn, ACT_SILU, d)  # K12b s2d stem
+        self.b1, self.b3, self.b5, self.b7 = (_dc(m, d) for m in (ref.b1, ref.b3, ref.b5, ref.b7))
+        self._ref = ref
+        self._flops = {}
         self.b2, self.b4, self.b6, self.b8 = (DC2f(m, d) for m in (ref.b2, ref.b4, ref.b6, ref.b8))
         self.b9 = DSPPF(ref.b9, d)
         self.h12, self.h15, self.h18, self.h21 = (DC2f(m, d) for m in
@@ -291,46 +293,16 @@ class KvYoloV8n:
         return out
 
     def flops_per_image(self, hw: int = 640) -> int:
-        return int(self._flops(hw))
+        """Model FLOPs (2*MAC of all convs) of the reference architecture."""
+        if hw not in self._flops:
+            self._flops[hw] = count_flops(self._ref, (1, 3, hw, hw))
+        return self._flops[hw]
 
-    def _flops(self, hw):
-        total = 0
-        h = hw
-        def acc(c, hin):
-            nonlocal total
-            ho = c.spec.out_hw(hin, hin)[0]
-            total += c.flops_per_pixel * ho * ho
-            return ho
-        h = acc(self.b0, h); h = acc(self.b1, h)
-        for blk in (self.b2,):
-            for c in blk.convs():
-                acc(c, h)
-        h = acc(self.b3, h); h3 = h
-        for c in self.b4.convs():
-            acc(c, h)
-        h = acc(self.b5, h); h4 = h
-        for c in self.b6.convs():
-            acc(c, h)
-        h = acc(self.b7, h); h5 = h
-        for c in self.b8.convs() + self.b9.convs():
-            acc(c, h)
-        for c in self.h12.convs():
-            acc(c, h4)
-        for c in self.h15.convs():
-            acc(c, h3)
-        acc(self.h16, h3)
-        for c in self.h18.convs():
-            acc(c, h4)
-        acc(self.h19, h4)
-        for c in self.h21.convs():
-            acc(c, h5)
-        for lv, hl in zip(self.levels, (h3, h4, h5)):
-            for c in lv.convs():
-                acc(c, hl)
-        return total
+    def preprocess(self, frames_u8: torch.Tensor) -> torch.Tensor:
+        return ops.preprocess(frames_u8, mean=(0.0, 0.0, 0.0), std=(1.0, 1.0, 1.0), s2d=True)
 
     def heads(self, x: torch.Tensor):
-        """x: preprocessed bf16 NHWC4 [N,640,640,4] -> three [N,h,w,144] head outputs."""
+        """x: preprocessed bf16 s2d [N,320,320,16] -> three [N,h,w,144] head outputs."""
         N = x.shape[0]
         dev = x.device
         bf = torch.bfloat16
@@ -360,7 +332,6 @@ class KvYoloV8n:
         return [lv(p) for lv, p in zip(self.levels, (p3, p4, p5))]
 
     def __call__(self, frames_u8: torch.Tensor):
-        x = ops.preprocess(frames_u8, mean=(0.0, 0.0, 0.0), std=(1.0, 1.0, 1.0))
-        feats = self.heads(x)
+        feats = self.heads(self.preprocess(frames_u8))
         boxes, scores, cls = ops.yolo_decode(feats, STRIDES, self.nc)
         return ops.nms(boxes, scores, cls, self.conf, self.iou, self.max_det)

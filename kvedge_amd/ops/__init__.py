@@ -101,6 +101,11 @@ class ConvSpec:
     pad: int = 0
     act: int = ACT_NONE
     mode: int = MODE_GENERAL
+    pad_b: int = -1  # bottom/right padding when asymmetric (s2d stem); -1 = same as pad
+
+    @property
+    def pad_end(self) -> int:
+        return self.pad if self.pad_b < 0 else self.pad_b
 
     @property
     def cin_eff(self) -> int:
@@ -121,8 +126,8 @@ class ConvSpec:
         return (self.K + BK - 1) // BK * BK
 
     def out_hw(self, h: int, w: int):
-        return ((h + 2 * self.pad - self.kh) // self.stride + 1,
-                (w + 2 * self.pad - self.kw) // self.stride + 1)
+        p = self.pad + self.pad_end
+        return ((h + p - self.kh) // self.stride + 1, (w + p - self.kw) // self.stride + 1)
 
     @staticmethod
     def auto(cin, cout, k, stride=1, pad=None, act=ACT_NONE) -> "ConvSpec":
@@ -298,10 +303,13 @@ IMAGENET_STD = (0.229, 0.224, 0.225)
 
 
 def preprocess(x: torch.Tensor, out: Optional[torch.Tensor] = None, mean=IMAGENET_MEAN,
-               std=IMAGENET_STD) -> torch.Tensor:
+               std=IMAGENET_STD, s2d: bool = False) -> torch.Tensor:
+    """uint8 NHWC3 frames -> normalized bf16, either NHWC4 (channel 3 zero) or, with
+    ``s2d``, space-to-depth [N, H/2, W/2, 16] (channel (dy*2+dx)*4 + c)."""
     N, H, W, _ = x.shape
     if out is None:
-        out = torch.empty(N, H, W, 4, dtype=torch.bfloat16, device=x.device)
+        shape = (N, H // 2, W // 2, 16) if s2d else (N, H, W, 4)
+        out = torch.empty(shape, dtype=torch.bfloat16, device=x.device)
     if x.is_cuda:
         _native().preprocess(x, out, list(mean), list(std))
     else:

@@ -27,7 +27,8 @@ def conv2d(x, spec, w, bias, res, out, x_coff=0, y_coff=0, r_coff=0):
     if spec.mode == MODE_STEM:
         xin = xin[..., :spec.cin]
     wt = unpack_conv_weight(w, spec).to(xin.device)
-    y = F.conv2d(xin.permute(0, 3, 1, 2), wt, None, spec.stride, spec.pad).permute(0, 2, 3, 1)
+    xp = F.pad(xin.permute(0, 3, 1, 2), (spec.pad, spec.pad_end, spec.pad, spec.pad_end))
+    y = F.conv2d(xp, wt, None, spec.stride, 0).permute(0, 2, 3, 1)
     if bias is not None:
         y = y + bias.float()
     act, post = spec.act & 3, bool(spec.act & 4)
@@ -153,6 +154,11 @@ def preprocess(x, out, mean, std):
     m = torch.tensor(mean, dtype=torch.float32)
     s = torch.tensor(std, dtype=torch.float32)
     y = (xf - m) * (1.0 / s)
-    out.zero_()
-    out[..., :3] = y.to(out.dtype)
+    y4 = torch.zeros(*y.shape[:3], 4, dtype=torch.float32)
+    y4[..., :3] = y
+    if out.shape[-1] == 16:  # space-to-depth: channel (dy*2+dx)*4 + c
+        N, H, W, _ = y4.shape
+        y4 = y4.view(N, H // 2, 2, W // 2, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(
+            N, H // 2, W // 2, 16)
+    out.copy_(y4.to(out.dtype))
     return out

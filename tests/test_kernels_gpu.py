@@ -82,10 +82,28 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale + 0.02
 
 
-@pytest.mark.parametrize("tile", list(range(6)))
-def test_conv_every_tile(tile):
-    err, scale = _conv_case(2, 30, 30, 128, 192, 3, 1, 1, ops.ACT_RELU, res=True, tile=tile)
-    assert err <= 0.02 * scale + 0.02, (tile, err)
+N_TILES = 13  # v1 register-staged (0-5) + v2 LDS-DMA (6-12); checked below
+
+
+def test_tile_count():
+    assert int(torch.ops.kvedge.conv_num_tiles()) == N_TILES
+
+
+@pytest.mark.parametrize("tile", list(range(N_TILES)))
+@pytest.mark.parametrize("case", [
+    # (N, H, W, cin, cout, k, stride, pad, act, res, ldx_extra, x_coff)
+    (2, 30, 30, 128, 192, 3, 1, 1, ops.ACT_RELU, True, 0, 0),     # KxK, Cin % 64 == 0
+    (2, 17, 17, 64, 128, 1, 1, 0, ops.ACT_NONE, False, 32, 16),   # 1x1 GEMM from a slice
+    (2, 23, 23, 256, 64, 1, 2, 0, ops.ACT_NONE, False, 0, 0),     # strided 1x1
+    (2, 20, 20, 48, 80, 3, 2, 1, ops.ACT_SILU, False, 0, 0),      # generic gather Cin=48
+    (1, 9, 9, 16, 64, 4, 1, 2, ops.ACT_RELU, False, 0, 0),        # s2d-stem-like Cin=16 4x4
+    (3, 1, 1, 192, 136, 1, 1, 0, ops.ACT_NONE, False, 0, 0),      # K/N tails (Kpad > K)
+])
+def test_conv_every_tile(tile, case):
+    N, H, W, cin, cout, k, s, p, act, res, lx, xc = case
+    err, scale = _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
+                            tile=tile)
+    assert err <= 0.02 * scale + 0.02, (tile, case, err, scale)
 
 
 def test_conv_identity_asymmetric():

@@ -39,7 +39,7 @@ def test_resnet50_cpu_deployed_vs_module():
     fr = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8,
                        generator=torch.Generator().manual_seed(3))
     with torch.no_grad():
-        lg = kv.logits(ops.preprocess(fr)).float()
+        lg = kv.logits(kv.preprocess(fr)).float()
         lr = ref(frames_to_nchw(fr))
     cos = nn.functional.cosine_similarity(lg.flatten(), lr.flatten(), dim=0)
     assert cos > 0.98, float(cos)
@@ -72,7 +72,7 @@ def test_yolov8n_cpu_structure_and_parity():
     fr = torch.randint(0, 256, (1, 256, 256, 3), dtype=torch.uint8,
                        generator=torch.Generator().manual_seed(2))
     with torch.no_grad():
-        hk = kv.heads(ops.preprocess(fr, mean=(0, 0, 0), std=(1, 1, 1)))
+        hk = kv.heads(kv.preprocess(fr))
         hr = ref(frames_to_yolo(fr))
     for k, r in zip(hk, hr):
         assert k.shape == r.permute(0, 2, 3, 1).shape

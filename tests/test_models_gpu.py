@@ -26,8 +26,8 @@ def test_resnet50_parity(resnet):
     ref, kv, kv_cpu = resnet
     fr = _frames(3, 1)
     with torch.no_grad():
-        lg_gpu = kv.logits(ops.preprocess(fr.cuda())).float().cpu()
-        lg_cpu = kv_cpu.logits(ops.preprocess(fr)).float()
+        lg_gpu = kv.logits(kv.preprocess(fr.cuda())).float().cpu()
+        lg_cpu = kv_cpu.logits(kv_cpu.preprocess(fr)).float()
         lg_ref = ref(frames_to_nchw(fr)).float()
     cos_dep = torch.nn.functional.cosine_similarity(lg_gpu.flatten(), lg_cpu.flatten(), dim=0)
     cos_ref = torch.nn.functional.cosine_similarity(lg_gpu.flatten(), lg_ref.flatten(), dim=0)
@@ -68,8 +68,8 @@ def test_yolov8n_parity(yolo):
     ref, kv, kv_cpu = yolo
     fr = _frames(2, 5, hw=320)
     with torch.no_grad():
-        hg = kv.heads(ops.preprocess(fr.cuda(), mean=(0, 0, 0), std=(1, 1, 1)))
-        hc = kv_cpu.heads(ops.preprocess(fr, mean=(0, 0, 0), std=(1, 1, 1)))
+        hg = kv.heads(kv.preprocess(fr.cuda()))
+        hc = kv_cpu.heads(kv_cpu.preprocess(fr))
         hr = ref(frames_to_yolo(fr))
     for g, c, r in zip(hg, hc, hr):
         g = g.float().cpu()
@@ -88,7 +88,7 @@ def test_yolov8n_pipeline_graph(yolo):
     assert int(cnt.max()) <= 300 and int(cnt.min()) >= 0
     # NMS on the same decoded boxes: GPU kernel == CPU reference
     frames = eng.frames.clone()
-    x = ops.preprocess(frames, mean=(0, 0, 0), std=(1, 1, 1))
+    x = kv.preprocess(frames)
     b, s, c = ops.yolo_decode(kv.heads(x), (8, 16, 32), 80)
     o_g, n_g = ops.nms(b, s, c, 0.05, 0.7, 300)
     o_c, n_c = ops.nms(b.cpu(), s.cpu(), c.cpu(), 0.05, 0.7, 300)
