@@ -37,6 +37,10 @@ def main(argv=None):
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "yolov8n"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-autotune", action="store_true")
+    ap.add_argument("--microbatch", type=int, default=int(os.environ.get("KVEDGE_MICROBATCH", 0)),
+                    help="ResNet-50: run the first --mb-blocks bottlenecks in micro-batches "
+                         "(Infinity-Cache residency); 0 = off")
+    ap.add_argument("--mb-blocks", type=int, default=int(os.environ.get("KVEDGE_MB_BLOCKS", 3)))
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
@@ -57,6 +61,7 @@ def main(argv=None):
         from kvedge_amd.models.resnet import KvResNet50
 
         model = KvResNet50.build(seed=a.seed, device=di.device)
+        model.microbatch, model.microbatch_blocks = a.microbatch, a.mb_blocks
         hw = KvResNet50.image_size
     else:
         from kvedge_amd.models.yolov8 import KvYoloV8n
@@ -115,6 +120,8 @@ def main(argv=None):
             "image_size": hw,
             "parallelism": f"dp{world}",
             "hip_graph": eng.graph is not None,
+            "microbatch": getattr(model, "microbatch", 0),
+            "mb_blocks": getattr(model, "microbatch_blocks", 0),
         },
         "extra": {
             "tflops_per_gpu": round(value / world * flops / 1e12, 2) if flops else None,

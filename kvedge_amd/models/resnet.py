@@ -117,11 +117,16 @@ class DeployedBottleneck:
             self.down = DeployedConv.from_modules(b.downsample[0], b.downsample[1], ACT_NONE,
                                                   device)
 
-    def __call__(self, x):
+    def __call__(self, x, out=None):
         idt = x if self.down is None else self.down(x)
         y = self.c1(x)
         y = self.c2(y)
-        return self.c3(y, res=idt)
+        return self.c3(y, res=idt, out=out)
+
+    def out_shape(self, x_shape):
+        N, H, W, _ = x_shape
+        Ho, Wo = self.c2.spec.out_hw(H, W)
+        return (N, Ho, Wo, self.c3.spec.cout)
 
     def convs(self):
         return [c for c in (self.c1, self.c2, self.c3, self.down) if c is not None]
@@ -166,11 +171,36 @@ class KvResNet50:
     def preprocess(self, frames_u8: torch.Tensor) -> torch.Tensor:
         return ops.preprocess(frames_u8, s2d=True)
 
+    # Early, memory-bound stages run in micro-batches so their activations stay resident
+    # in the 256 MiB Infinity Cache between layers (a 256-image layer1 tensor is 411 MB,
+    # a 32-image one 51 MB); the compute-bound late stages run on the whole batch.
+    microbatch: int = 0          # 0 = off
+    microbatch_blocks: int = 3   # bottlenecks (from the start) run per micro-batch
+
     def features(self, x: torch.Tensor) -> torch.Tensor:
         """x: preprocessed bf16 s2d [B,112,112,16] -> final feature map [B,7,7,2048] bf16."""
-        x = self.stem(x)
-        x = ops.maxpool2d(x, 3, 2, 1)
-        for b in self.blocks:
+        B = x.shape[0]
+        mb = self.microbatch
+        nb = self.microbatch_blocks
+        if mb and B > mb and B % mb == 0 and nb > 0:
+            full = None
+            for i in range(0, B, mb):
+                y = self.stem(x[i:i + mb])
+                y = ops.maxpool2d(y, 3, 2, 1)
+                for b in self.blocks[:nb - 1]:
+                    y = b(y)
+                last = self.blocks[nb - 1]
+                if full is None:
+                    shp = last.out_shape(y.shape)
+                    full = torch.empty((B,) + shp[1:], dtype=y.dtype, device=y.device)
+                last(y, out=full[i:i + mb])  # write straight into the full-batch tensor
+            x = full
+            rest = self.blocks[nb:]
+        else:
+            x = self.stem(x)
+            x = ops.maxpool2d(x, 3, 2, 1)
+            rest = self.blocks
+        for b in rest:
             x = b(x)
         return x
 

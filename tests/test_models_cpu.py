@@ -95,3 +95,16 @@ def test_residual_after_activation_flag():
                                 None, 1, 1).permute(0, 2, 3, 1)
     ref = nn.functional.silu(conv) + r.float()
     assert (y.float() - ref).abs().max() < 0.05
+
+
+def test_resnet50_microbatch_equivalence():
+    ref = init_resnet50(seed=1, calibrate=False)
+    kv = KvResNet50(ref, "cpu")
+    fr = torch.randint(0, 256, (4, 64, 64, 3), dtype=torch.uint8,
+                       generator=torch.Generator().manual_seed(4))
+    with torch.no_grad():
+        x = kv.preprocess(fr)
+        full = kv.features(x).float()
+        kv.microbatch, kv.microbatch_blocks = 2, 4
+        micro = kv.features(x).float()
+    assert torch.equal(full, micro)

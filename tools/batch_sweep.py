@@ -1,5 +1,9 @@
 #!/usr/bin/env python3
-"""Per-GPU batch sweep of the headline ResNet-50 step (hipGraph), one process."""
+"""Sweep of the headline ResNet-50 step (hipGraph, autotuned tiles) over per-GPU batch
+and early-stage micro-batching, one process.
+
+  --configs "256:0:0,256:64:3"   batch:microbatch:microbatch_blocks
+"""
 import argparse
 import json
 import os
@@ -10,9 +14,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batches", default="32,64,128,192,256,384,512")
+    ap.add_argument("--configs", default="64:0:0,128:0:0,256:0:0,512:0:0,256:64:3,256:32:3,"
+                                          "256:64:7,256:32:7,512:64:3,512:64:7")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--out", default="gpurun_out/sweep.jsonl")
     a = ap.parse_args()
     import torch
     from kvedge_amd import ops
@@ -24,16 +30,20 @@ def main():
     else:
         from kvedge_amd.models.yolov8 import KvYoloV8n as M
     model = M.build(seed=0, device="cuda")
-    res = []
-    for b in [int(x) for x in a.batches.split(",")]:
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    for cfg in a.configs.split(","):
+        b, mb, nb = (int(v) for v in cfg.split(":"))
+        if hasattr(model, "microbatch"):
+            model.microbatch, model.microbatch_blocks = mb, nb
         eng = InferenceEngine(model, b, M.image_size, device="cuda").prepare(warmup=2)
         for _ in range(3):
             eng.run()
         dt = eng.run_timed(a.steps)
-        r = {"model": a.model, "batch": b, "images_per_s": round(b * a.steps / dt, 1),
-             "ms_per_step": round(dt / a.steps * 1e3, 3)}
+        r = {"model": a.model, "batch": b, "microbatch": mb, "mb_blocks": nb,
+             "images_per_s": round(b * a.steps / dt, 1), "ms_per_step": round(dt / a.steps * 1e3, 3)}
         print(json.dumps(r), flush=True)
-        res.append(r)
+        with open(a.out, "a") as f:
+            f.write(json.dumps(r) + "\n")
         del eng
         torch.cuda.empty_cache()
 

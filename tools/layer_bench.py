@@ -31,7 +31,7 @@ def main():
     # (name, conv, H_in, has_res)
     layers = []
     h = 224
-    layers.append(("stem", kv.stem, h, False))
+    layers.append(("stem", kv.stem, h // 2, False))  # s2d stem runs on the 112x112x16 input
     h = 56
     seen = set()
     for i, b in enumerate(kv.blocks):
