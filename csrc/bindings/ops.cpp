@@ -73,6 +73,50 @@ void conv(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
   TORCH_CHECK(rc == 0, "kvedge: kv_conv2d failed rc=", rc);
 }
 
+// Bottleneck conv3 with the downsample branch folded in as extra K (mode 4):
+//   y = act( x1 (1x1) . W[:, :K1]  +  x2 (1x1, stride s2) . W[:, K1:]  + bias )
+void conv_dual(const at::Tensor& x1, const at::Tensor& x2, const at::Tensor& w,
+               const c10::optional<at::Tensor>& bias, at::Tensor& y, int64_t stride2,
+               int64_t act, int64_t tile) {
+  check_bf16(x1, "x1");
+  check_bf16(x2, "x2");
+  check_bf16(w, "w");
+  check_bf16(y, "y");
+  TORCH_CHECK(x1.dim() == 4 && x2.dim() == 4 && y.dim() == 4, "kvedge: NHWC tensors");
+  const int64_t N = x1.size(0), Ho = x1.size(1), Wo = x1.size(2), K1 = x1.size(3);
+  const int64_t K2 = x2.size(3), Cout = y.size(3);
+  TORCH_CHECK(x2.size(0) == N && (x2.size(1) + stride2 - 1) / stride2 == Ho &&
+                  (x2.size(2) + stride2 - 1) / stride2 == Wo, "kvedge: x2 geometry vs stride");
+  TORCH_CHECK(y.size(0) == N && y.size(1) == Ho && y.size(2) == Wo, "kvedge: y shape");
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == Cout && w.size(1) == K1 + K2, "kvedge: w [Cout, K1+K2]");
+  TORCH_CHECK(K1 % 64 == 0 && K2 % 64 == 0, "kvedge: K1, K2 multiples of 64");
+  const c10::DeviceGuard g(x1.device());
+  KvConvParams p{};
+  p.x = x1.data_ptr();
+  p.w = w.data_ptr();
+  p.bias = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_dev(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= Cout, "kvedge: bias fp32[Cout]");
+    p.bias = bias->data_ptr<float>();
+  }
+  p.res = nullptr;
+  p.y = y.data_ptr();
+  p.N = (int)N; p.H = (int)Ho; p.W = (int)Wo; p.Cin = (int)K1; p.ldx = (int)K1; p.x_coff = 0;
+  p.Ho = (int)Ho; p.Wo = (int)Wo; p.Cout = (int)Cout;
+  p.KH = 1; p.KW = 1; p.stride = 1; p.pad = 0;
+  p.K = (int)(K1 + K2); p.Kpad = (int)(K1 + K2);
+  p.M = (int)(N * Ho * Wo);
+  p.ldy = (int)Cout; p.y_coff = 0; p.ldr = 0; p.r_coff = 0;
+  p.act = (int)act; p.mode = 4;
+  p.x2 = x2.data_ptr(); p.K1 = (int)K1; p.H2 = (int)x2.size(1); p.W2 = (int)x2.size(2);
+  p.ldx2 = (int)K2; p.stride2 = (int)stride2;
+  TORCH_CHECK(x1.numel() < (1ll << 30) && x2.numel() < (1ll << 30) && y.numel() < (1ll << 31),
+              "kvedge: tensor too large for 32-bit buffer offsets");
+  const int rc = kv_conv2d(&p, (int)tile, cur_stream(x1));
+  TORCH_CHECK(rc == 0, "kvedge: conv_dual failed rc=", rc);
+}
+
 void maxpool2d(const at::Tensor& x, at::Tensor& y, int64_t N, int64_t H, int64_t W, int64_t C,
                int64_t ldx, int64_t x_coff, int64_t ldy, int64_t y_coff, int64_t k, int64_t stride, int64_t pad,
                int64_t Ho, int64_t Wo) {
@@ -239,6 +283,8 @@ TORCH_LIBRARY(kvedge, m) {
   m.def("conv(Tensor x, Tensor w, Tensor? bias, Tensor? res, Tensor(a!) y, int N, int H, int W, "
         "int Cin, int ldx, int x_coff, int Ho, int Wo, int Cout, int KH, int KW, int stride, "
         "int pad, int K, int ldy, int y_coff, int ldr, int r_coff, int act, int mode, int tile) -> ()");
+  m.def("conv_dual(Tensor x1, Tensor x2, Tensor w, Tensor? bias, Tensor(a!) y, int stride2, int act, "
+        "int tile) -> ()");
   m.def("maxpool2d(Tensor x, Tensor(a!) y, int N, int H, int W, int C, int ldx, int x_coff, int ldy, "
         "int y_coff, int k, int stride, int pad, int Ho, int Wo) -> ()");
   m.def("sppf_pool(Tensor(a!) buf, int N, int H, int W, int C) -> ()");
@@ -260,6 +306,7 @@ TORCH_LIBRARY(kvedge, m) {
 
 TORCH_LIBRARY_IMPL(kvedge, CUDA, m) {
   m.impl("conv", conv);
+  m.impl("conv_dual", conv_dual);
   m.impl("maxpool2d", maxpool2d);
   m.impl("sppf_pool", sppf_pool);
   m.impl("global_avgpool", global_avgpool);

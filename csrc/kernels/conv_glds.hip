@@ -63,10 +63,30 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
 
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, p.N * p.H * p.W * p.ldx * 2);
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w, p.Cout * p.Kpad * 2);
+  const __amdgpu_buffer_rsrc_t rx2 =
+      make_rsrc(MODE == 4 ? p.x2 : p.x, MODE == 4 ? p.N * p.H2 * p.W2 * p.ldx2 * 2 : 0);
+
+  // ---- residual prefetch: issued before the K loop, consumed by the epilogue, so its
+  // latency hides under the GEMM instead of serialising after it (memory-bound layers).
+  constexpr int CPR = BN / 8;
+  constexpr int PER = BM * CPR / 256;
+  constexpr bool kPrefetchRes = PER <= 8;
+  bf16x8 rpre[kPrefetchRes ? PER : 1];
+  if (kPrefetchRes && p.res) {
+    const bf16* R = reinterpret_cast<const bf16*>(p.res);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int idx = threadIdx.x + 256 * j;
+      const int m = m0 + idx / CPR, n = n0 + (idx % CPR) * 8;
+      if (m < p.M && n < p.Cout)
+        rpre[j] = *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
+    }
+  }
 
   // ---- per-lane source descriptors (constant over the K loop) -------------
   const int lrow = lane >> 3, pch = lane & 7;
-  int a_off[A_INS];   // MODE 0: pixel-row base offset (elements); MODE 1: full byte offset
+  int a_off[A_INS];   // MODE 0: pixel-row base offset (elements); MODE 1/4: full byte offset
+  int a_off2[A_INS];  // MODE 4: byte offset of the strided second source
   unsigned a_msk[A_INS];
   int a_lc[A_INS];
   int a_h0[A_INS], a_w0[A_INS];  // MODE 3
@@ -80,8 +100,15 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
     a_msk[i] = 0u;
     a_h0[i] = -(1 << 28);
     a_w0[i] = -(1 << 28);
-    if (MODE == 1) {
+    a_off2[i] = kOOB;
+    if (MODE == 1 || MODE == 4) {
       a_off[i] = m < p.M ? (m * p.ldx + p.x_coff + lc * 8) * 2 : kOOB;
+      if (MODE == 4 && m < p.M) {
+        const int img = m / HoWo;
+        const int rem = m - img * HoWo;
+        const int ho = rem / p.Wo, wo = rem - (rem / p.Wo) * p.Wo;
+        a_off2[i] = (((img * p.H2 + ho * p.stride2) * p.W2 + wo * p.stride2) * p.ldx2 + lc * 8) * 2;
+      }
     } else {
       a_off[i] = 0;
       if (m < p.M) {
@@ -132,6 +159,17 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
       for (int i = 0; i < A_INS; ++i) {
         const int v = (kbase + a_lc[i] * 8 < p.Cin) ? a_off[i] : kOOB;
         glds16(rx, As + (wv * A_INS + i) * 512, v, kbase * 2);
+      }
+    } else if (MODE == 4) {
+      const int kbase = kt * BK;  // K1 and K - K1 are multiples of 64: no tails
+      if (kbase < p.K1) {
+#pragma unroll
+        for (int i = 0; i < A_INS; ++i)
+          glds16(rx, As + (wv * A_INS + i) * 512, a_off[i], kbase * 2);
+      } else {
+#pragma unroll
+        for (int i = 0; i < A_INS; ++i)
+          glds16(rx2, As + (wv * A_INS + i) * 512, a_off2[i], (kbase - p.K1) * 2);
       }
     } else if (MODE == 0) {
       const int k0 = kt * BK;
@@ -239,8 +277,6 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
   __syncthreads();
   bf16* __restrict__ Y = reinterpret_cast<bf16*>(p.y);
   const bf16* __restrict__ R = reinterpret_cast<const bf16*>(p.res);
-  constexpr int CPR = BN / 8;
-  constexpr int PER = BM * CPR / 256;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const int idx = tid + 256 * j;
@@ -249,7 +285,8 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
     if (m >= p.M || n >= p.Cout) continue;
     bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + ml * CS + ch * 8);
     if (has_res) {
-      const bf16x8 rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
+      const bf16x8 rv = kPrefetchRes ? rpre[kPrefetchRes ? j : 0]
+                                     : *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = f2bf(apply_act((float)v[e] + (float)rv[e], act2));
     }
@@ -266,6 +303,7 @@ ConvKernelFn glds_get(int mode) {
   switch (mode) {
     case 0: return conv_glds_kernel<BM, BN, WM, WN, 0>;
     case 1: return conv_glds_kernel<BM, BN, WM, WN, 1>;
+    case 4: return conv_glds_kernel<BM, BN, WM, WN, 4>;
     default: return conv_glds_kernel<BM, BN, WM, WN, 3>;
   }
 }
@@ -296,6 +334,10 @@ int glds_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   const long long xb = (long long)p->N * p->H * p->W * p->ldx * 2;
   const long long wb = (long long)p->Cout * p->Kpad * 2;
   if (xb >= kOOB || wb >= kOOB) return -9;
+  if (mode == 4) {
+    const long long x2b = (long long)p->N * p->H2 * p->W2 * p->ldx2 * 2;
+    if (!p->x2 || x2b >= kOOB || p->K1 % BK || (p->Kpad - p->K1) % BK || p->ldx2 % 8) return -10;
+  }
   const GldsTile& e = kGldsTiles[tile];
   const long long nwg = (long long)((p->M + e.bm - 1) / e.bm) * ((p->Cout + e.bn - 1) / e.bn);
   if (nwg <= 0) return 0;

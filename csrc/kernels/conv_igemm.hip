@@ -331,6 +331,13 @@ extern "C" int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream) {
   if (p->mode != 2 && (p->Cin % 8 != 0 || p->ldx % 8 != 0 || p->x_coff % 8 != 0)) return -3;
   if (p->mode == 1 && (p->KH != 1 || p->KW != 1 || p->stride != 1 || p->pad != 0)) return -4;
   if ((p->ldy % 8) || (p->y_coff % 8) || (p->res && ((p->ldr % 8) || (p->r_coff % 8)))) return -5;
+  if (p->mode == 4) {  // dual-source (fused downsample): v2 LDS-DMA family only
+    if (tile < 0) {
+      const long long nwg128 = ((p->M + 127) / 128) * ((p->Cout + 127) / 128);
+      tile = kNumTiles + (nwg128 >= 512 ? 0 : 4);
+    }
+    if (tile < kNumTiles) return -8;
+  }
   if (tile < 0) tile = kv_conv_pick_tile(p);
   if (tile >= kNumTiles + glds_num_tiles()) return -6;
   if (tile >= kNumTiles) return glds_launch(p, tile - kNumTiles, stream);

@@ -31,7 +31,12 @@ typedef struct KvConvParams {
   int M;              // N*Ho*Wo
   int ldy, y_coff, ldr, r_coff;
   int act;            // bits[1:0]: 0 none, 1 relu, 2 silu; bit 2: residual after act
-  int mode;           // 0 general, 1 1x1/s1/p0 GEMM, 2 stem (Cin=4, KW padded even)
+  int mode;           // 0 general, 1 1x1/s1/p0 GEMM, 2 stem (Cin=4, KW padded even),
+                      // 4 dual 1x1 (bottleneck conv3 + fused downsample, v2 tiles only)
+  // mode 4 second source: k in [K1, K) reads x2 [N, H2, W2, ldx2] at stride stride2
+  // (the bottleneck's input, i.e. the downsample branch folded in as extra K).
+  const void* x2;
+  int K1, H2, W2, ldx2, stride2;
 } KvConvParams;
 
 // tile: -1 = heuristic; otherwise an index into the tile table (kv_conv_num_tiles()).

@@ -108,14 +108,55 @@ class DeployedConv:
         out = ops.conv2d(x, self.spec, self.w, self.b, res=res, out=out, x_coff=x_coff,
                          y_coff=y_coff, r_coff=r_coff, tile=self.tile if tile is None else tile)
         if _RECORDER is not None:
-            _RECORDER.append((self, dict(x=x, res=res, out=out, x_coff=x_coff, y_coff=y_coff,
-                                         r_coff=r_coff)))
+            s = self.spec
+            key = ("conv", s.cin, s.cout, s.kh, s.kw, s.stride, s.pad, s.act, s.mode,
+                   tuple(x.shape), x_coff, tuple(out.shape), res is not None)
+            fn = lambda t, o=out: ops.conv2d(x, s, self.w, self.b, res=res, out=o,  # noqa: E731
+                                             x_coff=x_coff, y_coff=y_coff, r_coff=r_coff, tile=t)
+            _RECORDER.append((self, key, fn))
         return out
 
     @property
     def flops_per_pixel(self) -> int:
         s = self.spec
         return 2 * s.kh * s.kw * s.cin * s.cout
+
+
+@dataclass
+class DeployedDualConv:
+    """Bottleneck conv3 (+BN) and its downsample conv (+BN) as ONE GEMM over the
+    concatenated reduction dim: out = act(y . W3 + x[::s, ::s] . Wd + b3 + bd).
+    Replaces a downsample launch plus the residual write + read of its output."""
+    w: torch.Tensor          # [Cout, K1 + K2] bf16
+    b: torch.Tensor          # [Cout] fp32
+    k1: int
+    stride2: int
+    act: int
+    tile: int = -1
+
+    @staticmethod
+    def from_modules(conv3, bn3, down_conv, down_bn, act, device="cpu") -> "DeployedDualConv":
+        w3, b3 = fold_bn(conv3, bn3)
+        wd, bd = fold_bn(down_conv, down_bn)
+        assert w3.shape[2:] == (1, 1) and wd.shape[2:] == (1, 1)
+        w = torch.cat([w3[:, :, 0, 0], wd[:, :, 0, 0]], 1)
+        return DeployedDualConv(w.to(torch.bfloat16).contiguous().to(device),
+                                (b3 + bd).contiguous().to(device), w3.shape[1],
+                                down_conv.stride[0], act)
+
+    def __call__(self, y, x, out=None, tile=None):
+        out = ops.conv_dual(y, x, self.w, self.b, self.act, self.stride2, out=out,
+                            tile=self.tile if tile is None else tile)
+        if _RECORDER is not None:
+            key = ("dual", tuple(y.shape), tuple(x.shape), tuple(self.w.shape), self.stride2,
+                   self.act)
+            fn = lambda t, o=out: ops.conv_dual(y, x, self.w, self.b, self.act,  # noqa: E731
+                                                self.stride2, out=o, tile=t)
+            _RECORDER.append((self, key, fn))
+        return out
+
+    def flops_per_pixel(self) -> int:
+        return 2 * self.w.shape[0] * self.w.shape[1]
 
 
 @torch.no_grad()

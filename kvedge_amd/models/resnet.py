@@ -19,7 +19,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .layers import DeployedConv, calibrate_bn, count_flops, frames_to_nchw
+from .layers import DeployedConv, DeployedDualConv, calibrate_bn, count_flops, frames_to_nchw
 
 ACT_NONE, ACT_RELU = ops.ACT_NONE, ops.ACT_RELU
 
@@ -107,20 +107,29 @@ def init_resnet50(seed: int = 0, num_classes: int = 1000, calibrate: bool = True
 # deployed (NHWC bf16, HIP kernels)
 # ---------------------------------------------------------------------------
 class DeployedBottleneck:
-    def __init__(self, b: Bottleneck, device):
+    """conv1 -> conv2 -> conv3 with bias+residual+ReLU fused in conv3's epilogue.  Blocks
+    with a downsample branch run conv3 and the downsample as ONE GEMM over K = width + cin
+    (DeployedDualConv): the downsample output is never materialised (fuse_down=True)."""
+
+    def __init__(self, b: Bottleneck, device, fuse_down: bool = True):
         self.c1 = DeployedConv.from_modules(b.conv1, b.bn1, ACT_RELU, device)
         self.c2 = DeployedConv.from_modules(b.conv2, b.bn2, ACT_RELU, device)
-        # conv3: bias + residual + ReLU fused in the epilogue
         self.c3 = DeployedConv.from_modules(b.conv3, b.bn3, ACT_RELU, device)
         self.down = None
+        self.dual = None
         if b.downsample is not None:
             self.down = DeployedConv.from_modules(b.downsample[0], b.downsample[1], ACT_NONE,
                                                   device)
+            if fuse_down:
+                self.dual = DeployedDualConv.from_modules(b.conv3, b.bn3, b.downsample[0],
+                                                          b.downsample[1], ACT_RELU, device)
 
     def __call__(self, x, out=None):
-        idt = x if self.down is None else self.down(x)
         y = self.c1(x)
         y = self.c2(y)
+        if self.dual is not None:
+            return self.dual(y, x, out=out)
+        idt = x if self.down is None else self.down(x)
         return self.c3(y, res=idt, out=out)
 
     def out_shape(self, x_shape):
@@ -129,7 +138,7 @@ class DeployedBottleneck:
         return (N, Ho, Wo, self.c3.spec.cout)
 
     def convs(self):
-        return [c for c in (self.c1, self.c2, self.c3, self.down) if c is not None]
+        return [c for c in (self.c1, self.c2, self.c3, self.down, self.dual) if c is not None]
 
 
 class KvResNet50:

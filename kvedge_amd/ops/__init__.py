@@ -189,6 +189,23 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, w: torch.Tensor, bias: Optional[torc
     return out
 
 
+def conv_dual(x1: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
+              act: int, stride2: int, out: Optional[torch.Tensor] = None,
+              tile: int = -1) -> torch.Tensor:
+    """Bottleneck conv3 + downsample in ONE GEMM (K = K1 + K2):
+    out = act(x1 . W[:, :K1]^T + x2[::s, ::s] . W[:, K1:]^T + bias), all 1x1.
+    The downsample's output tensor is never written or re-read."""
+    N, Ho, Wo, K1 = x1.shape
+    cout = w.shape[0]
+    if out is None:
+        out = torch.empty(N, Ho, Wo, cout, dtype=torch.bfloat16, device=x1.device)
+    if x1.is_cuda:
+        _native().conv_dual(x1, x2, w, bias, out, stride2, act, tile)
+    else:
+        _ref.conv_dual(x1, x2, w, bias, act, stride2, out)
+    return out
+
+
 def maxpool2d(x: torch.Tensor, k: int, stride: int, pad: int, out: Optional[torch.Tensor] = None,
               C: Optional[int] = None, x_coff: int = 0, y_coff: int = 0) -> torch.Tensor:
     N, H, W, ldx = x.shape

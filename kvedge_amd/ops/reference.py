@@ -162,3 +162,13 @@ def preprocess(x, out, mean, std):
             N, H // 2, W // 2, 16)
     out.copy_(y4.to(out.dtype))
     return out
+
+
+def conv_dual(x1, x2, w, bias, act, stride2, out):
+    K1 = x1.shape[-1]
+    wf = w.float()
+    y = x1.float() @ wf[:, :K1].t() + x2[:, ::stride2, ::stride2].float() @ wf[:, K1:].t()
+    if bias is not None:
+        y = y + bias.float()
+    out.copy_(_act(y, act & 3).to(out.dtype))
+    return out

@@ -198,3 +198,28 @@ def test_nms_dense_overlaps():
     o, n = ops.nms(boxes.cuda(), scores.cuda(), cls.cuda(), conf=0.1, iou=0.45, max_det=300)
     assert torch.equal(n.cpu(), n_ref)
     assert (o.cpu() - o_ref).abs().max() < 1e-4
+
+
+@pytest.mark.parametrize("tile", [-1] + list(range(6, N_TILES)))
+@pytest.mark.parametrize("geom", [(2, 14, 14, 64, 128, 256, 2), (2, 7, 7, 128, 256, 512, 1),
+                                  (1, 5, 5, 64, 64, 128, 2)])
+def test_conv_dual_fused_downsample(tile, geom):
+    N, Ho, Wo, K1, K2, cout, s = geom
+    g = torch.Generator().manual_seed(tile + 5)
+    x1 = torch.randn(N, Ho, Wo, K1, generator=g).to(torch.bfloat16)
+    x2 = torch.randn(N, Ho * s, Wo * s, K2, generator=g).to(torch.bfloat16)
+    w = (torch.randn(cout, K1 + K2, generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(cout, generator=g)
+    ref = ops.conv_dual(x1, x2, w, b, ops.ACT_RELU, s)
+    got = ops.conv_dual(x1.cuda(), x2.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, s, tile=tile)
+    torch.cuda.synchronize()
+    err = (got.cpu().float() - ref.float()).abs().max().item()
+    assert err <= 0.02 * ref.float().abs().max().item() + 0.02
+
+
+def test_conv_dual_rejects_v1_tiles():
+    x1 = torch.zeros(1, 4, 4, 64, dtype=torch.bfloat16, device="cuda")
+    x2 = torch.zeros(1, 4, 4, 64, dtype=torch.bfloat16, device="cuda")
+    w = torch.zeros(64, 128, dtype=torch.bfloat16, device="cuda")
+    with pytest.raises(RuntimeError):
+        ops.conv_dual(x1, x2, w, None, ops.ACT_NONE, 1, tile=0)

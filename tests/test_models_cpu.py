@@ -34,7 +34,8 @@ def test_deployed_conv_from_modules():
 def test_resnet50_cpu_deployed_vs_module():
     ref = init_resnet50(seed=0)
     kv = KvResNet50(ref, "cpu")
-    assert len(kv.convs()) == 1 + 16 * 3 + 4 + 1  # stem + bottleneck convs + downsamples + fc
+    # stem + bottleneck convs + downsamples + fused conv3/downsample GEMMs + fc
+    assert len(kv.convs()) == 1 + 16 * 3 + 4 + 4 + 1
     assert abs(kv.flops_per_image() / 1e9 - 8.18) < 0.05
     fr = torch.randint(0, 256, (2, 224, 224, 3), dtype=torch.uint8,
                        generator=torch.Generator().manual_seed(3))
