@@ -32,6 +32,10 @@ for s in $STEPS; do
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 5 --warmup 2 ;;
     sweep) run sweep 600 python tools/batch_sweep.py ;;
     pmc)   run pmc 1000 bash tools/prof_layers.sh 256 ;;
+    fwd)   run fwdprof 600 rocprofv3 --kernel-trace --output-format csv -d $OUT/fwd -o fwd -- python3 tools/profile_forward.py --batch 256 &&
+           python tools/profile_forward.py --summarize $OUT/fwd/fwd_kernel_trace.csv > $OUT/fwd_summary.md ;;
+    fwdyolo) run fwdyolo 600 rocprofv3 --kernel-trace --output-format csv -d $OUT/fwdy -o fwdy -- python3 tools/profile_forward.py --model yolov8n --batch 64 &&
+           python tools/profile_forward.py --summarize $OUT/fwdy/fwdy_kernel_trace.csv > $OUT/fwd_yolo_summary.md ;;
     rccl)  run rccl 300 ./kvedge_amd/bin/kv_rccl_bench 1024 268435456 10 bf16 ;;
     layers64) run layers64 600 python tools/layer_bench.py --batch 64 --out $OUT/layer_bench_b64.md ;;
     layers) run layers 600 python tools/layer_bench.py ;;
