@@ -41,6 +41,14 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   return v;
 }
 
+// Branch-free variant for unrolled epilogues: a runtime-uniform `act` otherwise turns
+// every element into its own branch + IEEE divide.  SiLU via v_exp + v_rcp.
+__device__ __forceinline__ float apply_act_bf(float v, int act) {
+  const float s = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+  const float r = fmaxf(v, 0.0f);
+  return act == kActRelu ? r : (act == kActSilu ? s : v);
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));

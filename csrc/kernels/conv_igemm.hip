@@ -306,9 +306,12 @@ int glds_num_tiles();
 int glds_launch(const KvConvParams* p, int tile, hipStream_t stream);
 int glds_tile_bm(int tile);
 int glds_tile_bn(int tile);
+// v3 persistent streaming family (conv_stream.hip, 1x1 GEMM / dual only): indices after v2
+int stream_num_tiles();
+int stream_launch(const KvConvParams* p, int tile, hipStream_t stream);
 }  // namespace kvedge
 
-extern "C" int kv_conv_num_tiles(void) { return kNumTiles + glds_num_tiles(); }
+extern "C" int kv_conv_num_tiles(void) { return kNumTiles + glds_num_tiles() + stream_num_tiles(); }
 
 extern "C" int kv_conv_pick_tile(const KvConvParams* p) {
   // Heuristic: enough workgroups to cover 256 CUs x 2, largest tile otherwise.
@@ -339,7 +342,9 @@ extern "C" int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream) {
     if (tile < kNumTiles) return -8;
   }
   if (tile < 0) tile = kv_conv_pick_tile(p);
-  if (tile >= kNumTiles + glds_num_tiles()) return -6;
+  const int v3 = kNumTiles + glds_num_tiles();
+  if (tile >= v3 + stream_num_tiles()) return -6;
+  if (tile >= v3) return stream_launch(p, tile - v3, stream);
   if (tile >= kNumTiles) return glds_launch(p, tile - kNumTiles, stream);
   const TileEntry& e = kTiles[tile];
   const long long nwg = (long long)((p->M + e.cfg.bm - 1) / e.cfg.bm) *

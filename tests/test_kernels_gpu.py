@@ -82,7 +82,8 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale + 0.02
 
 
-N_TILES = 13  # v1 register-staged (0-5) + v2 LDS-DMA (6-12); checked below
+N_TILES = 17  # v1 register-staged (0-5) + v2 LDS-DMA (6-12) + v3 streaming (13-16)
+STREAM0 = 13  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
 
 
 def test_tile_count():
@@ -101,8 +102,31 @@ def test_tile_count():
 ])
 def test_conv_every_tile(tile, case):
     N, H, W, cin, cout, k, s, p, act, res, lx, xc = case
+    if tile >= STREAM0 and (k != 1 or s != 1):
+        with pytest.raises(RuntimeError):
+            _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
+                       tile=tile)
+        return
     err, scale = _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
                             tile=tile)
+    assert err <= 0.02 * scale + 0.02, (tile, case, err, scale)
+
+
+@pytest.mark.parametrize("tile", [-1] + list(range(STREAM0, N_TILES)))
+@pytest.mark.parametrize("case", [
+    # (N, H, W, cin, cout, act, res, ldx_extra, x_coff, ldy_extra, y_coff)
+    (4, 56, 56, 256, 512, ops.ACT_RELU, True, 0, 0, 0, 0),     # several M tiles per workgroup
+    (4, 56, 56, 64, 256, ops.ACT_RELU | ops.RES_AFTER_ACT, True, 0, 0, 0, 0),
+    (8, 28, 28, 512, 128, ops.ACT_SILU, False, 64, 64, 32, 16),  # slices in and out
+    (3, 7, 7, 2048, 1000, ops.ACT_NONE, False, 0, 0, 0, 0),     # N tail, short M
+    (5, 13, 13, 40, 72, ops.ACT_SILU, True, 0, 0, 0, 0),       # Cin % 64, Cout % 64 tails
+])
+def test_conv_stream_gemm(tile, case):
+    """Persistent streaming 1x1 kernel: multi-tile walks, residual prefetch across
+    tiles, residual before/after the activation, sliced operands, tails."""
+    N, H, W, cin, cout, act, res, lx, xc, ly, yc = case
+    err, scale = _conv_case(N, H, W, cin, cout, 1, 1, 0, act, res=res, ldx_extra=lx, x_coff=xc,
+                            ldy_extra=ly, y_coff=yc, tile=tile)
     assert err <= 0.02 * scale + 0.02, (tile, case, err, scale)
 
 

@@ -43,8 +43,9 @@ def summarize(path, reps):
     body = rows[idx + 1:]
     agg = collections.OrderedDict()
     for r in body:
-        name = r["Kernel_Name"].replace("void kvedge::(anonymous namespace)::", "").split("(")[0]
-        key = (name[:60], r.get("Grid_Size", ""))
+        name = r["Kernel_Name"].replace("void ", "").replace(
+            "kvedge::(anonymous namespace)::", "").split("(")[0]
+        key = (name[:60], r.get("Grid_Size_X", r.get("Grid_Size", "")))
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         agg.setdefault(key, []).append(dur)
     total = sum(sum(v) for v in agg.values()) / reps
