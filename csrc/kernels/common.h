@@ -41,12 +41,36 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   return v;
 }
 
-// Branch-free variant for unrolled epilogues: a runtime-uniform `act` otherwise turns
-// every element into its own branch + IEEE divide.  SiLU via v_exp + v_rcp.
-__device__ __forceinline__ float apply_act_bf(float v, int act) {
-  const float s = v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
-  const float r = fmaxf(v, 0.0f);
-  return act == kActRelu ? r : (act == kActSilu ? s : v);
+// Compile-time activation for fused epilogues.  A runtime `act` inside a fully unrolled
+// epilogue costs a scalar branch per element (and an IEEE divide per SiLU); the kernels
+// instead instantiate the epilogue once per activation pair via dispatch_act().
+template <int I>
+struct IC {
+  static constexpr int value = I;
+};
+
+template <int ACT>
+__device__ __forceinline__ float act_c(float v) {
+  if constexpr (ACT == kActRelu) return fmaxf(v, 0.0f);
+  else if constexpr (ACT == kActSilu) return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));
+  else return v;
+}
+
+// act bits: [1:0] activation, bit 2 = residual added AFTER the activation (YOLO
+// Bottleneck x + SiLU(conv)); otherwise act(conv + res) (ResNet).  Calls
+// f(IC<act1>, IC<act2>): act1 applies to acc + bias, act2 after the residual add.
+template <class F>
+__device__ __forceinline__ void dispatch_act(int act_bits, bool has_res, F&& f) {
+  const int a = act_bits & 3;
+  if (!has_res || (act_bits & 4)) {
+    if (a == kActRelu) f(IC<kActRelu>{}, IC<kActNone>{});
+    else if (a == kActSilu) f(IC<kActSilu>{}, IC<kActNone>{});
+    else f(IC<kActNone>{}, IC<kActNone>{});
+  } else {
+    if (a == kActRelu) f(IC<kActNone>{}, IC<kActRelu>{});
+    else if (a == kActSilu) f(IC<kActNone>{}, IC<kActSilu>{});
+    else f(IC<kActNone>{}, IC<kActNone>{});
+  }
 }
 
 __device__ __forceinline__ float wave_max(float v) {

@@ -17,8 +17,12 @@
 //    the DMA writes are lane-linear (swizzle applied on the SOURCE address, guide rule
 //    21) and both the 32x32x16 and 16x16x32 fragment reads are conflict-free under the
 //    ds_read_b128 lane grouping (derivation: docs/kernels.md).
-//  * 2-stage ring: K step k+1 is issued before the MFMAs of step k; one vmcnt(0) +
-//    barrier per step (guide §5.5 T3+T4 "minimum 2-phase").
+//  * D-slot ring (D = 2..4): K step k+D-1 is issued before the MFMAs of step k.  Every
+//    step issues the same number of DMA ops (steps past the end are all out of range),
+//    so "step k landed" is an exact s_waitcnt vmcnt((D-2) * ops_per_step) that leaves
+//    the younger steps in flight; one barrier per step.  D = 2 is the classic 2-phase
+//    loop (guide §5.5 T3+T4); deeper rings trade LDS (occupancy) for latency hiding,
+//    and the autotuner picks per layer.
 //  * Fused epilogue (bias, residual before/after act, ReLU/SiLU) staged through LDS for
 //    full-row 16-B stores, as in v1.
 #include "common.h"
@@ -44,15 +48,20 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t rs, bf16* lds, int
 // MODE 0: KxK (or strided 1x1) conv with Cin % 64 == 0 -> tap uniform per K step
 // MODE 1: 1x1 / stride 1 / pad 0 GEMM (A rows contiguous)
 // MODE 3: generic gather, Cin % 8 == 0 (per-lane tap tracking)
-template <int BM, int BN, int WM, int WN, int MODE>
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N < 63 ? N : 63) : "memory");
+}
+
+template <int BM, int BN, int WM, int WN, int MODE, int D>
 __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p) {
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
   constexpr int A_INS = BM / 32;  // DMA instructions per wave per stage (8 rows each)
   constexpr int B_INS = BN / 32;
   constexpr int STAGE = (BM + BN) * BK;
-  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "tile");
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE];
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1 && D >= 2 && D <= 4, "tile");
+  __shared__ __attribute__((aligned(16))) bf16 smem[D * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -237,74 +246,91 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
   };
 
   const int nk = p.Kpad / BK;
-  issue(0, 0);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // stage `cur` landed for every wave; stage cur^1 no longer read
-    if (kt + 1 < nk) issue(cur ^ 1, kt + 1);
-    compute(cur);
+  if (D == 2) {
+    issue(0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // stage `cur` landed for every wave; stage cur^1 no longer read
+      if (kt + 1 < nk) issue(cur ^ 1, kt + 1);
+      compute(cur);
+    }
+  } else {
+    // steps >= nk are issued too (all lanes out of range or never read) so that every
+    // step is exactly A_INS + B_INS VMEM ops per wave and the wait below is exact
+#pragma unroll
+    for (int s = 0; s < D - 1; ++s) issue(s, s);
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      wait_vm<(D - 2) * (A_INS + B_INS)>();  // step kt landed (this wave's part)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();           // ... for every wave; slot kt-1 free
+      asm volatile("" ::: "memory");
+      issue(cur == 0 ? D - 1 : cur - 1, kt + D - 1);
+      compute(cur);
+      cur = cur == D - 1 ? 0 : cur + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land on the C tile
   }
   __syncthreads();
 
   // ---- fused epilogue through LDS (see conv_igemm.hip) ----------------------
   constexpr int CS = BN + 8;
-  static_assert(BM * CS <= 2 * STAGE, "C tile fits");
+  static_assert(BM * CS <= D * STAGE, "C tile fits");
   const bool has_res = p.res != nullptr;
-  const int act_fn = p.act & 3;
-  const bool res_post = (p.act & 4) != 0;
-  const int act1 = (has_res && !res_post) ? kActNone : act_fn;
-  const int act2 = res_post ? kActNone : act_fn;
-#pragma unroll
-  for (int tn = 0; tn < TN; ++tn) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int nl = wn * WTN + tn * 32 + g * 8 + fh * 4;
-      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (p.bias && n0 + nl < p.Cout) bv = *reinterpret_cast<const float4*>(p.bias + n0 + nl);
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm) {
-        const int ml = wm * WTM + tm * 32 + fr;
-        bf16x4 o;
-        o[0] = f2bf(apply_act(acc[tn][tm][4 * g + 0] + bv.x, act1));
-        o[1] = f2bf(apply_act(acc[tn][tm][4 * g + 1] + bv.y, act1));
-        o[2] = f2bf(apply_act(acc[tn][tm][4 * g + 2] + bv.z, act1));
-        o[3] = f2bf(apply_act(acc[tn][tm][4 * g + 3] + bv.w, act1));
-        *reinterpret_cast<bf16x4*>(smem + ml * CS + nl) = o;
-      }
-    }
-  }
-  __syncthreads();
   bf16* __restrict__ Y = reinterpret_cast<bf16*>(p.y);
   const bf16* __restrict__ R = reinterpret_cast<const bf16*>(p.res);
+  dispatch_act(p.act, has_res, [&](auto A1, auto A2) __attribute__((always_inline)) {
+    constexpr int act1 = decltype(A1)::value, act2 = decltype(A2)::value;
 #pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int idx = tid + 256 * j;
-    const int ml = idx / CPR, ch = idx % CPR;
-    const int m = m0 + ml, n = n0 + ch * 8;
-    if (m >= p.M || n >= p.Cout) continue;
-    bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + ml * CS + ch * 8);
-    if (has_res) {
-      const bf16x8 rv = kPrefetchRes ? rpre[kPrefetchRes ? j : 0]
-                                     : *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
+    for (int tn = 0; tn < TN; ++tn) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = f2bf(apply_act((float)v[e] + (float)rv[e], act2));
+      for (int g = 0; g < 4; ++g) {
+        const int nl = wn * WTN + tn * 32 + g * 8 + fh * 4;
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (p.bias && n0 + nl < p.Cout) bv = *reinterpret_cast<const float4*>(p.bias + n0 + nl);
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          const int ml = wm * WTM + tm * 32 + fr;
+          bf16x4 o;
+          o[0] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 0] + bv.x));
+          o[1] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 1] + bv.y));
+          o[2] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 2] + bv.z));
+          o[3] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 3] + bv.w));
+          *reinterpret_cast<bf16x4*>(smem + ml * CS + nl) = o;
+        }
+      }
     }
-    *reinterpret_cast<bf16x8*>(Y + (size_t)m * p.ldy + p.y_coff + n) = v;
-  }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int idx = tid + 256 * j;
+      const int ml = idx / CPR, ch = idx % CPR;
+      const int m = m0 + ml, n = n0 + ch * 8;
+      if (m >= p.M || n >= p.Cout) continue;
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + ml * CS + ch * 8);
+      if (has_res) {
+        const bf16x8 rv = kPrefetchRes ? rpre[kPrefetchRes ? j : 0]
+                                       : *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(act_c<act2>((float)v[e] + (float)rv[e]));
+      }
+      *reinterpret_cast<bf16x8*>(Y + (size_t)m * p.ldy + p.y_coff + n) = v;
+    }
+  });
 }
 
 }  // namespace
 
 typedef void (*ConvKernelFn)(const KvConvParams);
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int D = 2>
 ConvKernelFn glds_get(int mode) {
   switch (mode) {
-    case 0: return conv_glds_kernel<BM, BN, WM, WN, 0>;
-    case 1: return conv_glds_kernel<BM, BN, WM, WN, 1>;
-    case 4: return conv_glds_kernel<BM, BN, WM, WN, 4>;
-    default: return conv_glds_kernel<BM, BN, WM, WN, 3>;
+    case 0: return conv_glds_kernel<BM, BN, WM, WN, 0, D>;
+    case 1: return conv_glds_kernel<BM, BN, WM, WN, 1, D>;
+    case 4: return conv_glds_kernel<BM, BN, WM, WN, 4, D>;
+    default: return conv_glds_kernel<BM, BN, WM, WN, 3, D>;
   }
 }
 
@@ -321,6 +347,12 @@ static const GldsTile kGldsTiles[] = {
     {64, 128, &glds_get<64, 128, 2, 2>},
     {256, 128, &glds_get<256, 128, 2, 2>},
     {128, 256, &glds_get<128, 256, 2, 2>},
+    // deeper rings (3-4 K steps in flight); indices above are kept stable
+    {128, 128, &glds_get<128, 128, 2, 2, 3>},
+    {128, 64, &glds_get<128, 64, 2, 2, 3>},
+    {64, 128, &glds_get<64, 128, 2, 2, 3>},
+    {64, 64, &glds_get<64, 64, 2, 2, 4>},
+    {128, 64, &glds_get<128, 64, 2, 2, 4>},
 };
 
 int glds_num_tiles() { return (int)(sizeof(kGldsTiles) / sizeof(kGldsTiles[0])); }

@@ -223,48 +223,45 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const KvConvParams p
   //          writes whole 128-256 B row segments instead of 32-B pieces.
   constexpr int CS = BN + 8;  // C-tile row stride in elements
   static_assert(BM * CS <= 2 * (BM + BN) * BK, "C tile must fit the operand buffers");
-  // act bits: [1:0] activation, bit 2 = residual added AFTER the activation
-  // (YOLO Bottleneck: x + SiLU(conv)); otherwise act(conv + res) (ResNet).
   const bool has_res = p.res != nullptr;
-  const int act_fn = p.act & 3;
-  const bool res_post = (p.act & 4) != 0;
-  const int act1 = (has_res && !res_post) ? kActNone : act_fn;
-  const int act2 = res_post ? kActNone : act_fn;
-#pragma unroll
-  for (int tn = 0; tn < TN; ++tn) {
-    const int nl = wn * WTN + tn * 16 + (lane >> 4) * 4;
-    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (p.bias && n0 + nl < p.Cout) bv = *reinterpret_cast<const float4*>(p.bias + n0 + nl);
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
-      const int ml = wm * WTM + tm * 16 + (lane & 15);
-      bf16x4 o;
-      o[0] = f2bf(apply_act(acc[tn][tm][0] + bv.x, act1));
-      o[1] = f2bf(apply_act(acc[tn][tm][1] + bv.y, act1));
-      o[2] = f2bf(apply_act(acc[tn][tm][2] + bv.z, act1));
-      o[3] = f2bf(apply_act(acc[tn][tm][3] + bv.w, act1));
-      *reinterpret_cast<bf16x4*>(smem + ml * CS + nl) = o;
-    }
-  }
-  __syncthreads();
   bf16* __restrict__ Y = reinterpret_cast<bf16*>(p.y);
   const bf16* __restrict__ R = reinterpret_cast<const bf16*>(p.res);
   constexpr int CPR = BN / 8;               // 16-B chunks per tile row
   constexpr int PER = BM * CPR / 256;       // chunks per thread
+  dispatch_act(p.act, has_res, [&](auto A1, auto A2) __attribute__((always_inline)) {
+    constexpr int act1 = decltype(A1)::value, act2 = decltype(A2)::value;
 #pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int idx = tid + 256 * j;
-    const int ml = idx / CPR, ch = idx % CPR;
-    const int m = m0 + ml, n = n0 + ch * 8;
-    if (m >= p.M || n >= p.Cout) continue;
-    bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + ml * CS + ch * 8);
-    if (has_res) {
-      const bf16x8 rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
+    for (int tn = 0; tn < TN; ++tn) {
+      const int nl = wn * WTN + tn * 16 + (lane >> 4) * 4;
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p.bias && n0 + nl < p.Cout) bv = *reinterpret_cast<const float4*>(p.bias + n0 + nl);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = f2bf(apply_act((float)v[e] + (float)rv[e], act2));
+      for (int tm = 0; tm < TM; ++tm) {
+        const int ml = wm * WTM + tm * 16 + (lane & 15);
+        bf16x4 o;
+        o[0] = f2bf(act_c<act1>(acc[tn][tm][0] + bv.x));
+        o[1] = f2bf(act_c<act1>(acc[tn][tm][1] + bv.y));
+        o[2] = f2bf(act_c<act1>(acc[tn][tm][2] + bv.z));
+        o[3] = f2bf(act_c<act1>(acc[tn][tm][3] + bv.w));
+        *reinterpret_cast<bf16x4*>(smem + ml * CS + nl) = o;
+      }
     }
-    *reinterpret_cast<bf16x8*>(Y + (size_t)m * p.ldy + p.y_coff + n) = v;
-  }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int idx = tid + 256 * j;
+      const int ml = idx / CPR, ch = idx % CPR;
+      const int m = m0 + ml, n = n0 + ch * 8;
+      if (m >= p.M || n >= p.Cout) continue;
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + ml * CS + ch * 8);
+      if (has_res) {
+        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(act_c<act2>((float)v[e] + (float)rv[e]));
+      }
+      *reinterpret_cast<bf16x8*>(Y + (size_t)m * p.ldy + p.y_coff + n) = v;
+    }
+  });
 }
 
 typedef void (*ConvKernelFn)(const KvConvParams);

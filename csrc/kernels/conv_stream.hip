@@ -1,76 +1,114 @@
 // K3 v3 — persistent streaming 1x1 conv / GEMM for the HBM-bound layers (gfx950).
 //
-// Forward profile (tools/profile_forward.py, batch 256): ~50 % of a ResNet-50 step is
-// 1x1 convs with K <= 512 that move far more bytes than they compute (bottleneck
-// conv1 "reduce" and conv3 "expand + residual").  A one-tile-per-workgroup kernel
-// serialises  load A,B -> MFMA -> epilogue (residual read + store)  inside every
-// workgroup and leaves the overlap to occupancy alone; it reached 3.8-4.5 TB/s.
+// Forward profile (profiles/r1_v2_*, batch 256): ~50 % of a ResNet-50 step is 1x1
+// convs with K <= 512 that move far more bytes than they compute (bottleneck conv1
+// "reduce" and conv3 "expand + residual").  A one-tile-per-workgroup kernel serialises
+// load A,B -> MFMA -> epilogue inside every workgroup and leaves the overlap to
+// occupancy; it reached 3.8-4.5 TB/s.  The bound is bytes in flight per CU (Little's
+// law: ~6 TB/s x ~2-3 us loaded latency / 256 CUs ~ 48-72 KB per CU).
 //
-// Here a grid of ~3 workgroups per CU walks a flat stream of (M tile, K step) stages:
-//  * a 2-slot LDS-DMA ring (buffer_load ... lds, as in conv_glds.hip) is fed ACROSS
-//    tile boundaries: the first K step of tile i+1 is in flight while tile i finishes
-//    its MFMAs and its epilogue;
-//  * the residual of tile i+1 is prefetched into registers during tile i;
-//  * the epilogue stages C through its own LDS region (not the ring) and issues
-//    full-row 16-B stores that are never waited on;
-//  * each workgroup keeps one N slice for all its tiles (grid % n-slices == 0), so the
-//    weight slice stays hot in the CU's L1/L2.
+// Here a grid of 1-3 workgroups per CU walks a flat stream of (M tile, K step) stages:
+//  * a D-slot LDS-DMA ring (buffer_load ... lds) is fed D-1 stages ahead, ACROSS tile
+//    boundaries, so the next tiles' operands stream while this tile computes/stores;
+//  * the residual tile is loaded into a D-deep REGISTER ring with the tile's last K
+//    step (the loop is unrolled by D so every ring slot is a fixed register set); the
+//    register file (512 KB/CU) holds far more in-flight residual bytes than spare LDS;
+//  * BRES variants keep the workgroup's whole weight slice [BN x Kpad] resident in LDS
+//    (loaded once) and stream only activations;
+//  * every stage issues the same number of VMEM ops (out-of-range lanes/stages use an
+//    offset past num_records -> zero fill), so the wait for stage j is an exact
+//    vmcnt(n) computed from (D, #epilogues in the window): older stores stay in flight;
+//  * the nbn workgroups that share an M tile are adjacent after the bijective XCD
+//    remap, i.e. on the same XCD: the activation tile is fetched into one L2 once.
 // Modes: 1 = plain 1x1 (stride 1) GEMM, 4 = dual-source (conv3 + fused downsample).
 #include "common.h"
 #include "kvedge_kernels.h"
 
+#include <cstdlib>
+
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 namespace kvedge {
 namespace {
 
 constexpr int BK = 64;
 constexpr int kOOB = 0x7ffffff0;
+constexpr int kLdsMax = 160 * 1024;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const void* base, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
 }
 
+template <int AUX = 0>
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, bf16* lds, int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(
-      rs, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+      rs, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, AUX);
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, bool RES>
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(IC<I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N < 63 ? N : 63) : "memory");
+}
+
+// LDS bytes of one variant (host + device agree on the layout)
+__host__ __device__ constexpr int stream_lds_bytes(int bm, int bn, int d, bool res, bool bres,
+                                                   int kpad) {
+  return 2 * (d * (bm * BK + (bres ? 0 : bn * BK)) + (bres ? bn * kpad : 0) + bm * (bn + 8));
+}
+
+template <int BM, int BN, int D, int MODE, bool RES, bool BRES, int POL>
 __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams p) {
+  constexpr int WM = 2, WN = 2;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
   constexpr int A_INS = BM / 32, B_INS = BN / 32;
-  constexpr int STAGE = (BM + BN) * BK;
   constexpr int CS = BN + 8;
   constexpr int CPR = BN / 8;
-  constexpr int PER = BM * CPR / 256;
-  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1 && PER >= 1, "tile");
-  // one LDS array (guide §5 trap (a)): [ring slot 0 | ring slot 1 | C tile]
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * STAGE + BM * CS];
-  bf16* const Cs = smem + 2 * STAGE;
-  // VMEM ops a wave issues after the next stage's DMA in an epilogue iteration:
-  // PER output stores (+ PER residual prefetch loads).  Exact: every one of them is
-  // always issued (out-of-range lanes get an offset past num_records instead).
-  constexpr int EPI = PER + (RES ? PER : 0);
+  constexpr int PER = BM * CPR / 256;  // 16-B output (and residual) chunks per thread
+  constexpr int SA = BM * BK, SB = BRES ? 0 : BN * BK;
+  constexpr int SLOT = SA + SB;
+  // VMEM ops per stage per wave, and per epilogue (stores)
+  constexpr int SI = A_INS + (BRES ? 0 : B_INS) + (RES ? PER : 0);
+  constexpr int EPI = PER;
+  // cache policy of the streamed (read-once / write-once) bytes: 0 default, 2 = nt
+  constexpr int SP = POL;
+  static_assert(TM >= 1 && TN >= 1 && PER >= 1 && D >= 2 && D <= 6, "tile");
+  // one LDS array (guide §5 trap (a)): [D ring slots: A | B] [resident B] [C tile]
+  extern __shared__ __attribute__((aligned(16))) bf16 smem[];
+  const int nk = p.Kpad / BK;
+  bf16* const Bres = smem + D * SLOT;
+  bf16* const Cs = Bres + (BRES ? BN * p.Kpad : 0);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wv / WN, wn = wv % WN;
   const int nbm = (p.M + BM - 1) / BM, nbn = (p.Cout + BN - 1) / BN;
-  // grid is a multiple of nbn: this workgroup owns N slice nb for all its tiles
-  const int nb = blockIdx.x % nbn;
+  // grid = mgroups * nbn; the nbn slices of one M group are adjacent logical ids, and
+  // xcd_remap puts adjacent logical ids on the same XCD (shared L2 for the A tile)
+  const int logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int nb = logical % nbn;
   const int n0 = nb * BN;
   const int mstep = gridDim.x / nbn;
-  const int mfirst = blockIdx.x / nbn;
+  const int mfirst = logical / nbn;
   const int ntiles = mfirst < nbm ? (nbm - 1 - mfirst) / mstep + 1 : 0;
-  const int nk = p.Kpad / BK;
   const int nstages = ntiles * nk;
+  if (nstages == 0) return;
 
   const __amdgpu_buffer_rsrc_t rx = mk_rsrc(p.x, p.N * p.H * p.W * p.ldx * 2);
   const __amdgpu_buffer_rsrc_t rw = mk_rsrc(p.w, p.Cout * p.Kpad * 2);
   const __amdgpu_buffer_rsrc_t rx2 =
       mk_rsrc(MODE == 4 ? p.x2 : p.x, MODE == 4 ? p.N * p.H2 * p.W2 * p.ldx2 * 2 : 0);
+  const __amdgpu_buffer_rsrc_t rr = mk_rsrc(RES ? p.res : p.x, RES ? p.M * p.ldr * 2 : 0);
+  const __amdgpu_buffer_rsrc_t ry = mk_rsrc(p.y, p.M * p.ldy * 2);
 
   const int lrow = lane >> 3, pch = lane & 7;
   int b_off[B_INS];
@@ -88,56 +126,55 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams 
   }
   const int HoWo = p.Ho * p.Wo;
 
-  // issue one (tile, kt) stage into ring slot `slot`
-  auto issue = [&](int s, int slot) {
+  typedef u32x4 ResRegs[RES ? PER : 1];
+  // one (tile, kt) stage into ring slot `slot`: always SI VMEM ops per wave
+  auto issue = [&](int s, int slot, ResRegs& rdst) __attribute__((always_inline)) {
     const int ti = s / nk, kt = s - ti * nk;
+    const bool tv = ti < ntiles;
     const int m0 = (mfirst + ti * mstep) * BM;
-    bf16* As = smem + slot * STAGE;
-    bf16* Bs = As + BM * BK;
+    bf16* As = smem + slot * SLOT;
     const int kbase = kt * BK;
     if (MODE == 4 && kbase >= p.K1) {
 #pragma unroll
       for (int i = 0; i < A_INS; ++i) {
         const int m = m0 + (wv * A_INS + i) * 8 + lrow;
         int v = kOOB;
-        if (m < p.M) {
-          const int img = m / HoWo, rem = m - (m / HoWo) * HoWo;
-          const int ho = rem / p.Wo, wo = rem - (rem / p.Wo) * p.Wo;
+        if (tv && m < p.M) {
+          const int img = m / HoWo, rem = m - img * HoWo;
+          const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
           v = (((img * p.H2 + ho * p.stride2) * p.W2 + wo * p.stride2) * p.ldx2 + a_lc[i] * 8) * 2;
         }
-        dma16(rx2, As + (wv * A_INS + i) * 512, v, (kbase - p.K1) * 2);
+        dma16<SP>(rx2, As + (wv * A_INS + i) * 512, v, (kbase - p.K1) * 2);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < A_INS; ++i) {
         const int m = m0 + (wv * A_INS + i) * 8 + lrow;
-        const bool ok = m < p.M && (MODE == 4 || kbase + a_lc[i] * 8 < p.Cin);
+        const bool ok = tv && m < p.M && (MODE == 4 || kbase + a_lc[i] * 8 < p.Cin);
         const int v = ok ? (m * p.ldx + p.x_coff + a_lc[i] * 8) * 2 : kOOB;
-        dma16(rx, As + (wv * A_INS + i) * 512, v, kbase * 2);
+        dma16<SP>(rx, As + (wv * A_INS + i) * 512, v, kbase * 2);
       }
     }
+    if (!BRES) {
+      bf16* Bs = As + SA;
 #pragma unroll
-    for (int i = 0; i < B_INS; ++i) dma16(rw, Bs + (wv * B_INS + i) * 512, b_off[i], kbase * 2);
-  };
-
-  const __amdgpu_buffer_rsrc_t rr = mk_rsrc(RES ? p.res : p.x, RES ? p.M * p.ldr * 2 : 0);
-  const __amdgpu_buffer_rsrc_t ry = mk_rsrc(p.y, p.M * p.ldy * 2);
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  u32x4 rpre[PER];
-  auto prefetch_res = [&](int ti) {  // always issues PER loads (counted waits rely on it)
-    if (!RES) return;
-    const int m0 = (mfirst + ti * mstep) * BM;
+      for (int i = 0; i < B_INS; ++i)
+        dma16(rw, Bs + (wv * B_INS + i) * 512, tv ? b_off[i] : kOOB, kbase * 2);
+    }
+    if (RES) {  // this thread's epilogue chunks idx = tid + 256 j of the residual tile
+      const bool last = kt == nk - 1 && tv;
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int idx = tid + 256 * j;
-      const int m = m0 + idx / CPR, n = n0 + (idx % CPR) * 8;
-      const int off = (ti < ntiles && m < p.M && n < p.Cout) ? (m * p.ldr + p.r_coff + n) * 2 : kOOB;
-      rpre[j] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
+      for (int j = 0; j < PER; ++j) {
+        const int idx = tid + 256 * j;
+        const int m = m0 + idx / CPR, n = n0 + (idx % CPR) * 8;
+        const int off = (last && m < p.M && n < p.Cout) ? (m * p.ldr + p.r_coff + n) * 2 : kOOB;
+        rdst[j] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, SP);
+      }
     }
   };
 
   floatx16 acc[TN][TM];
-  auto zero_acc = [&]() {
+  auto zero_acc = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int a = 0; a < TN; ++a)
 #pragma unroll
@@ -147,9 +184,9 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams 
   };
 
   const int fr = lane & 31, fh = lane >> 5;
-  auto compute = [&](int slot) {
-    const bf16* As = smem + slot * STAGE;
-    const bf16* Bs = As + BM * BK;
+  auto compute = [&](int slot, int kt) __attribute__((always_inline)) {
+    const bf16* As = smem + slot * SLOT;
+    const bf16* Bs = BRES ? Bres + kt * BN * BK : As + SA;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int q = ks * 2 + fh;
@@ -172,14 +209,9 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams 
     }
   };
 
-  const int act_fn = p.act & 3;
-  const bool res_post = (p.act & 4) != 0;
-  const int act1 = (RES && !res_post) ? kActNone : act_fn;
-  const int act2 = res_post ? kActNone : act_fn;
-  bf16* __restrict__ Y = reinterpret_cast<bf16*>(p.y);
 
   // this lane's bias values for the whole run (the N slice is fixed): registers, not
-  // LDS -- an LDS read here would make hipcc drain the in-flight LDS-DMA (vmcnt(0)).
+  // LDS -- an LDS read in the epilogue would make hipcc drain the in-flight DMA.
   float4 bias_r[TN][4];
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn)
@@ -189,7 +221,10 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams 
       bias_r[tn][g] = (p.bias && n < p.Cout) ? *reinterpret_cast<const float4*>(p.bias + n)
                                              : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-  auto epilogue = [&](int ti) {
+
+  // act1/act2 compile-time: instantiated per activation pair by dispatch_act() below
+  auto epilogue = [&](int ti, const ResRegs& rres, auto A1, auto A2) __attribute__((always_inline)) {
+    constexpr int act1 = decltype(A1)::value, act2 = decltype(A2)::value;
     const int m0 = (mfirst + ti * mstep) * BM;
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
@@ -201,16 +236,16 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams 
         for (int tm = 0; tm < TM; ++tm) {
           const int ml = wm * WTM + tm * 32 + fr;
           bf16x4 o;
-          o[0] = f2bf(apply_act_bf(acc[tn][tm][4 * g + 0] + bv.x, act1));
-          o[1] = f2bf(apply_act_bf(acc[tn][tm][4 * g + 1] + bv.y, act1));
-          o[2] = f2bf(apply_act_bf(acc[tn][tm][4 * g + 2] + bv.z, act1));
-          o[3] = f2bf(apply_act_bf(acc[tn][tm][4 * g + 3] + bv.w, act1));
+          o[0] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 0] + bv.x));
+          o[1] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 1] + bv.y));
+          o[2] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 2] + bv.z));
+          o[3] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 3] + bv.w));
           *reinterpret_cast<bf16x4*>(Cs + ml * CS + nl) = o;
         }
       }
     }
-    // C tile complete: LDS writes drained + raw barrier (no vmcnt: the next stage's
-    // DMA and the previous stores stay in flight)
+    // C tile complete: LDS writes drained + raw barrier (no vmcnt: the DMA ring and
+    // the previous stores stay in flight)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -221,69 +256,100 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams 
       const int m = m0 + ml, n = n0 + ch * 8;
       bf16x8 v = *reinterpret_cast<const bf16x8*>(Cs + ml * CS + ch * 8);
       if (RES) {
-        const bf16x8 rv = __builtin_bit_cast(bf16x8, rpre[j]);
+        const bf16x8 rv = __builtin_bit_cast(bf16x8, rres[j]);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = f2bf(apply_act_bf((float)v[e] + (float)rv[e], act2));
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(act_c<act2>((float)v[e] + (float)rv[e]));
       }
       const int off = (m < p.M && n < p.Cout) ? (m * p.ldy + p.y_coff + n) * 2 : kOOB;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ry, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ry, off, 0, SP);
     }
   };
 
-  if (nstages == 0) return;
-  prefetch_res(0);
-  issue(0, 0);
-  zero_acc();
-  bool after_epi = false;
-  for (int s = 0; s < nstages; ++s) {
-    const int slot = s & 1;
-    const int ti = s / nk, kt = s - ti * nk;
-    // stage s landed: after an epilogue its EPI stores/prefetches are younger than this
-    // stage's DMA and may stay in flight; otherwise drain everything.
-    if (after_epi)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EPI) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // all waves: stage s visible, slot^1 and C tile free
-    asm volatile("" ::: "memory");
-    // unconditional: past the last stage this fetches zeros/weights into the free slot.
-    // A conditional issue makes hipcc's waitcnt merge assume the residual prefetch may
-    // be the youngest VMEM op and emit vmcnt(1) in the epilogue (drains the ring).
-    issue(s + 1, slot ^ 1);
-    compute(slot);
-    after_epi = false;
-    if (kt == nk - 1) {
-      epilogue(ti);
-      prefetch_res(ti + 1);  // rides behind the stores; consumed one tile later
-      zero_acc();
-      after_epi = true;
-    }
+  if (BRES) {  // the weight slice, once: nk x [BN][BK] swizzled blocks
+    for (int kt = 0; kt < nk; ++kt)
+#pragma unroll
+      for (int i = 0; i < B_INS; ++i)
+        dma16(rw, Bres + kt * BN * BK + (wv * B_INS + i) * 512, b_off[i], kt * BK * 2);
   }
+  ResRegs rres[D];
+  static_for<D - 1>([&](auto S) __attribute__((always_inline)) {
+    constexpr int i = decltype(S)::value;
+    issue(i, i, rres[i]);
+  });
+  zero_acc();
+  // Stage j with j % D == u: ring slot u, residual registers rres[u].  The stage count
+  // is rounded up to a multiple of D; the extra stages are all out of range (zero DMA,
+  // no stores), which keeps every iteration's VMEM count -- and so the waits -- exact.
+  const int nround = (nstages + D - 1) / D * D;
+  dispatch_act(p.act, RES, [&](auto A1, auto A2) __attribute__((always_inline)) {
+  for (int j0 = 0; j0 < nround; j0 += D) {
+    static_for<D>([&](auto U) __attribute__((always_inline)) {
+      constexpr int u = decltype(U)::value;
+      const int j = j0 + u;
+      const int ti = j / nk, kt = j - ti * nk;
+      // Stage j landed.  Issued after it: stages j+1..j+D-2 (SI ops each) and the stores
+      // of every epilogue in iterations [max(0, j-D+1), j-1].
+      const int lo = j - D + 1 > 0 ? j - D + 1 : 0;
+      const int e = j / nk - lo / nk;
+      if (e <= 0) wait_vm<(D - 2) * SI>();
+      else if (e == 1) wait_vm<(D - 2) * SI + EPI>();
+      else if (e == 2) wait_vm<(D - 2) * SI + 2 * EPI>();
+      else if (e == 3) wait_vm<(D - 2) * SI + 3 * EPI>();
+      else if (e == 4) wait_vm<(D - 2) * SI + 4 * EPI>();
+      else wait_vm<(D - 2) * SI + 5 * EPI>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // all waves: stage j visible, slot j-1 and C tile free
+      asm volatile("" ::: "memory");
+      constexpr int un = (u + D - 1) % D;
+      issue(j + D - 1, un, rres[un]);
+      compute(u, kt);
+      if (kt == nk - 1) {
+        epilogue(ti, rres[u], A1, A2);
+        zero_acc();
+      }
+    });
+  }
+  });
 }
 
 }  // namespace
 
 typedef void (*StreamFn)(const KvConvParams);
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int D, bool BRES, int POL = 0>
 StreamFn stream_get(int mode, bool res) {
-  if (mode == 4) return conv_stream_kernel<BM, BN, WM, WN, 4, false>;
-  return res ? conv_stream_kernel<BM, BN, WM, WN, 1, true> : conv_stream_kernel<BM, BN, WM, WN, 1, false>;
+  if (mode == 4) return conv_stream_kernel<BM, BN, D, 4, false, BRES, POL>;
+  return res ? conv_stream_kernel<BM, BN, D, 1, true, BRES, POL>
+             : conv_stream_kernel<BM, BN, D, 1, false, BRES, POL>;
 }
 
 struct StreamTile {
-  int bm, bn, per_cu;
+  int bm, bn, d;
+  bool bres;
   StreamFn (*get)(int, bool);
 };
 
 static const StreamTile kStreamTiles[] = {
-    // per_cu = workgroups the LDS footprint lets one CU hold (2 ring slots + C tile)
-    {64, 64, 3, &stream_get<64, 64, 2, 2>},     //  41 KB
-    {64, 128, 2, &stream_get<64, 128, 2, 2>},   //  65 KB
-    {128, 64, 2, &stream_get<128, 64, 2, 2>},   //  65 KB
-    {128, 128, 1, &stream_get<128, 128, 2, 2>}, //  99 KB
+    // resident weight slice (BRES): only activations stream through the ring
+    {64, 64, 4, true, &stream_get<64, 64, 4, true>},
+    {64, 128, 4, true, &stream_get<64, 128, 4, true>},
+    {128, 64, 4, true, &stream_get<128, 64, 4, true>},
+    {64, 64, 6, true, &stream_get<64, 64, 6, true>},
+    {64, 128, 3, true, &stream_get<64, 128, 3, true>},
+    // weights streamed with every K step (large K)
+    {64, 64, 4, false, &stream_get<64, 64, 4, false>},
+    {128, 64, 4, false, &stream_get<128, 64, 4, false>},
+    {128, 128, 3, false, &stream_get<128, 128, 3, false>},
+    {64, 128, 4, false, &stream_get<64, 128, 4, false>},
+    // nt (streaming) cache policy on activations / residual / output
+    {64, 128, 3, true, &stream_get<64, 128, 3, true, 2>},
+    {64, 64, 4, true, &stream_get<64, 64, 4, true, 2>},
+    {128, 128, 3, false, &stream_get<128, 128, 3, false, 2>},
 };
+
+}  // namespace kvedge
+
+namespace kvedge {
 
 int stream_num_tiles() { return (int)(sizeof(kStreamTiles) / sizeof(kStreamTiles[0])); }
 
@@ -301,13 +367,26 @@ int stream_launch(const KvConvParams* p, int tile, hipStream_t stream) {
     if (!p->x2 || x2b >= kOOB || p->K1 % BK || (p->Kpad - p->K1) % BK) return -10;
   }
   const StreamTile& e = kStreamTiles[tile];
+  const bool res = p->res != nullptr;
+  const int lds = stream_lds_bytes(e.bm, e.bn, e.d, res, e.bres, p->Kpad);
+  if (lds > kLdsMax) return -11;  // resident weight slice does not fit
   const int nbm = (p->M + e.bm - 1) / e.bm, nbn = (p->Cout + e.bn - 1) / e.bn;
   if (nbm <= 0 || nbn <= 0) return 0;
-  int mgroups = (256 * e.per_cu + nbn - 1) / nbn;  // ~per_cu workgroups per CU
+  int per_cu = kLdsMax / lds;
+  if (per_cu > 4) per_cu = 4;
+  static const int per_cu_env = [] {  // tuning knob: cap resident workgroups per CU
+    const char* s = getenv("KVEDGE_STREAM_PER_CU");
+    return s ? atoi(s) : 0;
+  }();
+  if (per_cu_env > 0 && per_cu_env < per_cu) per_cu = per_cu_env;
+  int mgroups = (256 * per_cu + nbn - 1) / nbn;  // ~per_cu workgroups on every CU
   if (mgroups > nbm) mgroups = nbm;
   if (mgroups < 1) mgroups = 1;
-  hipLaunchKernelGGL(e.get(p->mode, p->res != nullptr), dim3((unsigned)(mgroups * nbn)), dim3(256),
-                     0, stream, *p);
+  StreamFn fn = e.get(p->mode, res);
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+    return -7;
+  hipLaunchKernelGGL(fn, dim3((unsigned)(mgroups * nbn)), dim3(256), (unsigned)lds, stream, *p);
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }
 

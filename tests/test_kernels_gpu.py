@@ -82,8 +82,20 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale + 0.02
 
 
-N_TILES = 17  # v1 register-staged (0-5) + v2 LDS-DMA (6-12) + v3 streaming (13-16)
-STREAM0 = 13  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
+N_TILES = 30  # v1 register-staged (0-5) + v2 LDS-DMA (6-17) + v3 streaming (18-29)
+STREAM0 = 18  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
+# v3 (bm, bn, ring depth, weight slice resident in LDS) -- conv_stream.hip kStreamTiles
+STREAM_TILES = [(64, 64, 4, True), (64, 128, 4, True), (128, 64, 4, True), (64, 64, 6, True),
+                (64, 128, 3, True), (64, 64, 4, False), (128, 64, 4, False), (128, 128, 3, False),
+                (64, 128, 4, False), (64, 128, 3, True), (64, 64, 4, True), (128, 128, 3, False)]
+
+
+def _stream_fits(tile, kpad, res):
+    """Mirror of stream_lds_bytes(): resident-weight tiles refuse slices > 160 KiB LDS."""
+    bm, bn, d, bres = STREAM_TILES[tile - STREAM0]
+    lds = 2 * (d * (bm * 64 + (0 if bres else bn * 64)) + (bn * kpad if bres else 0)
+               + bm * (bn + 8))
+    return lds <= 160 * 1024
 
 
 def test_tile_count():
@@ -102,7 +114,7 @@ def test_tile_count():
 ])
 def test_conv_every_tile(tile, case):
     N, H, W, cin, cout, k, s, p, act, res, lx, xc = case
-    if tile >= STREAM0 and (k != 1 or s != 1):
+    if tile >= STREAM0 and (k != 1 or s != 1 or not _stream_fits(tile, (cin * k * k + 63) // 64 * 64, res)):
         with pytest.raises(RuntimeError):
             _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
                        tile=tile)
@@ -125,6 +137,11 @@ def test_conv_stream_gemm(tile, case):
     """Persistent streaming 1x1 kernel: multi-tile walks, residual prefetch across
     tiles, residual before/after the activation, sliced operands, tails."""
     N, H, W, cin, cout, act, res, lx, xc, ly, yc = case
+    if tile >= STREAM0 and not _stream_fits(tile, (cin + 63) // 64 * 64, res):
+        with pytest.raises(RuntimeError):
+            _conv_case(N, H, W, cin, cout, 1, 1, 0, act, res=res, ldx_extra=lx, x_coff=xc,
+                       ldy_extra=ly, y_coff=yc, tile=tile)
+        return
     err, scale = _conv_case(N, H, W, cin, cout, 1, 1, 0, act, res=res, ldx_extra=lx, x_coff=xc,
                             ldy_extra=ly, y_coff=yc, tile=tile)
     assert err <= 0.02 * scale + 0.02, (tile, case, err, scale)

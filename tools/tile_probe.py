@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Full tile x layer timing matrix for ResNet-50's 1x1 (GEMM-mode / dual) convs: every
+kernel-family tile that accepts the layer, standalone, with effective HBM bandwidth.
+Complements tools/layer_bench.py (which only reports the best tile)."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--tiles", default="")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    import torch
+    from kvedge_amd import ops
+    from kvedge_amd.ops import ConvSpec
+
+    assert ops.load()
+    B = a.batch
+    # (name, hw, cin, cout, res)
+    layers = [("s1.c1a", 56, 64, 64, False), ("s1.c1", 56, 256, 64, False),
+              ("s1.c3", 56, 64, 256, True), ("s2.c1a", 56, 256, 128, False),
+              ("s2.c1", 28, 512, 128, False), ("s2.c3", 28, 128, 512, True),
+              ("s3.c1", 14, 1024, 256, False), ("s3.c3", 14, 256, 1024, True),
+              ("s4.c3", 7, 512, 2048, True), ("s1.c3-nores", 56, 64, 256, False),
+              ("s2.c3-nores", 28, 128, 512, False), ("s1.c1a-wide", 56, 64, 512, False)]
+    if a.only:
+        layers = [l for l in layers if l[0] in a.only.split(",")]
+    ntiles = int(torch.ops.kvedge.conv_num_tiles())
+    tiles = [int(t) for t in a.tiles.split(",")] if a.tiles else list(range(ntiles))
+
+    def timeit(fn):
+        for _ in range(3):
+            fn()
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        st.record()
+        for _ in range(a.iters):
+            fn()
+        en.record()
+        torch.cuda.synchronize()
+        return st.elapsed_time(en) / a.iters * 1e3
+
+    print("| layer | " + " | ".join(str(t) for t in tiles) + " | best GB/s |")
+    print("|---" * (len(tiles) + 2) + "|")
+    for name, hw, cin, cout, res in layers:
+        spec = ConvSpec.auto(cin, cout, 1, 1, 0, ops.ACT_RELU)
+        x = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
+        w = (torch.randn(cout, spec.Kpad, device="cuda") * 0.05).to(torch.bfloat16)
+        b = torch.randn(cout, device="cuda")
+        out = torch.empty(B, hw, hw, cout, device="cuda", dtype=torch.bfloat16)
+        r = torch.randn(B, hw, hw, cout, device="cuda").to(torch.bfloat16) if res else None
+        byts = 2.0 * B * hw * hw * (cin + cout * (2 if res else 1)) + 2.0 * cout * spec.Kpad
+        cells, best = [], 1e30
+        for t in tiles:
+            try:
+                us = timeit(lambda: ops.conv2d(x, spec, w, b, res=r, out=out, tile=t))
+            except RuntimeError:
+                cells.append("-")
+                continue
+            best = min(best, us)
+            cells.append(f"{us:.1f}")
+        print(f"| {name} | " + " | ".join(cells) + f" | {byts / best / 1e3:.0f} |", flush=True)
+
+
+if __name__ == "__main__":
+    main()
