@@ -187,25 +187,41 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams 
   auto compute = [&](int slot, int kt) __attribute__((always_inline)) {
     const bf16* As = smem + slot * SLOT;
     const bf16* Bs = BRES ? Bres + kt * BN * BK : As + SA;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
+    // fragments double-buffered in registers: the ds_reads of step ks+1 are issued
+    // before the MFMAs of step ks, so LDS latency hides under the MFMA pipe instead of
+    // an lgkmcnt(0) stall in front of every group of MFMAs
+    bf16x8 af[2][TM], bfg[2][TN];
+    auto load = [&](int buf, int ks) __attribute__((always_inline)) {
       const int q = ks * 2 + fh;
-      bf16x8 af[TM], bfg[TN];
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
         const int row = wm * WTM + tm * 32 + fr;
-        af[tm] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((q ^ ((row >> 1) & 7)) << 3));
+        af[buf][tm] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((q ^ ((row >> 1) & 7)) << 3));
       }
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
         const int row = wn * WTN + tn * 32 + fr;
-        bfg[tn] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((q ^ ((row >> 1) & 7)) << 3));
+        bfg[buf][tn] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((q ^ ((row >> 1) & 7)) << 3));
       }
+    };
+    load(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (ks < 3) load((ks + 1) & 1, ks + 1);
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
-          acc[tn][tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfg[tn], af[tm], acc[tn][tm], 0, 0, 0);
+          acc[tn][tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfg[ks & 1][tn], af[ks & 1][tm],
+                                                                acc[tn][tm], 0, 0, 0);
+    }
+    // pin the order for the scheduler (it otherwise re-coalesces both register sets):
+    // reads(0) | reads(1) MFMAs(0) | reads(2) MFMAs(1) | reads(3) MFMAs(2) | MFMAs(3)
+    __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (ks < 3) __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
     }
   };
 

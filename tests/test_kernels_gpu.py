@@ -82,8 +82,8 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale + 0.02
 
 
-N_TILES = 30  # v1 register-staged (0-5) + v2 LDS-DMA (6-17) + v3 streaming (18-29)
-STREAM0 = 18  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
+N_TILES = 32  # v1 register-staged (0-5) + v2 LDS-DMA (6-19) + v3 streaming (20-31)
+STREAM0 = 20  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
 # v3 (bm, bn, ring depth, weight slice resident in LDS) -- conv_stream.hip kStreamTiles
 STREAM_TILES = [(64, 64, 4, True), (64, 128, 4, True), (128, 64, 4, True), (64, 64, 6, True),
                 (64, 128, 3, True), (64, 64, 4, False), (128, 64, 4, False), (128, 128, 3, False),
@@ -264,3 +264,35 @@ def test_conv_dual_rejects_v1_tiles():
     w = torch.zeros(64, 128, dtype=torch.bfloat16, device="cuda")
     with pytest.raises(RuntimeError):
         ops.conv_dual(x1, x2, w, None, ops.ACT_NONE, 1, tile=0)
+
+
+@pytest.mark.parametrize("tile", [-1, 1, 6, 7, 12, 13, STREAM0, STREAM0 + 1, STREAM0 + 5])
+@pytest.mark.parametrize("k", [1, 3])
+def test_conv_poisoned_canary(tile, k):
+    """SURVEY §5.2 poisoned-buffer check: the output buffer is NaN-filled, with a NaN
+    canary tail after the tensor and NaN in the channels outside the written slice.  Every
+    written element must be finite, and every byte outside the slice must stay NaN
+    (a kernel that writes past M/N tails or outside [y_coff, y_coff+cout) fails here)."""
+    if tile >= STREAM0 and k != 1:
+        pytest.skip("v3 tiles take 1x1 GEMMs only")
+    N, H, W, cin, cout, ldy, y_coff = 3, 13, 11, 64, 72, 104, 16
+    spec = ConvSpec.auto(cin, cout, k, 1, k // 2, ops.ACT_RELU)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(N, H, W, cin, generator=g).to(torch.bfloat16).cuda()
+    w = ops.pack_conv_weight(torch.randn(cout, cin, k, k, generator=g) * 0.1, spec).cuda()
+    b = torch.randn(cout, generator=g).cuda()
+    Ho, Wo = spec.out_hw(H, W)
+    n_out = N * Ho * Wo * ldy
+    flat = torch.full((n_out + 4096,), float("nan"), dtype=torch.bfloat16, device="cuda")
+    out = flat[:n_out].view(N, Ho, Wo, ldy)
+    ops.conv2d(x, spec, w, b, out=out, y_coff=y_coff, tile=tile)
+    torch.cuda.synchronize()
+    o = out.cpu().float()
+    inside = o[..., y_coff:y_coff + cout]
+    assert torch.isfinite(inside).all()
+    mask = torch.ones(ldy, dtype=torch.bool)
+    mask[y_coff:y_coff + cout] = False
+    assert torch.isnan(o[..., mask]).all()
+    assert torch.isnan(flat[n_out:].cpu().float()).all()
+    ref = ops.conv2d(x.cpu(), spec, w.cpu(), b.cpu())
+    assert (inside - ref.float()).abs().max().item() <= 0.02 * ref.float().abs().max().item() + 0.02

@@ -22,13 +22,15 @@ def main():
 
     assert ops.load()
     B = a.batch
-    # (name, hw, cin, cout, res)
+    # (name, hw, cin, cout, res[, k])
     layers = [("s1.c1a", 56, 64, 64, False), ("s1.c1", 56, 256, 64, False),
               ("s1.c3", 56, 64, 256, True), ("s2.c1a", 56, 256, 128, False),
               ("s2.c1", 28, 512, 128, False), ("s2.c3", 28, 128, 512, True),
               ("s3.c1", 14, 1024, 256, False), ("s3.c3", 14, 256, 1024, True),
               ("s4.c3", 7, 512, 2048, True), ("s1.c3-nores", 56, 64, 256, False),
-              ("s2.c3-nores", 28, 128, 512, False), ("s1.c1a-wide", 56, 64, 512, False)]
+              ("s2.c3-nores", 28, 128, 512, False), ("s1.c1a-wide", 56, 64, 512, False),
+              ("s1.c2", 56, 64, 64, False, 3), ("s2.c2", 28, 128, 128, False, 3),
+              ("s3.c2", 14, 256, 256, False, 3), ("s4.c2", 7, 512, 512, False, 3)]
     if a.only:
         layers = [l for l in layers if l[0] in a.only.split(",")]
     ntiles = int(torch.ops.kvedge.conv_num_tiles())
@@ -46,16 +48,18 @@ def main():
         torch.cuda.synchronize()
         return st.elapsed_time(en) / a.iters * 1e3
 
-    print("| layer | " + " | ".join(str(t) for t in tiles) + " | best GB/s |")
+    print("| layer | " + " | ".join(str(t) for t in tiles) + " | best |")
     print("|---" * (len(tiles) + 2) + "|")
-    for name, hw, cin, cout, res in layers:
-        spec = ConvSpec.auto(cin, cout, 1, 1, 0, ops.ACT_RELU)
+    for name, hw, cin, cout, res, *kk in layers:
+        k = kk[0] if kk else 1
+        spec = ConvSpec.auto(cin, cout, k, 1, k // 2, ops.ACT_RELU)
         x = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
         w = (torch.randn(cout, spec.Kpad, device="cuda") * 0.05).to(torch.bfloat16)
         b = torch.randn(cout, device="cuda")
         out = torch.empty(B, hw, hw, cout, device="cuda", dtype=torch.bfloat16)
         r = torch.randn(B, hw, hw, cout, device="cuda").to(torch.bfloat16) if res else None
         byts = 2.0 * B * hw * hw * (cin + cout * (2 if res else 1)) + 2.0 * cout * spec.Kpad
+        flops = 2.0 * B * hw * hw * cout * cin * k * k
         cells, best = [], 1e30
         for t in tiles:
             try:
@@ -65,7 +69,8 @@ def main():
                 continue
             best = min(best, us)
             cells.append(f"{us:.1f}")
-        print(f"| {name} | " + " | ".join(cells) + f" | {byts / best / 1e3:.0f} |", flush=True)
+        print(f"| {name} | " + " | ".join(cells) + f" | {byts / best / 1e3:.0f} GB/s "
+              f"{flops / best / 1e6:.0f} TF/s |", flush=True)
 
 
 if __name__ == "__main__":
