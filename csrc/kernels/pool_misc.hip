@@ -68,53 +68,78 @@ __global__ __launch_bounds__(kBlock) void maxpool_kernel(const bf16* __restrict_
 // ---- K5b SPPF: y1 = mp5(x), y2 = mp5(y1) = mp9(x), y3 = mp13(x) ------------
 // Composition of stride-1 max filters with -inf padding is the max over the
 // summed window, so one pass over x produces all three slices exactly.
+// Separable, LDS-resident: one workgroup per (image, 16-channel group) holds the
+// H x W x 16 input slice, the three row-max images (radius 2/4/6) and writes the
+// column maxes of each -- O(13+13) reads per output instead of the 13x13 window scan
+// (the first version read 169 x 16 B per output from global: 155 us at 64x20x20x128).
+constexpr int kSppfCg = 16;  // channels per workgroup
 __global__ __launch_bounds__(kBlock) void sppf_kernel(bf16* __restrict__ buf, int N, int H,
                                                       int W, int C) {
-  const int C8 = C / 8;
+  extern __shared__ __attribute__((aligned(16))) bf16 sp[];  // 4 x [H*W][16]
+  const int HW = H * W;
+  const int ncg = C / kSppfCg;
+  const int n = blockIdx.x / ncg, cg = blockIdx.x - n * ncg;
   const int ld = 4 * C;
-  const long long total = (long long)N * H * W * C8;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c8 = (int)(i % C8);
-    long long pix = i / C8;
-    const int w = (int)(pix % W);
-    pix /= W;
-    const int h = (int)(pix % H);
-    const int n = (int)(pix / H);
-    float m5[8], m9[8], m13[8];
+  bf16* in = sp;
+  bf16* hr[3] = {sp + HW * kSppfCg, sp + 2 * HW * kSppfCg, sp + 3 * HW * kSppfCg};
+  bf16* base = buf + (long long)n * HW * ld + cg * kSppfCg;
+  for (int q = threadIdx.x; q < HW * 2; q += kBlock) {  // 2 x 16 B per pixel
+    const int pix = q >> 1, hf = q & 1;
+    *reinterpret_cast<bf16x8*>(in + pix * kSppfCg + hf * 8) =
+        *reinterpret_cast<const bf16x8*>(base + (long long)pix * ld + hf * 8);
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < HW * 2; q += kBlock) {  // row maxes, radius 2 / 4 / 6
+    const int pix = q >> 1, hf = q & 1;
+    const int y = pix / W, x = pix - y * W;
+    float m[3][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) m5[j] = m9[j] = m13[j] = -INFINITY;
-    for (int dr = -6; dr <= 6; ++dr) {
-      const int hi = h + dr;
-      if ((unsigned)hi >= (unsigned)H) continue;
-      const int adr = dr < 0 ? -dr : dr;
-      for (int ds = -6; ds <= 6; ++ds) {
-        const int wi = w + ds;
-        if ((unsigned)wi >= (unsigned)W) continue;
-        const int ads = ds < 0 ? -ds : ds;
-        const int ring = adr > ads ? adr : ads;
-        const bf16x8 v =
-            *reinterpret_cast<const bf16x8*>(buf + ((long long)(n * H + hi) * W + wi) * ld + c8 * 8);
+    for (int k = 0; k < 3; ++k)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float f = (float)v[j];
-          m13[j] = fmaxf(m13[j], f);
-          if (ring <= 4) m9[j] = fmaxf(m9[j], f);
-          if (ring <= 2) m5[j] = fmaxf(m5[j], f);
-        }
+      for (int j = 0; j < 8; ++j) m[k][j] = -INFINITY;
+    for (int dx = -6; dx <= 6; ++dx) {
+      const int xi = x + dx;
+      if ((unsigned)xi >= (unsigned)W) continue;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(in + (y * W + xi) * kSppfCg + hf * 8);
+      const int ad = dx < 0 ? -dx : dx;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = (float)v[j];
+        m[2][j] = fmaxf(m[2][j], f);
+        if (ad <= 4) m[1][j] = fmaxf(m[1][j], f);
+        if (ad <= 2) m[0][j] = fmaxf(m[0][j], f);
       }
     }
-    bf16* o = buf + ((long long)(n * H + h) * W + w) * ld + c8 * 8;
-    bf16x8 a, b, c;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      a[j] = f2bf(m5[j]);
-      b[j] = f2bf(m9[j]);
-      c[j] = f2bf(m13[j]);
+    for (int k = 0; k < 3; ++k) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(m[k][j]);
+      *reinterpret_cast<bf16x8*>(hr[k] + pix * kSppfCg + hf * 8) = o;
     }
-    *reinterpret_cast<bf16x8*>(o + C) = a;
-    *reinterpret_cast<bf16x8*>(o + 2 * C) = b;
-    *reinterpret_cast<bf16x8*>(o + 3 * C) = c;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < HW * 2; q += kBlock) {  // column maxes -> slices 1..3
+    const int pix = q >> 1, hf = q & 1;
+    const int y = pix / W, x = pix - y * W;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int rad = 2 * (k + 1);
+      float m[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+      for (int dy = -rad; dy <= rad; ++dy) {
+        const int yi = y + dy;
+        if ((unsigned)yi >= (unsigned)H) continue;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(hr[k] + (yi * W + x) * kSppfCg + hf * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], (float)v[j]);
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(m[j]);
+      *reinterpret_cast<bf16x8*>(base + (long long)pix * ld + (k + 1) * C + hf * 8) = o;
+    }
   }
 }
 
@@ -327,10 +352,13 @@ extern "C" int kv_maxpool2d(const void* x, void* y, int N, int H, int W, int C, 
 }
 
 extern "C" int kv_sppf_pool(void* buf, int N, int H, int W, int C, hipStream_t s) {
-  if (C % 8) return -1;
-  const long long work = (long long)N * H * W * (C / 8);
-  hipLaunchKernelGGL(sppf_kernel, dim3(grid_for(work)), dim3(kBlock), 0, s, (bf16*)buf, N, H, W,
-                     C);
+  if (C % kSppfCg) return -1;
+  const long long lds = 4LL * H * W * kSppfCg * 2;
+  if (lds > 160 * 1024) return -2;  // 4 LDS images of the 16-channel slice must fit
+  const long long g = (long long)N * (C / kSppfCg);
+  if (g <= 0) return 0;
+  hipLaunchKernelGGL(sppf_kernel, dim3((unsigned)g), dim3(kBlock), (unsigned)lds, s, (bf16*)buf, N,
+                     H, W, C);
   KV_CHECK_LAUNCH();
 }
 

@@ -212,12 +212,13 @@ def test_synth_preprocess_bn():
     assert (y.float() - y_ref.float()).abs().max() <= 0.05
 
 
-def test_yolo_decode_and_nms():
+@pytest.mark.parametrize("hs", [(16, 8, 4), (10, 5, 3)])
+def test_yolo_decode_and_nms(hs):
     nc = 80
-    feats = [_rand((2, h, h, 64 + nc), 10 + i, 2.0) for i, h in enumerate((16, 8, 4))]
+    feats = [_rand((2, h, h, 64 + nc), 10 + i, 2.0) for i, h in enumerate(hs)]
     b_ref, s_ref, c_ref = ops.yolo_decode(feats, (8, 16, 32), nc)
     b, s, c = ops.yolo_decode([f.cuda() for f in feats], (8, 16, 32), nc)
-    assert (b.cpu() - b_ref).abs().max() < 1e-2
+    assert (b.cpu() - b_ref).abs().max() < 2e-2
     assert (s.cpu() - s_ref).abs().max() < 1e-5
     assert torch.equal(c.cpu(), c_ref)
     out_ref, cnt_ref = ops.nms(b_ref, s_ref, c_ref, conf=0.6, iou=0.5, max_det=100)
