@@ -373,6 +373,9 @@ static const GldsTile kGldsTiles[] = {
     // layers are LDS-bandwidth-bound at 64x64 per wave), one workgroup per CU, 3 slots
     {256, 128, &glds_get<256, 128, 2, 2, 3>},
     {128, 256, &glds_get<128, 256, 2, 2, 3>},
+    // narrow N (YOLO's 16/32-channel layers at 160^2 / 320^2): BN = 32, 4 waves along M
+    {128, 32, &glds_get<128, 32, 4, 1>},
+    {256, 32, &glds_get<256, 32, 4, 1>},
 };
 
 int glds_num_tiles() { return (int)(sizeof(kGldsTiles) / sizeof(kGldsTiles[0])); }
