@@ -32,8 +32,9 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("KVEDGE_BENCH_BATCH", 256)),
-                    help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("KVEDGE_BENCH_BATCH", 0)),
+                    help="per-GPU batch (0 = model default: ResNet-50 640, YOLOv8n 256 -- the "
+                         "throughput knees of the batch sweep, profiles/r1_batch_sweep.jsonl)")
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "yolov8n"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-autotune", action="store_true")
@@ -56,6 +57,8 @@ def main(argv=None):
     if not ops.load():
         raise RuntimeError("kvedge native kernels not built: run python -m kvedge_amd._build")
 
+    if a.batch <= 0:
+        a.batch = 640 if a.model == "resnet50" else 256
     t_build = time.perf_counter()
     if a.model == "resnet50":
         from kvedge_amd.models.resnet import KvResNet50

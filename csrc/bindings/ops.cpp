@@ -130,6 +130,25 @@ void maxpool2d(const at::Tensor& x, at::Tensor& y, int64_t N, int64_t H, int64_t
   TORCH_CHECK(rc == 0, "kvedge: maxpool2d failed rc=", rc);
 }
 
+void stem_pool(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, at::Tensor& y,
+               int64_t y_coff) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == 16, "kvedge: stem_pool x must be [N,H,W,16] (s2d)");
+  TORCH_CHECK(w.numel() == 64 * 256, "kvedge: stem_pool w must be [64][256]");
+  TORCH_CHECK(bias.is_cuda() && bias.scalar_type() == at::kFloat && bias.numel() == 64 &&
+                  bias.is_contiguous(), "kvedge: stem_pool bias");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2);
+  TORCH_CHECK(y.dim() == 4 && y.size(0) == N && y.size(1) == (H - 1) / 2 + 1 &&
+                  y.size(2) == (W - 1) / 2 + 1 && y.size(3) >= y_coff + 64,
+              "kvedge: stem_pool y shape");
+  const c10::DeviceGuard g(x.device());
+  const int rc = kv_stem_pool(x.data_ptr(), w.data_ptr(), bias.data_ptr<float>(), y.data_ptr(),
+                              (int)N, (int)H, (int)W, (int)y.size(3), (int)y_coff, cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: stem_pool failed rc=", rc);
+}
+
 void sppf_pool(at::Tensor& buf, int64_t N, int64_t H, int64_t W, int64_t C) {
   check_bf16(buf, "buf");
   TORCH_CHECK(buf.numel() == N * H * W * 4 * C, "kvedge: sppf buffer must be [N,H,W,4C]");
@@ -285,6 +304,7 @@ TORCH_LIBRARY(kvedge, m) {
         "int pad, int K, int ldy, int y_coff, int ldr, int r_coff, int act, int mode, int tile) -> ()");
   m.def("conv_dual(Tensor x1, Tensor x2, Tensor w, Tensor? bias, Tensor(a!) y, int stride2, int act, "
         "int tile) -> ()");
+  m.def("stem_pool(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int y_coff) -> ()");
   m.def("maxpool2d(Tensor x, Tensor(a!) y, int N, int H, int W, int C, int ldx, int x_coff, int ldy, "
         "int y_coff, int k, int stride, int pad, int Ho, int Wo) -> ()");
   m.def("sppf_pool(Tensor(a!) buf, int N, int H, int W, int C) -> ()");
@@ -308,6 +328,7 @@ TORCH_LIBRARY_IMPL(kvedge, CUDA, m) {
   m.impl("conv", conv);
   m.impl("conv_dual", conv_dual);
   m.impl("maxpool2d", maxpool2d);
+  m.impl("stem_pool", stem_pool);
   m.impl("sppf_pool", sppf_pool);
   m.impl("global_avgpool", global_avgpool);
   m.impl("softmax_rows", softmax_rows);

@@ -45,6 +45,12 @@ int kv_conv_num_tiles(void);
 int kv_conv_pick_tile(const KvConvParams* p);
 
 // K5: max pool NHWC (k x k, stride, pad); C % 8 == 0.  ldx/ldy allow channel slices.
+// Fused ResNet stem (4x4 stride-1 conv over the s2d image [N,H,W,16], Cout 64, weights
+// [64][256] packed, bias, ReLU) + 3x3/2 max pool -> y [N,(H+1)/2,(W+1)/2,ldy] at y_coff.
+int kv_stem_pool(const void* x, const void* w, const float* bias, void* y, int N, int H, int W,
+                 int ldy, int y_coff, hipStream_t s);
+int kv_stem_pool_lds_bytes(int W);
+
 int kv_maxpool2d(const void* x, void* y, int N, int H, int W, int C, int ldx, int x_coff,
                  int ldy, int y_coff, int k, int stride, int pad, int Ho, int Wo, hipStream_t s);
 // K5b: YOLOv8 SPPF: buf holds [x | y1 | y2 | y3] channel slices (4*C wide); x is

@@ -1,0 +1,232 @@
+// K2+K5 fused: ResNet stem (7x7/2 conv as a stride-1 4x4 conv over the space-to-depth
+// image, BN folded, ReLU) + 3x3/2 max pool, in one kernel (gfx950).
+//
+// Unfused, the stem writes a [N,112,112,64] bf16 tensor (411 MB at batch 256) that the
+// max pool reads back to write a 4x smaller one: 280 + 119 us per batch-256 step
+// (profiles/r1_v4_resnet50_b256_forward.md), the stem itself at 0.37 PF/s because its
+// implicit GEMM (N = 64, K = 256) re-fetches each input pixel for all 16 taps.
+//
+// Persistent: one workgroup per CU walks bands of RB = 2 pooled output rows (image-major):
+//  * the 64 x 256 weight matrix is loaded into VGPRs ONCE per workgroup (32 fragments
+//    per lane), the next band's input patch is prefetched into registers while this
+//    band computes (a one-band-per-workgroup first version was latency-bound: 17 us
+//    per band, slower than the unfused pair);
+//  * the s2d input rows the band needs (8 rows x (W+3) pixels x 16 ch = 29 KB) are
+//    loaded ONCE into LDS (zero padding included); every tap's A fragment is then a
+//    shifted ds_read_b128 of that patch -- no re-fetch from L2 per tap;
+//  * the 2*RB+1 = 5 stem rows the pool windows touch are computed with
+//    v_mfma_f32_32x32x16_bf16 (D = W * A^T as in conv_glds.hip), the whole 64 x 256
+//    weight matrix held in VGPRs (32 fragments per lane, loaded once);
+//  * bias + ReLU, bf16, into an LDS stem tile; then the 3x3/2 pool reads the tile and
+//    writes the pooled [RB, W/2, 64] band with 16-B stores.
+// 5 stem rows per 4 pooled-input rows is a 25 % recompute of the conv, paid to never
+// write or re-read the 112x112x64 intermediate.
+//
+// Patch layout: pixel p (row-major over the (8, W+3) patch) holds 16 channels = two
+// 16-B halves, stored half-swapped when bit 3 of p is set: 16 consecutive pixels read
+// by one ds_read_b128 lane group then cover all 64 banks (stride 32 B would otherwise
+// collide lanes l and l+8).
+#include "common.h"
+#include "kvedge_kernels.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace kvedge {
+namespace {
+
+constexpr int kCo = 64;        // stem output channels
+constexpr int kCin = 16;       // s2d channels
+constexpr int kTaps = 16;      // 4x4
+constexpr int kK = kTaps * kCin;
+constexpr int kRB = 2;         // pooled rows per workgroup
+constexpr int kSR = 2 * kRB + 1;  // stem rows per band
+constexpr int kPR = kSR + 3;      // patch (input) rows per band
+constexpr int kTS = kCo + 8;      // stem-tile pixel stride (elements)
+
+__device__ __forceinline__ int patch_off(int p, int fh) {  // bytes
+  return p * 32 + ((fh ^ ((p >> 3) & 1)) << 4);
+}
+
+__global__ __launch_bounds__(256, 1) void stem_pool_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ w, const float* __restrict__ bias,
+    bf16* __restrict__ y, int N, int H, int W, int Hp, int Wp, int ldy, int y_coff) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int PW = W + 3;
+  unsigned char* patch = lds;                                       // kPR * PW * 32 B
+  bf16* tile = reinterpret_cast<bf16*>(lds + ((kPR * PW * 32 + 15) & ~15));  // kSR*W px
+
+  const int nbands = (Hp + kRB - 1) / kRB;
+  const int total = N * nbands;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int fr = lane & 31, fh = lane >> 5;
+
+  // ---- weights -> VGPRs, once: fragment (cb, t) rows n = cb*32 + fr, k = t*16 + fh*8 ..
+  bf16x8 wreg[2][kTaps];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int t = 0; t < kTaps; ++t)
+      wreg[cb][t] = *reinterpret_cast<const bf16x8*>(w + (cb * 32 + fr) * kK + t * 16 + fh * 8);
+  // bias for this lane's accumulator channels: n = cb*32 + g*8 + fh*4 + j
+  float4 bv[2][4];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      bv[cb][g] = *reinterpret_cast<const float4*>(bias + cb * 32 + g * 8 + fh * 4);
+
+  // ---- patch prefetch: this thread's 16-B chunks q = tid + 256 i of a band's patch
+  constexpr int kPre = 8;  // chunks per thread: covers kPR * PW * 2 <= 2048 (W <= 125)
+  uint4 pre[kPre];
+  // buffer loads with the range check doing the zero padding: always issued, no branch
+  // and no zero-init of `pre` (a v_mov into a register whose last writer was a VMEM
+  // load made hipcc wait vmcnt(0) -- i.e. for the previous band's pool stores -- at the
+  // top of every band)
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16*>(x), (short)0, N * H * W * kCin * 2, 0x00020000);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  auto fetch = [&](int item) __attribute__((always_inline)) {
+    const int n = item / nbands, band = item - n * nbands;
+    const int iy0 = 2 * band * kRB - 3;
+#pragma unroll
+    for (int i = 0; i < kPre; ++i) {
+      const int q = tid + 256 * i;
+      const int p = q >> 1, h = q & 1;
+      const int pr = p / PW, pc = p - pr * PW;
+      const int iy = iy0 + pr, ix = pc - 2;
+      const bool ok = item < total && q < kPR * PW * 2 && (unsigned)iy < (unsigned)H &&
+                      (unsigned)ix < (unsigned)W;
+      const int off = ok ? (((n * H + iy) * W + ix) * kCin + h * 8) * 2 : 0x7ffffff0;
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+      pre[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto commit = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < kPre; ++i) {
+      const int q = tid + 256 * i;
+      if (q < kPR * PW * 2) *reinterpret_cast<uint4*>(patch + patch_off(q >> 1, q & 1)) = pre[i];
+    }
+  };
+
+  int item = blockIdx.x;
+  fetch(item);
+  commit();
+  __syncthreads();
+  for (; item < total; item += gridDim.x) {
+    const int n = item / nbands, band = item - n * nbands;
+    const int P0 = band * kRB;  // first pooled row
+    const int y0 = 2 * P0 - 1;  // first stem row (may be -1)
+    fetch(item + gridDim.x);    // next band's patch: in flight during this band's MFMAs
+
+    // ---- stem rows of the band: 32-pixel row blocks round-robin over the 4 waves
+    const int npix = kSR * W;
+    const int nrb = (npix + 31) / 32;
+    for (int rb = wv; rb < nrb; rb += 4) {
+      const int j = min(rb * 32 + fr, npix - 1);  // clamp: rows past npix are discarded
+      const int yl = j / W, xc = j - yl * W;
+      const int pbase = yl * PW + xc;
+      floatx16 acc[2];
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[cb][e] = 0.f;
+      bf16x8 af[2];
+      auto load = [&](int buf, int t) __attribute__((always_inline)) {
+        const int p = pbase + (t >> 2) * PW + (t & 3);
+        af[buf] = *reinterpret_cast<const bf16x8*>(patch + patch_off(p, fh));
+      };
+      load(0, 0);
+#pragma unroll
+      for (int t = 0; t < kTaps; ++t) {
+        if (t + 1 < kTaps) load((t + 1) & 1, t + 1);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wreg[0][t], af[t & 1], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wreg[1][t], af[t & 1], acc[1], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+      for (int t = 0; t < kTaps; ++t) {
+        if (t + 1 < kTaps) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      }
+      // bias + ReLU -> bf16 stem tile; stem rows outside the image become 0, which the
+      // pool may read freely (every window also holds a valid post-ReLU value >= 0)
+      const int jr = rb * 32 + fr;
+      const bool ok = jr < npix && (unsigned)(y0 + yl) < (unsigned)H;
+      if (jr < npix) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            bf16x4 o;
+            o[0] = f2bf(ok ? fmaxf(acc[cb][4 * g + 0] + bv[cb][g].x, 0.f) : 0.f);
+            o[1] = f2bf(ok ? fmaxf(acc[cb][4 * g + 1] + bv[cb][g].y, 0.f) : 0.f);
+            o[2] = f2bf(ok ? fmaxf(acc[cb][4 * g + 2] + bv[cb][g].z, 0.f) : 0.f);
+            o[3] = f2bf(ok ? fmaxf(acc[cb][4 * g + 3] + bv[cb][g].w, 0.f) : 0.f);
+            *reinterpret_cast<bf16x4*>(tile + jr * kTS + cb * 32 + g * 8 + fh * 4) = o;
+          }
+      }
+    }
+    __syncthreads();  // stem tile complete; patch no longer read
+
+    // ---- 3x3/2 max pool (pad 1) of the band -> global, 16 B per thread-iteration
+    const int per_row = Wp * (kCo / 8);
+    for (int q = tid; q < kRB * per_row; q += 256) {
+      const int pr = q / per_row, rem = q - pr * per_row;
+      const int px = rem >> 3, c8 = rem & 7;
+      const int P = P0 + pr;
+      if (P >= Hp) continue;
+      float m[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m[e] = 0.f;  // post-ReLU values are >= 0
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+        const int yl = 2 * pr + dy;  // stem row 2P-1+dy - y0
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          const int xs = 2 * px + dx;
+          if ((unsigned)xs >= (unsigned)W) continue;
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(tile + (yl * W + xs) * kTS + c8 * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], (float)v[e]);
+        }
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = f2bf(m[e]);
+      *reinterpret_cast<bf16x8*>(y + ((long long)(n * Hp + P) * Wp + px) * ldy + y_coff + c8 * 8) = o;
+    }
+    commit();         // next band's patch (its loads have landed by now)
+    __syncthreads();  // tile free, patch ready
+  }
+}
+
+}  // namespace
+}  // namespace kvedge
+
+using namespace kvedge;
+
+extern "C" int kv_stem_pool_lds_bytes(int W) {
+  return ((kPR * (W + 3) * 32 + 15) & ~15) + kSR * W * kTS * 2;
+}
+
+extern "C" int kv_stem_pool(const void* x, const void* w, const float* bias, void* y, int N, int H,
+                            int W, int ldy, int y_coff, hipStream_t s) {
+  if (N <= 0) return 0;
+  if (H <= 0 || W <= 0 || ldy % 8 || y_coff % 8 || ldy < y_coff + kCo || !bias) return -1;
+  const int lds = kv_stem_pool_lds_bytes(W);
+  if (lds > 160 * 1024 || kPR * (W + 3) * 2 > 8 * 256) return -2;  // patch prefetch: W <= 125
+  if ((long long)N * H * W * 16 * 2 >= 0x7ffffff0LL) return -4;   // buffer range (2 GiB)
+  const int Hp = (H - 1) / 2 + 1, Wp = (W - 1) / 2 + 1;  // 3x3 / 2, pad 1
+  const long long items = (long long)N * ((Hp + kRB - 1) / kRB);
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const long long g = items < ncu ? items : ncu;  // persistent: one workgroup per CU
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_kernel),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+    return -3;
+  hipLaunchKernelGGL(stem_pool_kernel, dim3((unsigned)g), dim3(256), (unsigned)lds, s,
+                     (const bf16*)x, (const bf16*)w, bias, (bf16*)y, N, H, W, Hp, Wp, ldy, y_coff);
+  return hipGetLastError() == hipSuccess ? 0 : -100;
+}

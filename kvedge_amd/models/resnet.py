@@ -185,6 +185,12 @@ class KvResNet50:
     # a 32-image one 51 MB); the compute-bound late stages run on the whole batch.
     microbatch: int = 0          # 0 = off
     microbatch_blocks: int = 3   # bottlenecks (from the start) run per micro-batch
+    fuse_stem_pool: bool = True  # stem conv + max pool as one kernel (stem_pool.hip)
+
+    def stem_and_pool(self, x: torch.Tensor) -> torch.Tensor:
+        if self.fuse_stem_pool:
+            return ops.stem_pool(x, self.stem.spec, self.stem.w, self.stem.b)
+        return ops.maxpool2d(self.stem(x), 3, 2, 1)
 
     def features(self, x: torch.Tensor) -> torch.Tensor:
         """x: preprocessed bf16 s2d [B,112,112,16] -> final feature map [B,7,7,2048] bf16."""
@@ -194,8 +200,7 @@ class KvResNet50:
         if mb and B > mb and B % mb == 0 and nb > 0:
             full = None
             for i in range(0, B, mb):
-                y = self.stem(x[i:i + mb])
-                y = ops.maxpool2d(y, 3, 2, 1)
+                y = self.stem_and_pool(x[i:i + mb])
                 for b in self.blocks[:nb - 1]:
                     y = b(y)
                 last = self.blocks[nb - 1]
@@ -206,8 +211,7 @@ class KvResNet50:
             x = full
             rest = self.blocks[nb:]
         else:
-            x = self.stem(x)
-            x = ops.maxpool2d(x, 3, 2, 1)
+            x = self.stem_and_pool(x)
             rest = self.blocks
         for b in rest:
             x = b(x)

@@ -206,6 +206,28 @@ def conv_dual(x1: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, bias: Optiona
     return out
 
 
+def stem_pool(x: torch.Tensor, spec: "ConvSpec", w: torch.Tensor, bias: torch.Tensor,
+              out: Optional[torch.Tensor] = None, y_coff: int = 0) -> torch.Tensor:
+    """Fused ResNet stem + max pool: maxpool3x3/2(relu(conv_s2d(x) + bias)).
+
+    x: the space-to-depth image [N, H, W, 16] (ops.preprocess(s2d=True)); spec/w/bias:
+    the s2d stem DeployedConv (4x4, stride 1, pads 2/1, Cout 64, ReLU).  -> [N, H/2, W/2, 64].
+    GPU: one kernel (csrc/kernels/stem_pool.hip), the 112x112x64 stem output never
+    touches HBM.  CPU: the reference conv followed by the reference pool."""
+    assert spec.cin == 16 and spec.cout == 64 and spec.kh == 4 and spec.stride == 1
+    assert spec.pad == 2 and spec.pad_end == 1 and spec.act == ACT_RELU and spec.Kpad == 256
+    N, H, W, _ = x.shape
+    Hp, Wp = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    if out is None:
+        out = torch.empty(N, Hp, Wp, 64, dtype=torch.bfloat16, device=x.device)
+    if x.is_cuda:
+        _native().stem_pool(x, w, bias, out, y_coff)
+    else:
+        y = conv2d(x, spec, w, bias)
+        maxpool2d(y, 3, 2, 1, out=out, y_coff=y_coff)
+    return out
+
+
 def maxpool2d(x: torch.Tensor, k: int, stride: int, pad: int, out: Optional[torch.Tensor] = None,
               C: Optional[int] = None, x_coff: int = 0, y_coff: int = 0) -> torch.Tensor:
     N, H, W, ldx = x.shape

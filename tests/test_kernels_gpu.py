@@ -297,3 +297,29 @@ def test_conv_poisoned_canary(tile, k):
     assert torch.isnan(flat[n_out:].cpu().float()).all()
     ref = ops.conv2d(x.cpu(), spec, w.cpu(), b.cpu())
     assert (inside - ref.float()).abs().max().item() <= 0.02 * ref.float().abs().max().item() + 0.02
+
+
+@pytest.mark.parametrize("shape", [(2, 112, 112), (3, 17, 13), (1, 8, 30)])
+def test_stem_pool_fused(shape):
+    """Fused s2d stem conv + ReLU + 3x3/2 max pool == reference conv then reference pool."""
+    from kvedge_amd.models.layers import DeployedConv
+    import torch.nn as nn
+    N, H, W = shape
+    torch.manual_seed(5)
+    conv = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+    bn = nn.BatchNorm2d(64).eval()
+    bn.running_mean.uniform_(-0.2, 0.2)
+    bn.running_var.uniform_(0.5, 1.5)
+    stem = DeployedConv.stem_s2d(conv, bn, ops.ACT_RELU)
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(N, H, W, 16, generator=g).to(torch.bfloat16)
+    x[..., 3::4] = 0  # the s2d layout's pad channel
+    ref = ops.stem_pool(x, stem.spec, stem.w, stem.b)
+    out = torch.full((N, (H - 1) // 2 + 1, (W - 1) // 2 + 1, 72), float("nan"),
+                     dtype=torch.bfloat16, device="cuda")
+    ops.stem_pool(x.cuda(), stem.spec, stem.w.cuda(), stem.b.cuda(), out=out, y_coff=8)
+    torch.cuda.synchronize()
+    got = out.cpu().float()
+    assert torch.isnan(got[..., :8]).all()
+    err = (got[..., 8:] - ref.float()).abs().max().item()
+    assert err <= 0.02 * ref.float().abs().max().item() + 0.02, err
