@@ -44,6 +44,12 @@ def main(argv=None):
     ap.add_argument("--mb-blocks", type=int, default=int(os.environ.get("KVEDGE_MB_BLOCKS", 3)))
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--profile", default=None, metavar="PATH",
+                    help="after the timed run, profile one eager step per op (HIP events) "
+                         "and write the per-call table as JSON to PATH (rank 0)")
+    ap.add_argument("--native-loop", action="store_true",
+                    help="time the K steps with the native C++ serve loop (csrc/runtime) "
+                         "instead of Python graph.replay() calls")
     a = ap.parse_args(argv)
 
     import torch
@@ -83,9 +89,16 @@ def main(argv=None):
     torch.cuda.synchronize()
     parallel.barrier()
     torch.cuda.synchronize()
+    lat_hist = None
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        eng.run()
+    if a.native_loop and eng.graph is not None:
+        from kvedge_amd.runtime import LatencyHistogram
+
+        lat_hist = LatencyHistogram()
+        eng.serve_native(a.steps, depth=2, hist=lat_hist)
+    else:
+        for _ in range(a.steps):
+            eng.run()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     parallel.barrier()
@@ -131,14 +144,25 @@ def main(argv=None):
             "build_s": round(build_s, 2),
             "replica_checksums": sums,
             "backend": di.backend,
+            "timed_loop": "native" if lat_hist is not None else "python",
         },
     }
+    if lat_hist is not None:
+        lat_hist.allreduce()  # fleet-wide step-latency distribution (one SUM all-reduce)
+        res["extra"]["step_latency_ms"] = {k: round(v, 4) for k, v in lat_hist.summary().items()}
     if di.is_main:
         line = json.dumps(res)
         print(line, flush=True)
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
+    if a.profile and di.is_main:
+        from kvedge_amd.engine.profile import write_profile
+
+        prof = write_profile(eng, a.profile)
+        top = list(prof["by_op_ms"].items())[:6]
+        print(f"# eager-step profile -> {a.profile}: total {prof['total_ms']:.2f} ms; "
+              + ", ".join(f"{k} {v:.2f}" for k, v in top), file=sys.stderr)
     parallel.shutdown()
     return 0
 

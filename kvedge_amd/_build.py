@@ -70,13 +70,14 @@ def _run(cmd):
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 
 
-def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
+def build(force: bool = False, jobs: int = 0, verbose: bool = False, asan: bool = False) -> str:
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(BIN, exist_ok=True)
     inc, lib, abi = _torch_paths()
     headers = _headers()
     kernel_srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
-    runtime_srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    runtime_srcs = sorted(p for p in glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))
+                          if not p.endswith("_main.cpp"))
     bind_srcs = sorted(glob.glob(os.path.join(CSRC, "bindings", "*.cpp")))
     torch_flags = [f"-I{p}" for p in inc] + [
         f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
@@ -103,7 +104,8 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
         o = os.path.join(OBJ, os.path.basename(src) + ".o")
         objs.append(o)
         if force or _stale(o, [src] + headers):
-            tasks.append([hipcc(), *COMMON, *torch_flags, f"-I{py_inc}", "-c", src, "-o", o])
+            tasks.append([hipcc(), *COMMON, *torch_flags, f"-I{py_inc}", f"-I{CSRC}/runtime",
+                          "-c", src, "-o", o])
     if tasks:
         with cf.ThreadPoolExecutor(jobs) as ex:
             for out in ex.map(_run, tasks):
@@ -128,7 +130,24 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False) -> str:
         if force or _stale(out, [src] + extra_src + headers):
             _run([hipcc(), *COMMON, f"-I{CSRC}/runtime", f"-I{CSRC}/kernels", src, *extra_src,
                   "-o", out, f"-L{ROCM}/lib", *libs, f"-Wl,-rpath,{ROCM}/lib"])
+    if asan:
+        build_asan()
     return SO_PATH
+
+
+def build_asan() -> str:
+    """Host-AddressSanitizer + UBSan build of the native runtime self-test.
+    GPU ASan / xnack+ code objects are not available on the MI355X pool, so the
+    sanitizers are applied to host code only (`-Xarch_host -fsanitize=...`)."""
+    os.makedirs(BIN, exist_ok=True)
+    srcs = [os.path.join(CSRC, "runtime", "selftest_main.cpp")] + sorted(
+        p for p in glob.glob(os.path.join(CSRC, "runtime", "*.cpp")) if not p.endswith("_main.cpp"))
+    out = os.path.join(BIN, "kv_runtime_selftest_asan")
+    _run([hipcc(), "-O1", "-g", "-std=c++17", f"--offload-arch={ARCH}",
+          "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+          "-Xarch_host", "-fno-omit-frame-pointer", f"-I{CSRC}/runtime", *srcs, "-o", out,
+          f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib"])
+    return out
 
 
 def main(argv=None):
@@ -136,8 +155,10 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=0)
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--asan", action="store_true",
+                    help="also build the host-ASan/UBSan runtime self-test")
     a = ap.parse_args(argv)
-    path = build(force=a.force, jobs=a.jobs, verbose=a.verbose)
+    path = build(force=a.force, jobs=a.jobs, verbose=a.verbose, asan=a.asan)
     print(path)
 
 

@@ -47,13 +47,16 @@ class InferenceEngine:
     """
 
     def __init__(self, model: Callable, batch: int, image_size: int, device="cuda",
-                 seed: int = 0, use_graph: bool = True):
+                 seed: int = 0, use_graph: bool = True, synthetic: bool = True):
         self.model = model
         self.batch = batch
         self.hw = image_size
         self.device = torch.device(device)
         self.seed = seed
         self.use_graph = use_graph and self.device.type == "cuda"
+        # synthetic=False: the graph reads self.frames as-is (fed by set_frames, or by
+        # the native serve loop from a pinned FrameRing -- kvedge_amd.runtime)
+        self.synthetic = synthetic
         self.frames = torch.empty(batch, image_size, image_size, 3, dtype=torch.uint8,
                                   device=self.device)
         self.step_ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
@@ -63,7 +66,8 @@ class InferenceEngine:
 
     # one full edge-module step: synthesize frames, run the model
     def _step(self):
-        ops.synth_frames(self.frames, self.seed, self.step_ctr)
+        if self.synthetic:
+            ops.synth_frames(self.frames, self.seed, self.step_ctr)
         self.outputs = self.model(self.frames)
         return self.outputs
 
@@ -120,6 +124,29 @@ class InferenceEngine:
             dt = self.run_timed(1)
             st.add(dt)
         return st
+
+    def serve_native(self, n_steps: int, depth: int = 2, hist=None, ring=None,
+                     ring_timeout_ms: int = 1000):
+        """Replay the captured step ``n_steps`` times from the native C++ loop
+        (csrc/runtime: no Python per step, per-step device time into ``hist``).  With a
+        FrameRing, each step first DMAs one pinned frame batch into ``self.frames``
+        (build the engine with synthetic=False so the graph does not overwrite them)."""
+        from .. import runtime
+
+        if self.graph is None:
+            raise RuntimeError("serve_native needs a captured graph (prepare() on a GPU)")
+        if ring is not None and self.synthetic:
+            raise ValueError("ring-fed serving needs InferenceEngine(synthetic=False)")
+        with torch.cuda.device(self.device):
+            return runtime.serve(self.graph, n_steps, depth=depth, hist=hist, ring=ring,
+                                 dev_input=self.frames if ring is not None else None,
+                                 ring_timeout_ms=ring_timeout_ms)
+
+    def memory_plan(self, align: int = 256):
+        """Native arena plan of one step's activations (kvedge_amd.runtime.plan_memory)."""
+        from .. import runtime
+
+        return runtime.plan_memory(lambda: self.model(self.frames), self.batch, align)
 
     def set_frames(self, frames_u8: torch.Tensor):
         """Feed real frames instead of synthetic (disables the synthetic step)."""

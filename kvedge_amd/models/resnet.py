@@ -206,7 +206,7 @@ class KvResNet50:
                 last = self.blocks[nb - 1]
                 if full is None:
                     shp = last.out_shape(y.shape)
-                    full = torch.empty((B,) + shp[1:], dtype=y.dtype, device=y.device)
+                    full = ops.empty((B,) + shp[1:], dtype=y.dtype, device=y.device)
                 last(y, out=full[i:i + mb])  # write straight into the full-batch tensor
             x = full
             rest = self.blocks[nb:]

@@ -187,7 +187,7 @@ class DC2f:
     def __call__(self, x, x_coff=0, out=None, y_coff=0):
         N, H, W, _ = x.shape
         c, n = self.c, self.n
-        cat = torch.empty(N, H, W, (2 + n) * c, dtype=torch.bfloat16, device=x.device)
+        cat = ops.empty(N, H, W, (2 + n) * c, dtype=torch.bfloat16, device=x.device)
         self.cv1(x, x_coff=x_coff, out=cat, y_coff=0)
         for i, (b1, b2, add) in enumerate(self.m):
             t = b1(cat, x_coff=(1 + i) * c)
@@ -209,7 +209,7 @@ class DSPPF:
 
     def __call__(self, x, out=None, y_coff=0):
         N, H, W, _ = x.shape
-        buf = torch.empty(N, H, W, 4 * self.c_, dtype=torch.bfloat16, device=x.device)
+        buf = ops.empty(N, H, W, 4 * self.c_, dtype=torch.bfloat16, device=x.device)
         self.cv1(x, out=buf, y_coff=0)
         ops.sppf_pool(buf, self.c_)
         return self.cv2(buf, out=out, y_coff=y_coff)
@@ -241,7 +241,7 @@ class DDetectLevel:
     def __call__(self, p):
         N, h, w, _ = p.shape
         s = self.stem(p)
-        feat = torch.empty(N, h, w, 4 * REG_MAX + self.nc, dtype=torch.bfloat16, device=p.device)
+        feat = ops.empty(N, h, w, 4 * REG_MAX + self.nc, dtype=torch.bfloat16, device=p.device)
         ta = self.a1(s, x_coff=0)
         self.a2(ta, out=feat, y_coff=0)
         tb = self.b1(s, x_coff=self.ca)
@@ -311,10 +311,10 @@ class KvYoloV8n:
         x = self.b3(x)                                # [N,80,80,64]
         H3 = x.shape[1]
         H4, H5 = H3 // 2, H3 // 4
-        cat14 = torch.empty(N, H3, H3, 192, dtype=bf, device=dev)   # [up(h12) 128 | p3b 64]
-        cat11 = torch.empty(N, H4, H4, 384, dtype=bf, device=dev)   # [up(p5b) 256 | p4b 128]
-        cat17 = torch.empty(N, H4, H4, 192, dtype=bf, device=dev)   # [h16 64 | h12 128]
-        cat20 = torch.empty(N, H5, H5, 384, dtype=bf, device=dev)   # [h19 128 | p5b 256]
+        cat14 = ops.empty(N, H3, H3, 192, dtype=bf, device=dev)   # [up(h12) 128 | p3b 64]
+        cat11 = ops.empty(N, H4, H4, 384, dtype=bf, device=dev)   # [up(p5b) 256 | p4b 128]
+        cat17 = ops.empty(N, H4, H4, 192, dtype=bf, device=dev)   # [h16 64 | h12 128]
+        cat20 = ops.empty(N, H5, H5, 384, dtype=bf, device=dev)   # [h19 128 | p5b 256]
         self.b4(x, out=cat14, y_coff=128)                          # p3b
         x = self.b5(cat14, x_coff=128)                             # [N,40,40,128]
         self.b6(x, out=cat11, y_coff=256)                          # p4b

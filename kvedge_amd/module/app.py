@@ -28,7 +28,7 @@ from typing import Any, Dict, Optional, Tuple
 
 import torch
 
-from .. import parallel
+from .. import ops, parallel
 from .config import ModuleConfig
 from .transport import Transport, now_iso
 
@@ -67,6 +67,14 @@ class ModuleApp:
         self._win_imgs = 0
         self._win_t0 = 0.0
         self._lat_ms = []
+        # native log-linear histogram (csrc/runtime): replicas merge it with one SUM
+        # all-reduce, so the reported p99 is the fleet's true p99, not a max of p99s.
+        # (device != cuda and no built library: plain list, CPU tests only)
+        self._hist = None
+        if self.device.type == "cuda" or ops.load():
+            from ..runtime import LatencyHistogram
+
+            self._hist = LatencyHistogram()
         self._last_report = 0.0
         self.last_telemetry: Optional[Dict[str, Any]] = None
         self.rank = parallel.info().rank
@@ -156,7 +164,10 @@ class ModuleApp:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         dt = self.clock() - t0
-        self._lat_ms.append(dt * 1e3)
+        if self._hist is not None:
+            self._hist.add_ms(dt * 1e3)
+        else:
+            self._lat_ms.append(dt * 1e3)
         self._win_imgs += self.cfg.batch
         self.state["total_images"] += self.cfg.batch
         self.state["total_steps"] += 1
@@ -187,9 +198,13 @@ class ModuleApp:
     def _summary(self) -> Dict[str, Any]:
         now = self.clock()
         win = max(now - self._win_t0, 1e-9)
+        ips = self._win_imgs / win
+        if self._hist is not None:
+            p50, p99 = self._hist.quantiles_us([0.5, 0.99])
+            return {"images_per_s": ips, "p50_ms": p50 / 1e3, "p99_ms": p99 / 1e3,
+                    "window_s": win, "steps": self._hist.count}
         lat = sorted(self._lat_ms)
         q = lambda p: lat[min(len(lat) - 1, int(round(p / 100 * (len(lat) - 1))))] if lat else 0.0  # noqa
-        ips = self._win_imgs / win
         return {"images_per_s": ips, "p50_ms": q(50), "p99_ms": q(99), "window_s": win,
                 "steps": len(lat)}
 
@@ -198,7 +213,11 @@ class ModuleApp:
         ips_total, lat_max = s["images_per_s"], s["p99_ms"]
         if self.world > 1:  # C2 + C3 off the hot path, once per report interval
             ips_total = parallel.allreduce_scalars([s["images_per_s"]], op="sum")[0]
-            lat_max = parallel.allreduce_scalars([s["p99_ms"]], op="max")[0]
+            if self._hist is not None:  # fleet p99 from the merged histogram
+                self._hist.allreduce()
+                lat_max = self._hist.quantiles_us([0.99])[0] / 1e3
+            else:
+                lat_max = parallel.allreduce_scalars([s["p99_ms"]], op="max")[0]
         msg = {"ts": now_iso(), "model": self.cfg.model, "batch": self.cfg.batch,
                "dtype": self.cfg.dtype, "images_per_s": round(ips_total, 2),
                "images_per_s_rank": round(s["images_per_s"], 2),
@@ -211,6 +230,8 @@ class ModuleApp:
             self.state["messages"] += 1
         self.last_telemetry = msg
         self._win_imgs, self._lat_ms = 0, []
+        if self._hist is not None:
+            self._hist.reset()
         self._win_t0 = self._last_report = self.clock()
         self._save_state()
         return msg

@@ -80,6 +80,26 @@ def library_path() -> str:
     return _LIB_PATH
 
 
+# ---------------------------------------------------------------------------
+# activation allocation (every op/model output goes through here so the native arena
+# planner can see tensor lifetimes: kvedge_amd.runtime.plan_memory)
+# ---------------------------------------------------------------------------
+_recorder = None
+
+
+def empty(*shape, dtype=None, device=None) -> torch.Tensor:
+    t = torch.empty(*shape, dtype=dtype, device=device)
+    if _recorder is not None:
+        _recorder(t)
+    return t
+
+
+def set_alloc_recorder(fn) -> None:
+    """Install (or clear with None) a callback seeing every activation allocation."""
+    global _recorder
+    _recorder = fn
+
+
 def _native():
     if not load():
         raise RuntimeError(
@@ -176,7 +196,7 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, w: torch.Tensor, bias: Optional[torc
     N, H, W, ldx = x.shape
     Ho, Wo = spec.out_hw(H, W)
     if out is None:
-        out = torch.empty(N, Ho, Wo, spec.cout, dtype=torch.bfloat16, device=x.device)
+        out = empty(N, Ho, Wo, spec.cout, dtype=torch.bfloat16, device=x.device)
     assert out.shape[:3] == (N, Ho, Wo), (out.shape, (N, Ho, Wo))
     ldy = out.shape[3]
     ldr = res.shape[-1] if res is not None else 0
@@ -198,7 +218,7 @@ def conv_dual(x1: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, bias: Optiona
     N, Ho, Wo, K1 = x1.shape
     cout = w.shape[0]
     if out is None:
-        out = torch.empty(N, Ho, Wo, cout, dtype=torch.bfloat16, device=x1.device)
+        out = empty(N, Ho, Wo, cout, dtype=torch.bfloat16, device=x1.device)
     if x1.is_cuda:
         _native().conv_dual(x1, x2, w, bias, out, stride2, act, tile)
     else:
@@ -219,7 +239,7 @@ def stem_pool(x: torch.Tensor, spec: "ConvSpec", w: torch.Tensor, bias: torch.Te
     N, H, W, _ = x.shape
     Hp, Wp = (H - 1) // 2 + 1, (W - 1) // 2 + 1
     if out is None:
-        out = torch.empty(N, Hp, Wp, 64, dtype=torch.bfloat16, device=x.device)
+        out = empty(N, Hp, Wp, 64, dtype=torch.bfloat16, device=x.device)
     if x.is_cuda:
         _native().stem_pool(x, w, bias, out, y_coff)
     else:
@@ -235,7 +255,7 @@ def maxpool2d(x: torch.Tensor, k: int, stride: int, pad: int, out: Optional[torc
     Ho = (H + 2 * pad - k) // stride + 1
     Wo = (W + 2 * pad - k) // stride + 1
     if out is None:
-        out = torch.empty(N, Ho, Wo, C, dtype=x.dtype, device=x.device)
+        out = empty(N, Ho, Wo, C, dtype=x.dtype, device=x.device)
     if x.is_cuda:
         _native().maxpool2d(x, out, N, H, W, C, ldx, x_coff, out.shape[3], y_coff, k, stride, pad,
                             Ho, Wo)
@@ -258,7 +278,7 @@ def sppf_pool(buf: torch.Tensor, C: int) -> torch.Tensor:
 def global_avgpool(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     N, H, W, C = x.shape
     if out is None:
-        out = torch.empty(N, C, dtype=x.dtype, device=x.device)
+        out = empty(N, C, dtype=x.dtype, device=x.device)
     if x.is_cuda:
         _native().global_avgpool(x, out, N, H * W, C)
     else:
@@ -269,9 +289,9 @@ def global_avgpool(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch
 def softmax_rows(x: torch.Tensor, out: Optional[torch.Tensor] = None,
                  argmax: Optional[torch.Tensor] = None):
     if out is None:
-        out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+        out = empty(x.shape, dtype=torch.float32, device=x.device)
     if argmax is None:
-        argmax = torch.empty(x.shape[0], dtype=torch.int64, device=x.device)
+        argmax = empty(x.shape[0], dtype=torch.int64, device=x.device)
     if x.is_cuda:
         _native().softmax_rows(x, out, argmax)
     else:
@@ -301,9 +321,9 @@ def yolo_decode(feats: Sequence[torch.Tensor], strides: Sequence[int], nc: int,
     A = sum(h * w for h, w in hw)
     dev = f0.device
     if boxes is None:
-        boxes = torch.empty(N, A, 4, dtype=torch.float32, device=dev)
-        scores = torch.empty(N, A, dtype=torch.float32, device=dev)
-        cls = torch.empty(N, A, dtype=torch.int32, device=dev)
+        boxes = empty(N, A, 4, dtype=torch.float32, device=dev)
+        scores = empty(N, A, dtype=torch.float32, device=dev)
+        cls = empty(N, A, dtype=torch.int32, device=dev)
     if f0.is_cuda:
         _native().yolo_decode(f0, f1, f2, hw[0][0], hw[0][1], hw[1][0], hw[1][1], hw[2][0],
                               hw[2][1], strides[0], strides[1], strides[2], nc, boxes, scores, cls)
@@ -316,8 +336,8 @@ def nms(boxes, scores, cls, conf: float = 0.25, iou: float = 0.7, max_det: int =
         out=None, count=None):
     N = scores.shape[0]
     if out is None:
-        out = torch.empty(N, max_det, 6, dtype=torch.float32, device=scores.device)
-        count = torch.empty(N, dtype=torch.int32, device=scores.device)
+        out = empty(N, max_det, 6, dtype=torch.float32, device=scores.device)
+        count = empty(N, dtype=torch.int32, device=scores.device)
     if scores.is_cuda:
         _native().nms(boxes, scores, cls, conf, iou, max_det, out, count)
     else:
@@ -348,7 +368,7 @@ def preprocess(x: torch.Tensor, out: Optional[torch.Tensor] = None, mean=IMAGENE
     N, H, W, _ = x.shape
     if out is None:
         shape = (N, H // 2, W // 2, 16) if s2d else (N, H, W, 4)
-        out = torch.empty(shape, dtype=torch.bfloat16, device=x.device)
+        out = empty(shape, dtype=torch.bfloat16, device=x.device)
     if x.is_cuda:
         _native().preprocess(x, out, list(mean), list(std))
     else:
