@@ -1,0 +1,301 @@
+// K2 v4: direct 3x3 convolution (stride 1 or 2, pad 1) for narrow channel counts,
+// NHWC bf16, fp32 accumulate (gfx950).
+//
+// Why a fourth conv family.  For 3x3 convs with few channels the implicit-GEMM families
+// re-stage the SAME input pixels once per tap (9x the A bytes through L2 -> LDS) while
+// the narrow N gives each staged byte few MACs:
+//   ResNet-50 stage 1, 64 -> 64 @56x56: 285 us per conv at batch 640 (0.52 PF/s) on the
+//     best v1/v2 tile against a ~0.1 ms HBM floor;
+//   YOLOv8n 16/32-channel convs @160x160 and @80x80: 4-6x their HBM floor
+//     (profiles/r1_v6_yolov8n_b256_forward.md, conv_glds<128,32,4,1,3,2>).
+// Here every input pixel is staged ONCE per band and all taps read it in place:
+//
+//  * Persistent, one 512-thread workgroup per CU (2 waves per SIMD) walking bands of kR
+//    output rows of one image.  The band's input patch (halo rows/cols and zero padding
+//    included, the padding via the buffer range check) is prefetched into VGPRs during
+//    the previous band's MFMAs and committed to LDS between bands.
+//  * Each wave owns one 32-channel block of Cout and holds that block's packed weights
+//    for the whole kernel (9*CIN/16 MFMA fragments: 36 VGPRs at CIN 16 .. 144 at CIN 64).
+//    Weights are read from HBM once per CU, never re-staged.
+//  * A 32-pixel output block is 9*CIN/16 v_mfma_f32_32x32x16_bf16, each fed by one
+//    ds_read_b128 of the patch.  Patch pixels sit at a pitch of CIN*2 + 16 bytes (48, 80,
+//    144 B): 16 consecutive pixels' 16-B reads then hit all 64 banks exactly once, so the
+//    LINEAR layout is conflict-free.  The three tap-row base pointers are formed once per
+//    block; every tap/k-step offset is then a compile-time constant (the ds_read
+//    immediate): no VALU per MFMA.
+//  * Accumulators are seeded with the folded-BN bias; the epilogue is act + cvt into an
+//    LDS output tile; the store pass adds the residual (YOLO Bottleneck: x + SiLU(conv))
+//    and writes full 16-B channel chunks, with channel-slice (ldy / y_coff) support.
+//  * Bands are dealt XCD-aware: concurrently running neighbour bands of one image sit on
+//    one XCD, so their shared halo rows come from one L2.
+#include <stdlib.h>
+
+#include "common.h"
+#include "kvedge_kernels.h"
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace kvedge {
+namespace {
+
+constexpr int kNT = 512;
+constexpr int kOOB = 0x7ffffff0;
+constexpr int kLds = 160 * 1024;
+
+template <int CIN>
+struct DirectCfg {
+  static constexpr int PB = CIN * 2 + 16;         // patch bytes per pixel
+  static constexpr int CPP = CIN / 8;             // 16-B chunks per pixel
+  static constexpr int KPT = CIN / 16;            // 16-wide k-steps per tap
+  static constexpr int KS = 9 * KPT;              // k-steps per output block
+  static constexpr int PRE = CIN >= 64 ? 7 : 10;  // prefetch uint4 per thread (VGPR budget)
+  static constexpr int MAX_PATCH = PRE * kNT * 16;
+};
+
+template <int CIN, int COUT, int S, int ACT, bool RES>
+__global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvParams p, int kR,
+                                                                int PW, int patch_rows) {
+  using C = DirectCfg<CIN>;
+  constexpr int NCB = (COUT + 31) / 32;  // 32-channel blocks
+  static_assert(8 % NCB == 0, "waves split evenly over channel blocks");
+  constexpr int NPH = 8 / NCB;           // pixel-block phases
+  constexpr int OS = COUT + 8;           // output tile pixel stride (elements)
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  unsigned char* patch = lds;
+  bf16* otile = reinterpret_cast<bf16*>(lds + ((patch_rows * PW * C::PB + 15) & ~15));
+
+  const int H = p.H, W = p.W, Ho = p.Ho, Wo = p.Wo;
+  const int nbands = (Ho + kR - 1) / kR;
+  const int total = p.N * nbands;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int fr = lane & 31, fh = lane >> 5;
+  const int cb = wv % NCB, ph = wv / NCB;
+
+  // ---- this wave's weight block -> VGPRs, once (rows past Cout are zero)
+  const bf16* wp = reinterpret_cast<const bf16*>(p.w);
+  const int wrow = cb * 32 + fr;
+  bf16x8 wreg[C::KS];
+#pragma unroll
+  for (int kk = 0; kk < C::KS; ++kk) {
+    bf16x8 v = {};
+    if (wrow < COUT) v = *reinterpret_cast<const bf16x8*>(wp + wrow * p.Kpad + kk * 16 + fh * 8);
+    wreg[kk] = v;
+  }
+  float4 bv[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int ch = cb * 32 + g * 8 + fh * 4;
+    bv[g] = (p.bias && ch < COUT) ? *reinterpret_cast<const float4*>(p.bias + ch)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+
+  // ---- band patch prefetch: 16-B chunk q -> patch pixel q / CPP (row-major, pitch PW)
+  const int nchunks = patch_rows * PW * C::CPP;
+  uint4 pre[C::PRE];
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.x), (short)0, p.N * H * W * p.ldx * 2, 0x00020000);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  auto fetch = [&](int item) __attribute__((always_inline)) {
+    const int n = item / nbands, band = item - n * nbands;
+    const int iy0 = band * kR * S - 1;
+    const bool live = item < total;
+#pragma unroll
+    for (int i = 0; i < C::PRE; ++i) {
+      const int q = tid + kNT * i;
+      const int pp = q / C::CPP, c = q - pp * C::CPP;
+      const int pr = pp / PW, pc = pp - pr * PW;
+      const int iy = iy0 + pr, ix = pc - 1;
+      const bool ok = live && q < nchunks && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      const int off = ok ? (((n * H + iy) * W + ix) * p.ldx + p.x_coff + c * 8) * 2 : kOOB;
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+      pre[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto commit = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < C::PRE; ++i) {
+      const int q = tid + kNT * i;
+      const int pp = q / C::CPP, c = q - pp * C::CPP;
+      if (q < nchunks) *reinterpret_cast<uint4*>(patch + pp * C::PB + c * 16) = pre[i];
+    }
+  };
+
+  bf16* __restrict__ Y = reinterpret_cast<bf16*>(p.y);
+  const bf16* __restrict__ R = reinterpret_cast<const bf16*>(p.res);
+  const int npix = kR * Wo;
+  const int nblk = (npix + 31) / 32;
+  const int rowb = PW * C::PB;
+  int item = xcd_remap(blockIdx.x, gridDim.x);  // neighbour bands share an XCD
+  fetch(item);
+  commit();
+  __syncthreads();
+  for (; item < total; item += gridDim.x) {
+    const int n = item / nbands, band = item - n * nbands;
+    const int oy0 = band * kR;
+    fetch(item + gridDim.x);  // next band: in flight during this band's MFMAs
+
+    for (int b = ph; b < nblk; b += NPH) {
+      const int j = min(b * 32 + fr, npix - 1);  // clamp: pixels past npix are discarded
+      const int yl = j / Wo, xc = j - yl * Wo;
+      const unsigned char* pa0 = patch + (yl * S * PW + xc * S) * C::PB + fh * 16;
+      const unsigned char* pa[3] = {pa0, pa0 + rowb, pa0 + 2 * rowb};
+      floatx16 acc;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        acc[4 * g + 0] = bv[g].x;
+        acc[4 * g + 1] = bv[g].y;
+        acc[4 * g + 2] = bv[g].z;
+        acc[4 * g + 3] = bv[g].w;
+      }
+      bf16x8 af[2];
+      auto load = [&](int buf, int kk) __attribute__((always_inline)) {
+        const int tap = kk / C::KPT, s4 = kk - (kk / C::KPT) * C::KPT;
+        const int r = tap / 3, s = tap - (tap / 3) * 3;
+        af[buf] = *reinterpret_cast<const bf16x8*>(pa[r] + s * C::PB + s4 * 32);
+      };
+      load(0, 0);
+#pragma unroll
+      for (int kk = 0; kk < C::KS; ++kk) {
+        if (kk + 1 < C::KS) load((kk + 1) & 1, kk + 1);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wreg[kk], af[kk & 1], acc, 0, 0, 0);
+      }
+      // reads(0) | reads(k+1) MFMA(k) ...: one fragment read in flight per MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+      for (int kk = 0; kk < C::KS; ++kk) {
+        if (kk + 1 < C::KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      const int jr = b * 32 + fr;
+      if (jr < npix) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          if (cb * 32 + g * 8 >= COUT) continue;  // compile-time for COUT % 32 == 0
+          bf16x4 o;
+          o[0] = f2bf(act_c<ACT>(acc[4 * g + 0]));
+          o[1] = f2bf(act_c<ACT>(acc[4 * g + 1]));
+          o[2] = f2bf(act_c<ACT>(acc[4 * g + 2]));
+          o[3] = f2bf(act_c<ACT>(acc[4 * g + 3]));
+          *reinterpret_cast<bf16x4*>(otile + jr * OS + cb * 32 + g * 8 + fh * 4) = o;
+        }
+      }
+    }
+    __syncthreads();  // output tile complete; patch no longer read
+
+    // ---- store the band (+ residual after the activation): 16-B channel chunks
+    constexpr int OCH = COUT / 8;
+    for (int q = tid; q < npix * OCH; q += kNT) {
+      const int px = q / OCH, c = q - (q / OCH) * OCH;
+      const int yl = px / Wo, xc = px - yl * Wo;
+      const int oy = oy0 + yl;
+      if (oy >= Ho) continue;
+      const long long m = (long long)(n * Ho + oy) * Wo + xc;
+      uint4 v = *reinterpret_cast<const uint4*>(otile + px * OS + c * 8);
+      if constexpr (RES) {
+        const bf16x8 r8 = *reinterpret_cast<const bf16x8*>(R + m * p.ldr + p.r_coff + c * 8);
+        bf16x8 o8 = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o8[e] = f2bf((float)o8[e] + (float)r8[e]);
+        v = __builtin_bit_cast(uint4, o8);
+      }
+      *reinterpret_cast<uint4*>(Y + m * p.ldy + p.y_coff + c * 8) = v;
+    }
+    commit();         // next band's patch (landed during the MFMAs)
+    __syncthreads();  // patch ready, output tile free
+  }
+}
+
+typedef void (*DirectFn)(const KvConvParams, int, int, int);
+
+struct DirectEntry {
+  int cin, cout, stride, act;
+  bool res;
+  DirectFn fn;
+};
+
+#define KV_DIRECT(CI, CO, S, A, R) {CI, CO, S, A, R, conv3x3_direct_kernel<CI, CO, S, A, R>}
+// the 3x3 shapes of ResNet-50 stage 1 and YOLOv8n's narrow layers (backbone, C2f
+// bottlenecks, PAN downsamplers, Detect 64-channel branches)
+static const DirectEntry kDirect[] = {
+    KV_DIRECT(64, 64, 1, kActRelu, false),   // ResNet-50 layer1 conv2 x3
+    KV_DIRECT(64, 64, 1, kActNone, false),
+    KV_DIRECT(16, 32, 2, kActSilu, false),   // YOLO b1
+    KV_DIRECT(16, 16, 1, kActSilu, false),   // b2 bottleneck cv1
+    KV_DIRECT(16, 16, 1, kActSilu, true),    // b2 bottleneck cv2 (+x)
+    KV_DIRECT(32, 64, 2, kActSilu, false),   // b3
+    KV_DIRECT(32, 32, 1, kActSilu, false),   // b4 / h15 bottlenecks
+    KV_DIRECT(32, 32, 1, kActSilu, true),
+    KV_DIRECT(64, 128, 2, kActSilu, false),  // b5
+    KV_DIRECT(64, 64, 1, kActSilu, false),   // b6 / h12 / h18 bottlenecks, Detect a1
+    KV_DIRECT(64, 64, 1, kActSilu, true),
+    KV_DIRECT(64, 64, 2, kActSilu, false),   // h16
+};
+#undef KV_DIRECT
+
+int direct_pb(int cin) { return cin * 2 + 16; }
+int direct_max_patch(int cin) { return (cin >= 64 ? 7 : 10) * kNT * 16; }
+
+}  // namespace
+
+int direct_num_tiles() { return 1; }
+
+// Returns the instantiation index for p (or < 0), and the band geometry it would use.
+static int direct_plan(const KvConvParams* p, int* kR, int* PW, int* rows, int* lds) {
+  if (p->mode != 0 || p->KH != 3 || p->KW != 3 || p->pad != 1) return -8;
+  if (p->stride != 1 && p->stride != 2) return -8;
+  const int act = p->act & 3;
+  const bool res = p->res != nullptr;
+  if (res && !(p->act & 4) && act != kActNone) return -8;  // only x + act(conv)
+  int idx = -1;
+  for (int i = 0; i < (int)(sizeof(kDirect) / sizeof(kDirect[0])); ++i) {
+    const DirectEntry& e = kDirect[i];
+    if (e.cin == p->Cin && e.cout == p->Cout && e.stride == p->stride && e.act == act &&
+        e.res == res) {
+      idx = i;
+      break;
+    }
+  }
+  if (idx < 0) return -8;
+  if (p->Kpad != (9 * p->Cin + 63) / 64 * 64 || p->ldx % 8 || p->x_coff % 8) return -8;
+  if (p->Ho != (p->H - 1) / p->stride + 1 || p->Wo != (p->W - 1) / p->stride + 1) return -8;
+  if ((long long)p->N * p->H * p->W * p->ldx * 2 >= kOOB) return -9;
+  const int S = p->stride;
+  *PW = (p->Wo - 1) * S + 3;
+  const int pb = direct_pb(p->Cin);
+  const int os = p->Cout + 8;
+  // rows per band: as many as fit (<= 8) in the prefetch budget and LDS
+  int r = 8;
+  for (; r >= 1; --r) {
+    const int prows = (r - 1) * S + 3;
+    const int patch = prows * *PW * pb;
+    const int ob = r * p->Wo * os * 2;
+    if (patch <= direct_max_patch(p->Cin) && ((patch + 15) & ~15) + ob <= kLds) break;
+  }
+  if (r < 1) return -11;
+  if (r > p->Ho) r = p->Ho;
+  *kR = r;
+  *rows = (r - 1) * S + 3;
+  *lds = ((*rows * *PW * pb + 15) & ~15) + r * p->Wo * os * 2;
+  return idx;
+}
+
+int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
+  if (tile < 0 || tile >= direct_num_tiles()) return -6;
+  int kR, PW, rows, lds;
+  const int idx = direct_plan(p, &kR, &PW, &rows, &lds);
+  if (idx < 0) return idx;
+  const long long items = (long long)p->N * ((p->Ho + kR - 1) / kR);
+  if (items <= 0) return 0;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const unsigned g = (unsigned)(items < ncu ? items : ncu);  // persistent: one per CU
+  const DirectFn fn = kDirect[idx].fn;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+    return -7;
+  hipLaunchKernelGGL(fn, dim3(g), dim3(kNT), (unsigned)lds, stream, *p, kR, PW, rows);
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
+}  // namespace kvedge

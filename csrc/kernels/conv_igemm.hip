@@ -306,9 +306,14 @@ int glds_tile_bn(int tile);
 // v3 persistent streaming family (conv_stream.hip, 1x1 GEMM / dual only): indices after v2
 int stream_num_tiles();
 int stream_launch(const KvConvParams* p, int tile, hipStream_t stream);
+// v4 family (conv_direct.hip): persistent direct 3x3 conv for narrow channel counts
+int direct_num_tiles();
+int direct_launch(const KvConvParams* p, int tile, hipStream_t stream);
 }  // namespace kvedge
 
-extern "C" int kv_conv_num_tiles(void) { return kNumTiles + glds_num_tiles() + stream_num_tiles(); }
+extern "C" int kv_conv_num_tiles(void) {
+  return kNumTiles + glds_num_tiles() + stream_num_tiles() + direct_num_tiles();
+}
 
 extern "C" int kv_conv_pick_tile(const KvConvParams* p) {
   // Heuristic: enough workgroups to cover 256 CUs x 2, largest tile otherwise.
@@ -325,7 +330,43 @@ extern "C" int kv_conv_pick_tile(const KvConvParams* p) {
   return 2;
 }
 
+#ifdef KVEDGE_CHECKS
+// Bounds-check build (`python -m kvedge_amd._build --checks`): before a
+// launch, every operand extent the kernel may touch must lie inside the device
+// allocation that contains its base pointer.  GPU ASan / xnack+ are unavailable on the
+// MI355X pool, so this host-side check is what guards the raw C ABI (native tools and
+// tests that bypass the torch bindings, which always check tensor extents).
+static bool kv_in_alloc(const void* ptr, long long bytes) {
+  if (!ptr || bytes <= 0) return true;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  const char* b = static_cast<const char*>(base);
+  const char* q = static_cast<const char*>(ptr);
+  return q >= b && q + bytes <= b + size;
+}
+
+static int kv_conv_check_extents(const KvConvParams* p) {
+  const long long M = (long long)p->N * p->Ho * p->Wo;
+  if (!kv_in_alloc(p->x, (long long)p->N * p->H * p->W * p->ldx * 2)) return -20;
+  if (!kv_in_alloc(p->w, (long long)p->Cout * p->Kpad * 2)) return -21;
+  if (!kv_in_alloc(p->bias, (long long)p->Cout * 4)) return -22;
+  if (!kv_in_alloc(p->y, M * p->ldy * 2)) return -23;
+  if (p->res && !kv_in_alloc(p->res, M * p->ldr * 2)) return -24;
+  if (p->mode == 4 && !kv_in_alloc(p->x2, (long long)p->N * p->H2 * p->W2 * p->ldx2 * 2)) return -25;
+  if (p->x_coff + p->Cin > p->ldx || p->y_coff + p->Cout > p->ldy) return -26;
+  if (p->res && p->r_coff + p->Cout > p->ldr) return -27;
+  return 0;
+}
+#endif
+
 extern "C" int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream) {
+#ifdef KVEDGE_CHECKS
+  if (const int rc = kv_conv_check_extents(p)) return rc;
+#endif
   if (p->Kpad % BK != 0 || p->Cout % 8 != 0) return -1;
   if (p->mode == 2 && (p->Cin != 4 || p->ldx != 4)) return -2;
   if (p->mode != 2 && (p->Cin % 8 != 0 || p->ldx % 8 != 0 || p->x_coff % 8 != 0)) return -3;
@@ -340,7 +381,9 @@ extern "C" int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream) {
   }
   if (tile < 0) tile = kv_conv_pick_tile(p);
   const int v3 = kNumTiles + glds_num_tiles();
-  if (tile >= v3 + stream_num_tiles()) return -6;
+  const int v4 = v3 + stream_num_tiles();
+  if (tile >= v4 + direct_num_tiles()) return -6;
+  if (tile >= v4) return direct_launch(p, tile - v4, stream);
   if (tile >= v3) return stream_launch(p, tile - v3, stream);
   if (tile >= kNumTiles) return glds_launch(p, tile - kNumTiles, stream);
   const TileEntry& e = kTiles[tile];

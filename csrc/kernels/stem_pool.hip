@@ -11,21 +11,31 @@
 //    per lane), the next band's input patch is prefetched into registers while this
 //    band computes (a one-band-per-workgroup first version was latency-bound: 17 us
 //    per band, slower than the unfused pair);
-//  * the s2d input rows the band needs (8 rows x (W+3) pixels x 16 ch = 29 KB) are
-//    loaded ONCE into LDS (zero padding included); every tap's A fragment is then a
-//    shifted ds_read_b128 of that patch -- no re-fetch from L2 per tap;
+//  * the s2d input rows the band needs (8 rows of 16-ch pixels) are loaded ONCE into
+//    LDS (zero padding included); every tap's A fragment is then a shifted
+//    ds_read_b128 of that patch -- no re-fetch from L2 per tap;
 //  * the 2*RB+1 = 5 stem rows the pool windows touch are computed with
-//    v_mfma_f32_32x32x16_bf16 (D = W * A^T as in conv_glds.hip), the whole 64 x 256
-//    weight matrix held in VGPRs (32 fragments per lane, loaded once);
-//  * bias + ReLU, bf16, into an LDS stem tile; then the 3x3/2 pool reads the tile and
-//    writes the pooled [RB, W/2, 64] band with 16-B stores.
+//    v_mfma_f32_32x32x16_bf16 (D = W * A^T as in conv_glds.hip), the accumulators
+//    seeded with the folded-BN bias;
+//  * ReLU, bf16, into an LDS stem tile; then the 3x3/2 pool reads the tile and writes
+//    the pooled [RB, W/2, 64] band with 16-B stores.
 // 5 stem rows per 4 pooled-input rows is a 25 % recompute of the conv, paid to never
 // write or re-read the 112x112x64 intermediate.
 //
-// Patch layout: pixel p (row-major over the (8, W+3) patch) holds 16 channels = two
-// 16-B halves, stored half-swapped when bit 3 of p is set: 16 consecutive pixels read
-// by one ds_read_b128 lane group then cover all 64 banks (stride 32 B would otherwise
-// collide lanes l and l+8).
+// VALU diet (PMC of the previous version, profiles/r1_v7_stem_pmc.md: 17 VALU per MFMA,
+// i.e. VALU-issue-bound at ~2x the MFMA time):
+//  * patch pixels at a fixed 48-B pitch (16 ch + 16 B pad) and a fixed row pitch of
+//    kPW = 128 pixels: 16 consecutive pixels' 16-B reads hit banks 12p mod 64, all 64
+//    exactly once (conflict-free with a LINEAR layout), so a tap's fragment address is
+//    the block base plus a compile-time constant = the ds_read immediate offset;
+//  * the bias seeds the accumulators (no per-element add) and out-of-image stem rows
+//    are skipped by the pool instead of being zeroed per element;
+//  * the pool runs packed 16-bit unsigned max (v_pk_max_u16) on the bf16 bit patterns:
+//    post-ReLU values are >= 0 and non-negative IEEE values order like their bits;
+//  * 512 threads (2 waves per SIMD): one wave's LDS reads / epilogue / pool overlap the
+//    other's MFMAs (256 threads: 691 us -> 558 us at batch 640 on its own).
+#include <stdlib.h>
+
 #include "common.h"
 #include "kvedge_kernels.h"
 
@@ -42,23 +52,33 @@ constexpr int kRB = 2;         // pooled rows per workgroup
 constexpr int kSR = 2 * kRB + 1;  // stem rows per band
 constexpr int kPR = kSR + 3;      // patch (input) rows per band
 constexpr int kTS = kCo + 8;      // stem-tile pixel stride (elements)
+constexpr int kPW = 128;          // patch row pitch in pixels (W + 3 <= kPW)
+constexpr int kPB = 48;           // patch bytes per pixel: 16 ch (32 B) + 16 B pad
 
-__device__ __forceinline__ int patch_off(int p, int fh) {  // bytes
-  return p * 32 + ((fh ^ ((p >> 3) & 1)) << 4);
+__device__ __forceinline__ int patch_off(int p, int h) { return p * kPB + h * 16; }
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ unsigned pk_max_u16(unsigned a, unsigned b) {
+  const u16x2 r = __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
+                                            __builtin_bit_cast(u16x2, b));
+  return __builtin_bit_cast(unsigned, r);
 }
 
-__global__ __launch_bounds__(256, 1) void stem_pool_kernel(
+template <int NT>  // threads per workgroup: 256 (1 wave/SIMD) or 512 (2 waves/SIMD)
+__global__ __launch_bounds__(NT, 1) void stem_pool_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ w, const float* __restrict__ bias,
     bf16* __restrict__ y, int N, int H, int W, int Hp, int Wp, int ldy, int y_coff) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int PW = W + 3;
-  unsigned char* patch = lds;                                       // kPR * PW * 32 B
-  bf16* tile = reinterpret_cast<bf16*>(lds + ((kPR * PW * 32 + 15) & ~15));  // kSR*W px
+  constexpr int kPatchBytes = kPR * kPW * kPB;
+  unsigned char* patch = lds;                                // kPR x kPW pixels
+  bf16* tile = reinterpret_cast<bf16*>(lds + kPatchBytes);    // kSR*W px, stride kTS
 
   const int nbands = (Hp + kRB - 1) / kRB;
   const int total = N * nbands;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int fr = lane & 31, fh = lane >> 5;
+  constexpr int kNW = NT / 64;
 
   // ---- weights -> VGPRs, once: fragment (cb, t) rows n = cb*32 + fr, k = t*16 + fh*8 ..
   bf16x8 wreg[2][kTaps];
@@ -67,7 +87,7 @@ __global__ __launch_bounds__(256, 1) void stem_pool_kernel(
 #pragma unroll
     for (int t = 0; t < kTaps; ++t)
       wreg[cb][t] = *reinterpret_cast<const bf16x8*>(w + (cb * 32 + fr) * kK + t * 16 + fh * 8);
-  // bias for this lane's accumulator channels: n = cb*32 + g*8 + fh*4 + j
+  // bias for this lane's accumulator channels n = cb*32 + g*8 + fh*4 + j
   float4 bv[2][4];
 #pragma unroll
   for (int cb = 0; cb < 2; ++cb)
@@ -75,27 +95,28 @@ __global__ __launch_bounds__(256, 1) void stem_pool_kernel(
     for (int g = 0; g < 4; ++g)
       bv[cb][g] = *reinterpret_cast<const float4*>(bias + cb * 32 + g * 8 + fh * 4);
 
-  // ---- patch prefetch: this thread's 16-B chunks q = tid + 256 i of a band's patch
-  constexpr int kPre = 8;  // chunks per thread: covers kPR * PW * 2 <= 2048 (W <= 125)
+  // ---- patch prefetch: 16-B chunks q = tid + NT*i of a band's (kPR x kPW) patch.  Every
+  // chunk is loaded: columns past the image and out-of-image rows read zeros through the
+  // buffer range check (no branch; no zero-init of `pre`: a v_mov into a register whose
+  // last writer was a VMEM load made hipcc wait vmcnt(0) at the top of every band)
+  constexpr int kChunks = kPR * kPW * 2;
+  constexpr int kPre = kChunks / NT;
+  static_assert(kChunks % NT == 0, "patch chunks per thread");
   uint4 pre[kPre];
-  // buffer loads with the range check doing the zero padding: always issued, no branch
-  // and no zero-init of `pre` (a v_mov into a register whose last writer was a VMEM
-  // load made hipcc wait vmcnt(0) -- i.e. for the previous band's pool stores -- at the
-  // top of every band)
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16*>(x), (short)0, N * H * W * kCin * 2, 0x00020000);
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   auto fetch = [&](int item) __attribute__((always_inline)) {
     const int n = item / nbands, band = item - n * nbands;
     const int iy0 = 2 * band * kRB - 3;
+    const bool live = item < total;
 #pragma unroll
     for (int i = 0; i < kPre; ++i) {
-      const int q = tid + 256 * i;
+      const int q = tid + NT * i;
       const int p = q >> 1, h = q & 1;
-      const int pr = p / PW, pc = p - pr * PW;
+      const int pr = p / kPW, pc = p % kPW;
       const int iy = iy0 + pr, ix = pc - 2;
-      const bool ok = item < total && q < kPR * PW * 2 && (unsigned)iy < (unsigned)H &&
-                      (unsigned)ix < (unsigned)W;
+      const bool ok = live && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
       const int off = ok ? (((n * H + iy) * W + ix) * kCin + h * 8) * 2 : 0x7ffffff0;
       const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
       pre[i] = make_uint4(v[0], v[1], v[2], v[3]);
@@ -104,8 +125,8 @@ __global__ __launch_bounds__(256, 1) void stem_pool_kernel(
   auto commit = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < kPre; ++i) {
-      const int q = tid + 256 * i;
-      if (q < kPR * PW * 2) *reinterpret_cast<uint4*>(patch + patch_off(q >> 1, q & 1)) = pre[i];
+      const int q = tid + NT * i;
+      *reinterpret_cast<uint4*>(patch + patch_off(q >> 1, q & 1)) = pre[i];
     }
   };
 
@@ -119,22 +140,26 @@ __global__ __launch_bounds__(256, 1) void stem_pool_kernel(
     const int y0 = 2 * P0 - 1;  // first stem row (may be -1)
     fetch(item + gridDim.x);    // next band's patch: in flight during this band's MFMAs
 
-    // ---- stem rows of the band: 32-pixel row blocks round-robin over the 4 waves
+    // ---- stem rows of the band: 32-pixel row blocks round-robin over the kNW waves
     const int npix = kSR * W;
     const int nrb = (npix + 31) / 32;
-    for (int rb = wv; rb < nrb; rb += 4) {
+    for (int rb = wv; rb < nrb; rb += kNW) {
       const int j = min(rb * 32 + fr, npix - 1);  // clamp: rows past npix are discarded
       const int yl = j / W, xc = j - yl * W;
-      const int pbase = yl * PW + xc;
+      const unsigned char* pa = patch + patch_off(yl * kPW + xc, fh);
       floatx16 acc[2];
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[cb][e] = 0.f;
+        for (int g = 0; g < 4; ++g) {
+          acc[cb][4 * g + 0] = bv[cb][g].x;
+          acc[cb][4 * g + 1] = bv[cb][g].y;
+          acc[cb][4 * g + 2] = bv[cb][g].z;
+          acc[cb][4 * g + 3] = bv[cb][g].w;
+        }
       bf16x8 af[2];
       auto load = [&](int buf, int t) __attribute__((always_inline)) {
-        const int p = pbase + (t >> 2) * PW + (t & 3);
-        af[buf] = *reinterpret_cast<const bf16x8*>(patch + patch_off(p, fh));
+        af[buf] = *reinterpret_cast<const bf16x8*>(pa + ((t >> 2) * kPW + (t & 3)) * kPB);
       };
       load(0, 0);
 #pragma unroll
@@ -149,20 +174,19 @@ __global__ __launch_bounds__(256, 1) void stem_pool_kernel(
         if (t + 1 < kTaps) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
       }
-      // bias + ReLU -> bf16 stem tile; stem rows outside the image become 0, which the
-      // pool may read freely (every window also holds a valid post-ReLU value >= 0)
+      // ReLU -> bf16 stem tile.  Stem rows outside the image (above the first band, below
+      // an odd-H image) are written but never pooled: the pool skips them as padding.
       const int jr = rb * 32 + fr;
-      const bool ok = jr < npix && (unsigned)(y0 + yl) < (unsigned)H;
       if (jr < npix) {
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             bf16x4 o;
-            o[0] = f2bf(ok ? fmaxf(acc[cb][4 * g + 0] + bv[cb][g].x, 0.f) : 0.f);
-            o[1] = f2bf(ok ? fmaxf(acc[cb][4 * g + 1] + bv[cb][g].y, 0.f) : 0.f);
-            o[2] = f2bf(ok ? fmaxf(acc[cb][4 * g + 2] + bv[cb][g].z, 0.f) : 0.f);
-            o[3] = f2bf(ok ? fmaxf(acc[cb][4 * g + 3] + bv[cb][g].w, 0.f) : 0.f);
+            o[0] = f2bf(fmaxf(acc[cb][4 * g + 0], 0.f));
+            o[1] = f2bf(fmaxf(acc[cb][4 * g + 1], 0.f));
+            o[2] = f2bf(fmaxf(acc[cb][4 * g + 2], 0.f));
+            o[3] = f2bf(fmaxf(acc[cb][4 * g + 3], 0.f));
             *reinterpret_cast<bf16x4*>(tile + jr * kTS + cb * 32 + g * 8 + fh * 4) = o;
           }
       }
@@ -170,31 +194,31 @@ __global__ __launch_bounds__(256, 1) void stem_pool_kernel(
     __syncthreads();  // stem tile complete; patch no longer read
 
     // ---- 3x3/2 max pool (pad 1) of the band -> global, 16 B per thread-iteration
-    const int per_row = Wp * (kCo / 8);
-    for (int q = tid; q < kRB * per_row; q += 256) {
-      const int pr = q / per_row, rem = q - pr * per_row;
-      const int px = rem >> 3, c8 = rem & 7;
+#pragma unroll
+    for (int pr = 0; pr < kRB; ++pr) {
       const int P = P0 + pr;
-      if (P >= Hp) continue;
-      float m[8];
+      if (P >= Hp) break;
+      bf16* yrow = y + (long long)(n * Hp + P) * Wp * ldy + y_coff;
+      for (int q = tid; q < Wp * (kCo / 8); q += NT) {
+        const int px = q >> 3, c8 = q & 7;
+        uint4 m = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) m[e] = 0.f;  // post-ReLU values are >= 0
+        for (int dy = 0; dy < 3; ++dy) {
+          const int yl = 2 * pr + dy;  // stem row y0 + yl
+          if ((unsigned)(y0 + yl) >= (unsigned)H) continue;  // padding row
 #pragma unroll
-      for (int dy = 0; dy < 3; ++dy) {
-        const int yl = 2 * pr + dy;  // stem row 2P-1+dy - y0
-#pragma unroll
-        for (int dx = -1; dx <= 1; ++dx) {
-          const int xs = 2 * px + dx;
-          if ((unsigned)xs >= (unsigned)W) continue;
-          const bf16x8 v = *reinterpret_cast<const bf16x8*>(tile + (yl * W + xs) * kTS + c8 * 8);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], (float)v[e]);
+          for (int dx = -1; dx <= 1; ++dx) {
+            const int xs = 2 * px + dx;
+            if ((unsigned)xs >= (unsigned)W) continue;
+            const uint4 v = *reinterpret_cast<const uint4*>(tile + (yl * W + xs) * kTS + c8 * 8);
+            m.x = pk_max_u16(m.x, v.x);
+            m.y = pk_max_u16(m.y, v.y);
+            m.z = pk_max_u16(m.z, v.z);
+            m.w = pk_max_u16(m.w, v.w);
+          }
         }
+        *reinterpret_cast<uint4*>(yrow + px * ldy + c8 * 8) = m;
       }
-      bf16x8 o;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(m[e]);
-      *reinterpret_cast<bf16x8*>(y + ((long long)(n * Hp + P) * Wp + px) * ldy + y_coff + c8 * 8) = o;
     }
     commit();         // next band's patch (its loads have landed by now)
     __syncthreads();  // tile free, patch ready
@@ -206,16 +230,14 @@ __global__ __launch_bounds__(256, 1) void stem_pool_kernel(
 
 using namespace kvedge;
 
-extern "C" int kv_stem_pool_lds_bytes(int W) {
-  return ((kPR * (W + 3) * 32 + 15) & ~15) + kSR * W * kTS * 2;
-}
+extern "C" int kv_stem_pool_lds_bytes(int W) { return kPR * kPW * kPB + kSR * W * kTS * 2; }
 
 extern "C" int kv_stem_pool(const void* x, const void* w, const float* bias, void* y, int N, int H,
                             int W, int ldy, int y_coff, hipStream_t s) {
   if (N <= 0) return 0;
   if (H <= 0 || W <= 0 || ldy % 8 || y_coff % 8 || ldy < y_coff + kCo || !bias) return -1;
   const int lds = kv_stem_pool_lds_bytes(W);
-  if (lds > 160 * 1024 || kPR * (W + 3) * 2 > 8 * 256) return -2;  // patch prefetch: W <= 125
+  if (lds > 160 * 1024 || W + 3 > kPW) return -2;                // patch row pitch: W <= 125
   if ((long long)N * H * W * 16 * 2 >= 0x7ffffff0LL) return -4;   // buffer range (2 GiB)
   const int Hp = (H - 1) / 2 + 1, Wp = (W - 1) / 2 + 1;  // 3x3 / 2, pad 1
   const long long items = (long long)N * ((Hp + kRB - 1) / kRB);
@@ -223,10 +245,20 @@ extern "C" int kv_stem_pool(const void* x, const void* w, const float* bias, voi
   if (hipGetDevice(&dev) == hipSuccess)
     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const long long g = items < ncu ? items : ncu;  // persistent: one workgroup per CU
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(stem_pool_kernel),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+  // KVEDGE_STEM_THREADS=256|512 (probe knob; default 512: two waves per SIMD)
+  static const int nt = [] {
+    const char* e = getenv("KVEDGE_STEM_THREADS");
+    return (e && atoi(e) == 256) ? 256 : 512;
+  }();
+  const void* fn = nt == 256 ? reinterpret_cast<const void*>(stem_pool_kernel<256>)
+                             : reinterpret_cast<const void*>(stem_pool_kernel<512>);
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
     return -3;
-  hipLaunchKernelGGL(stem_pool_kernel, dim3((unsigned)g), dim3(256), (unsigned)lds, s,
-                     (const bf16*)x, (const bf16*)w, bias, (bf16*)y, N, H, W, Hp, Wp, ldy, y_coff);
+  if (nt == 256)
+    hipLaunchKernelGGL(stem_pool_kernel<256>, dim3((unsigned)g), dim3(256), (unsigned)lds, s,
+                       (const bf16*)x, (const bf16*)w, bias, (bf16*)y, N, H, W, Hp, Wp, ldy, y_coff);
+  else
+    hipLaunchKernelGGL(stem_pool_kernel<512>, dim3((unsigned)g), dim3(512), (unsigned)lds, s,
+                       (const bf16*)x, (const bf16*)w, bias, (bf16*)y, N, H, W, Hp, Wp, ldy, y_coff);
   return hipGetLastError() == hipSuccess ? 0 : -100;
 }

@@ -68,6 +68,12 @@ def _run(cmd):
 
 
 COMMON = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+if os.environ.get("KVEDGE_CHECKS", "0") not in ("", "0"):
+    # bounds-check build: launchers verify operand extents against their allocations
+    # (a separate object dir so the fast build's objects are not clobbered)
+    COMMON.append("-DKVEDGE_CHECKS=1")
+    OBJ = os.path.join(ROOT, "build", "obj_checks")
+    SO_PATH = os.path.join(PKG, "_C_checks.so")
 
 
 def build(force: bool = False, jobs: int = 0, verbose: bool = False, asan: bool = False) -> str:
@@ -155,6 +161,9 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=0)
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--checks", action="store_true",
+                    help="bounds-check build (-DKVEDGE_CHECKS): set KVEDGE_CHECKS=1 instead "
+                         "(must be set before import); this flag only reports it")
     ap.add_argument("--asan", action="store_true",
                     help="also build the host-ASan/UBSan runtime self-test")
     a = ap.parse_args(argv)

@@ -28,7 +28,11 @@ import torch
 
 from . import reference as _ref
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_C.so")
+# KVEDGE_CHECKS=1 selects the bounds-check build (python -m kvedge_amd._build with the
+# same variable set): launchers verify operand extents against their HIP allocations.
+_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                         "_C_checks.so" if os.environ.get("KVEDGE_CHECKS", "0") not in ("", "0")
+                         else "_C.so")
 _loaded = False
 _load_error: Optional[str] = None
 

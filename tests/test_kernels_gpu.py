@@ -82,8 +82,9 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale + 0.02
 
 
-N_TILES = 34  # v1 register-staged (0-5) + v2 LDS-DMA (6-21) + v3 streaming (22-33)
+N_TILES = 35  # v1 register-staged (0-5) + v2 LDS-DMA (6-21) + v3 streaming (22-33) + v4 direct (34)
 STREAM0 = 22  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
+DIRECT0 = 34  # v4 direct 3x3 (conv_direct.hip): its instantiation table only
 # v3 (bm, bn, ring depth, weight slice resident in LDS) -- conv_stream.hip kStreamTiles
 STREAM_TILES = [(64, 64, 4, True), (64, 128, 4, True), (128, 64, 4, True), (64, 64, 6, True),
                 (64, 128, 3, True), (64, 64, 4, False), (128, 64, 4, False), (128, 128, 3, False),
@@ -114,6 +115,11 @@ def test_tile_count():
 ])
 def test_conv_every_tile(tile, case):
     N, H, W, cin, cout, k, s, p, act, res, lx, xc = case
+    if tile >= DIRECT0:  # none of these shapes is in the direct-conv instantiation table
+        with pytest.raises(RuntimeError):
+            _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
+                       tile=tile)
+        return
     if tile >= STREAM0 and (k != 1 or s != 1 or not _stream_fits(tile, (cin * k * k + 63) // 64 * 64, res)):
         with pytest.raises(RuntimeError):
             _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
@@ -124,7 +130,7 @@ def test_conv_every_tile(tile, case):
     assert err <= 0.02 * scale + 0.02, (tile, case, err, scale)
 
 
-@pytest.mark.parametrize("tile", [-1] + list(range(STREAM0, N_TILES)))
+@pytest.mark.parametrize("tile", [-1] + list(range(STREAM0, DIRECT0)))
 @pytest.mark.parametrize("case", [
     # (N, H, W, cin, cout, act, res, ldx_extra, x_coff, ldy_extra, y_coff)
     (4, 56, 56, 256, 512, ops.ACT_RELU, True, 0, 0, 0, 0),     # several M tiles per workgroup
@@ -242,7 +248,7 @@ def test_nms_dense_overlaps():
     assert (o.cpu() - o_ref).abs().max() < 1e-4
 
 
-@pytest.mark.parametrize("tile", [-1] + list(range(6, N_TILES)))
+@pytest.mark.parametrize("tile", [-1] + list(range(6, DIRECT0)))
 @pytest.mark.parametrize("geom", [(2, 14, 14, 64, 128, 256, 2), (2, 7, 7, 128, 256, 512, 1),
                                   (1, 5, 5, 64, 64, 128, 2)])
 def test_conv_dual_fused_downsample(tile, geom):
@@ -267,16 +273,20 @@ def test_conv_dual_rejects_v1_tiles():
         ops.conv_dual(x1, x2, w, None, ops.ACT_NONE, 1, tile=0)
 
 
-@pytest.mark.parametrize("tile", [-1, 1, 6, 7, 12, 13, STREAM0, STREAM0 + 1, STREAM0 + 5])
+@pytest.mark.parametrize("tile", [-1, 1, 6, 7, 12, 13, STREAM0, STREAM0 + 1, STREAM0 + 5, DIRECT0])
 @pytest.mark.parametrize("k", [1, 3])
 def test_conv_poisoned_canary(tile, k):
     """SURVEY §5.2 poisoned-buffer check: the output buffer is NaN-filled, with a NaN
     canary tail after the tensor and NaN in the channels outside the written slice.  Every
     written element must be finite, and every byte outside the slice must stay NaN
     (a kernel that writes past M/N tails or outside [y_coff, y_coff+cout) fails here)."""
-    if tile >= STREAM0 and k != 1:
+    if STREAM0 <= tile < DIRECT0 and k != 1:
         pytest.skip("v3 tiles take 1x1 GEMMs only")
+    if tile == DIRECT0 and k != 3:
+        pytest.skip("v4 takes 3x3 only")
     N, H, W, cin, cout, ldy, y_coff = 3, 13, 11, 64, 72, 104, 16
+    if tile == DIRECT0:
+        cout = 64  # an instantiated direct shape (64 -> 64 ReLU)
     spec = ConvSpec.auto(cin, cout, k, 1, k // 2, ops.ACT_RELU)
     g = torch.Generator().manual_seed(3)
     x = torch.randn(N, H, W, cin, generator=g).to(torch.bfloat16).cuda()
@@ -297,6 +307,37 @@ def test_conv_poisoned_canary(tile, k):
     assert torch.isnan(flat[n_out:].cpu().float()).all()
     ref = ops.conv2d(x.cpu(), spec, w.cpu(), b.cpu())
     assert (inside - ref.float()).abs().max().item() <= 0.02 * ref.float().abs().max().item() + 0.02
+
+
+@pytest.mark.parametrize("case", [
+    # (N, H, W, cin, cout, stride, act, res, ldx_extra, x_coff, ldy_extra, y_coff)
+    (2, 56, 56, 64, 64, 1, ops.ACT_RELU, False, 0, 0, 0, 0),     # ResNet-50 layer1 conv2
+    (3, 13, 11, 64, 64, 1, ops.ACT_RELU, False, 0, 0, 0, 0),     # H % 4, pixel-block tails
+    (1, 1, 1, 64, 64, 1, ops.ACT_NONE, False, 0, 0, 0, 0),
+    (2, 9, 62, 64, 64, 1, ops.ACT_SILU, True, 64, 64, 32, 16),   # widest row, slices, +res
+    (2, 40, 40, 16, 32, 2, ops.ACT_SILU, False, 0, 0, 0, 0),     # YOLO b1 (stride 2)
+    (2, 21, 19, 16, 16, 1, ops.ACT_SILU, True, 16, 16, 16, 0),   # C2f bottleneck 16
+    (2, 20, 20, 32, 64, 2, ops.ACT_SILU, False, 0, 0, 0, 0),     # YOLO b3
+    (2, 20, 20, 32, 32, 1, ops.ACT_SILU, True, 0, 0, 0, 0),
+    (2, 19, 17, 64, 128, 2, ops.ACT_SILU, False, 0, 0, 0, 0),    # YOLO b5 (odd H, W)
+    (2, 10, 10, 64, 64, 2, ops.ACT_SILU, False, 0, 0, 0, 0),     # h16
+    (1, 160, 160, 16, 16, 1, ops.ACT_SILU, False, 0, 0, 0, 0),   # full YOLO row width
+])
+def test_conv_direct3x3(case):
+    """v4 persistent direct 3x3 conv (csrc/kernels/conv_direct.hip) vs the fp32 reference:
+    both strides, odd sizes, channel slices in/out, residual after the activation."""
+    N, H, W, cin, cout, s, act, res, lx, xc, ly, yc = case
+    a = act | (ops.RES_AFTER_ACT if res and act != ops.ACT_NONE else 0)
+    err, scale = _conv_case(N, H, W, cin, cout, 3, s, 1, a, res=res, ldx_extra=lx, x_coff=xc,
+                            ldy_extra=ly, y_coff=yc, tile=DIRECT0)
+    assert err <= 0.02 * scale + 0.02, (case, err, scale)
+
+
+def test_conv_direct3x3_rejects():
+    with pytest.raises(RuntimeError):  # W + 2 patch wider than the prefetch budget allows
+        _conv_case(1, 4, 1200, 64, 64, 3, 1, 1, ops.ACT_RELU, tile=DIRECT0)
+    with pytest.raises(RuntimeError):  # not instantiated
+        _conv_case(1, 8, 8, 48, 48, 3, 1, 1, ops.ACT_RELU, tile=DIRECT0)
 
 
 @pytest.mark.parametrize("shape", [(2, 112, 112), (3, 17, 13), (1, 8, 30)])
