@@ -42,20 +42,22 @@ constexpr int kNT = 512;
 constexpr int kOOB = 0x7ffffff0;
 constexpr int kLds = 160 * 1024;
 
-template <int CIN>
+template <int CIN, int KK>
 struct DirectCfg {
   static constexpr int PB = CIN * 2 + 16;         // patch bytes per pixel
   static constexpr int CPP = CIN / 8;             // 16-B chunks per pixel
   static constexpr int KPT = CIN / 16;            // 16-wide k-steps per tap
-  static constexpr int KS = 9 * KPT;              // k-steps per output block
+  static constexpr int KS = KK * KK * KPT;        // k-steps per output block
   static constexpr int PRE = CIN >= 64 ? 7 : 10;  // prefetch uint4 per thread (VGPR budget)
   static constexpr int MAX_PATCH = PRE * kNT * 16;
 };
 
-template <int CIN, int COUT, int S, int ACT, bool RES>
+// KK = 3: 3x3, pad 1, stride S.  KK = 2: the space-to-depth form of a stride-2 3x3 stem
+// (DeployedConv.stem_s2d): 2x2, stride 1, top/left pad 1, bottom/right pad 0.
+template <int CIN, int COUT, int S, int KK, int ACT, bool RES>
 __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvParams p, int kR,
                                                                 int PW, int patch_rows) {
-  using C = DirectCfg<CIN>;
+  using C = DirectCfg<CIN, KK>;
   constexpr int NCB = (COUT + 31) / 32;  // 32-channel blocks
   static_assert(8 % NCB == 0, "waves split evenly over channel blocks");
   constexpr int NPH = 8 / NCB;           // pixel-block phases
@@ -138,7 +140,9 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
       const int j = min(b * 32 + fr, npix - 1);  // clamp: pixels past npix are discarded
       const int yl = j / Wo, xc = j - yl * Wo;
       const unsigned char* pa0 = patch + (yl * S * PW + xc * S) * C::PB + fh * 16;
-      const unsigned char* pa[3] = {pa0, pa0 + rowb, pa0 + 2 * rowb};
+      const unsigned char* pa[KK];
+#pragma unroll
+      for (int r = 0; r < KK; ++r) pa[r] = pa0 + r * rowb;
       floatx16 acc;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -150,7 +154,7 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
       bf16x8 af[2];
       auto load = [&](int buf, int kk) __attribute__((always_inline)) {
         const int tap = kk / C::KPT, s4 = kk - (kk / C::KPT) * C::KPT;
-        const int r = tap / 3, s = tap - (tap / 3) * 3;
+        const int r = tap / KK, s = tap - (tap / KK) * KK;
         af[buf] = *reinterpret_cast<const bf16x8*>(pa[r] + s * C::PB + s4 * 32);
       };
       load(0, 0);
@@ -208,12 +212,12 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
 typedef void (*DirectFn)(const KvConvParams, int, int, int);
 
 struct DirectEntry {
-  int cin, cout, stride, act;
+  int cin, cout, stride, kk, act;
   bool res;
   DirectFn fn;
 };
 
-#define KV_DIRECT(CI, CO, S, A, R) {CI, CO, S, A, R, conv3x3_direct_kernel<CI, CO, S, A, R>}
+#define KV_DIRECT(CI, CO, S, A, R) {CI, CO, S, 3, A, R, conv3x3_direct_kernel<CI, CO, S, 3, A, R>}
 // the 3x3 shapes of ResNet-50 stage 1 and YOLOv8n's narrow layers (backbone, C2f
 // bottlenecks, PAN downsamplers, Detect 64-channel branches)
 static const DirectEntry kDirect[] = {
@@ -229,6 +233,10 @@ static const DirectEntry kDirect[] = {
     KV_DIRECT(64, 64, 1, kActSilu, false),   // b6 / h12 / h18 bottlenecks, Detect a1
     KV_DIRECT(64, 64, 1, kActSilu, true),
     KV_DIRECT(64, 64, 2, kActSilu, false),   // h16
+    KV_DIRECT(64, 128, 1, kActSilu, false),  // Detect P3 merged branch stem 64 -> 144 =
+    KV_DIRECT(64, 16, 1, kActSilu, false),   //   128 + 16 (Cout split, direct_launch)
+    // YOLO b0 stem in space-to-depth form: 2x2 over [N,320,320,16]
+    {16, 16, 1, 2, kActSilu, false, conv3x3_direct_kernel<16, 16, 1, 2, kActSilu, false>},
 };
 #undef KV_DIRECT
 
@@ -241,32 +249,35 @@ int direct_num_tiles() { return 1; }
 
 // Returns the instantiation index for p (or < 0), and the band geometry it would use.
 static int direct_plan(const KvConvParams* p, int* kR, int* PW, int* rows, int* lds) {
-  if (p->mode != 0 || p->KH != 3 || p->KW != 3 || p->pad != 1) return -8;
+  const int kk = p->KH;
+  if (p->mode != 0 || p->KW != kk || (kk != 2 && kk != 3) || p->pad != 1) return -8;
   if (p->stride != 1 && p->stride != 2) return -8;
+  if (kk == 2 && (p->stride != 1 || p->Ho != p->H || p->Wo != p->W)) return -8;  // s2d stem
   const int act = p->act & 3;
   const bool res = p->res != nullptr;
   if (res && !(p->act & 4) && act != kActNone) return -8;  // only x + act(conv)
   int idx = -1;
   for (int i = 0; i < (int)(sizeof(kDirect) / sizeof(kDirect[0])); ++i) {
     const DirectEntry& e = kDirect[i];
-    if (e.cin == p->Cin && e.cout == p->Cout && e.stride == p->stride && e.act == act &&
-        e.res == res) {
+    if (e.cin == p->Cin && e.cout == p->Cout && e.stride == p->stride && e.kk == kk &&
+        e.act == act && e.res == res) {
       idx = i;
       break;
     }
   }
   if (idx < 0) return -8;
-  if (p->Kpad != (9 * p->Cin + 63) / 64 * 64 || p->ldx % 8 || p->x_coff % 8) return -8;
-  if (p->Ho != (p->H - 1) / p->stride + 1 || p->Wo != (p->W - 1) / p->stride + 1) return -8;
+  if (p->Kpad != (kk * kk * p->Cin + 63) / 64 * 64 || p->ldx % 8 || p->x_coff % 8) return -8;
+  if (kk == 3 && (p->Ho != (p->H - 1) / p->stride + 1 || p->Wo != (p->W - 1) / p->stride + 1))
+    return -8;
   if ((long long)p->N * p->H * p->W * p->ldx * 2 >= kOOB) return -9;
   const int S = p->stride;
-  *PW = (p->Wo - 1) * S + 3;
+  *PW = (p->Wo - 1) * S + kk;
   const int pb = direct_pb(p->Cin);
   const int os = p->Cout + 8;
   // rows per band: as many as fit (<= 8) in the prefetch budget and LDS
   int r = 8;
   for (; r >= 1; --r) {
-    const int prows = (r - 1) * S + 3;
+    const int prows = (r - 1) * S + kk;
     const int patch = prows * *PW * pb;
     const int ob = r * p->Wo * os * 2;
     if (patch <= direct_max_patch(p->Cin) && ((patch + 15) & ~15) + ob <= kLds) break;
@@ -274,13 +285,12 @@ static int direct_plan(const KvConvParams* p, int* kR, int* PW, int* rows, int* 
   if (r < 1) return -11;
   if (r > p->Ho) r = p->Ho;
   *kR = r;
-  *rows = (r - 1) * S + 3;
+  *rows = (r - 1) * S + kk;
   *lds = ((*rows * *PW * pb + 15) & ~15) + r * p->Wo * os * 2;
   return idx;
 }
 
-int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
-  if (tile < 0 || tile >= direct_num_tiles()) return -6;
+static int direct_launch_one(const KvConvParams* p, hipStream_t stream) {
   int kR, PW, rows, lds;
   const int idx = direct_plan(p, &kR, &PW, &rows, &lds);
   if (idx < 0) return idx;
@@ -288,7 +298,7 @@ int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   if (items <= 0) return 0;
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess)
-    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
   const unsigned g = (unsigned)(items < ncu ? items : ncu);  // persistent: one per CU
   const DirectFn fn = kDirect[idx].fn;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -296,6 +306,43 @@ int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
     return -7;
   hipLaunchKernelGGL(fn, dim3(g), dim3(kNT), (unsigned)lds, stream, *p, kR, PW, rows);
   return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
+// A Cout with no instantiation of its own is covered by consecutive output-channel slices
+// that have one (largest first), e.g. YOLO's merged Detect stem 64 -> 144 = 128 + 16: each
+// slice re-reads the input (cheap: the layer is MFMA-bound) and writes its y_coff range.
+int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
+  if (tile < 0 || tile >= direct_num_tiles()) return -6;
+  int kR, PW, rows, lds;
+  if (direct_plan(p, &kR, &PW, &rows, &lds) >= 0) return direct_launch_one(p, stream);
+  if (p->res || p->Cout % 16) return -8;
+  // validate the whole split before launching anything
+  int cuts[8], ncut = 0, done = 0;
+  while (done < p->Cout && ncut < 8) {
+    int best = 0;
+    for (const DirectEntry& e : kDirect) {
+      KvConvParams q = *p;
+      q.Cout = e.cout;
+      if (e.cout <= p->Cout - done && e.cout > best && direct_plan(&q, &kR, &PW, &rows, &lds) >= 0)
+        best = e.cout;
+    }
+    if (best == 0) return -8;
+    cuts[ncut++] = best;
+    done += best;
+  }
+  if (done != p->Cout) return -8;
+  int off = 0;
+  for (int i = 0; i < ncut; ++i) {
+    KvConvParams q = *p;
+    q.Cout = cuts[i];
+    q.w = static_cast<const bf16*>(p->w) + (size_t)off * p->Kpad;
+    q.bias = p->bias ? p->bias + off : nullptr;
+    q.y_coff = p->y_coff + off;
+    const int rc = direct_launch_one(&q, stream);
+    if (rc != 0) return rc;
+    off += cuts[i];
+  }
+  return 0;
 }
 
 }  // namespace kvedge

@@ -322,6 +322,7 @@ def test_conv_poisoned_canary(tile, k):
     (2, 19, 17, 64, 128, 2, ops.ACT_SILU, False, 0, 0, 0, 0),    # YOLO b5 (odd H, W)
     (2, 10, 10, 64, 64, 2, ops.ACT_SILU, False, 0, 0, 0, 0),     # h16
     (1, 160, 160, 16, 16, 1, ops.ACT_SILU, False, 0, 0, 0, 0),   # full YOLO row width
+    (2, 20, 20, 64, 144, 1, ops.ACT_SILU, False, 0, 0, 16, 8),   # Detect stem: 128 + 16 split
 ])
 def test_conv_direct3x3(case):
     """v4 persistent direct 3x3 conv (csrc/kernels/conv_direct.hip) vs the fp32 reference:
@@ -331,6 +332,24 @@ def test_conv_direct3x3(case):
     err, scale = _conv_case(N, H, W, cin, cout, 3, s, 1, a, res=res, ldx_extra=lx, x_coff=xc,
                             ldy_extra=ly, y_coff=yc, tile=DIRECT0)
     assert err <= 0.02 * scale + 0.02, (case, err, scale)
+
+
+@pytest.mark.parametrize("shape", [(2, 40, 40), (1, 13, 7)])
+def test_conv_direct_s2d_stem(shape):
+    """v4 in its 2x2 form: the space-to-depth YOLO stem (stride-2 3x3 on RGB as a stride-1
+    2x2 over [N,H/2,W/2,16] with top/left pad 1, bottom/right pad 0), SiLU."""
+    N, H, W = shape
+    spec = ConvSpec(16, 16, 2, 2, 1, 1, ops.ACT_SILU, ops.MODE_GENERAL, pad_b=0)
+    x = _rand((N, H, W, 16), 11)
+    g = torch.Generator().manual_seed(12)
+    wp = ops.pack_conv_weight(torch.randn(16, 16, 2, 2, generator=g) * 0.2, spec)
+    b = torch.randn(16, generator=g) * 0.1
+    ref = ops.conv2d(x, spec, wp, b)
+    got = ops.conv2d(x.cuda(), spec, wp.cuda(), b.cuda(), tile=DIRECT0)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape == (N, H, W, 16)
+    err = (got.cpu().float() - ref.float()).abs().max().item()
+    assert err <= 0.02 * ref.float().abs().max().item() + 0.02, err
 
 
 def test_conv_direct3x3_rejects():
