@@ -47,6 +47,9 @@ def main(argv=None):
     ap.add_argument("--profile", default=None, metavar="PATH",
                     help="after the timed run, profile one eager step per op (HIP events) "
                          "and write the per-call table as JSON to PATH (rank 0)")
+    ap.add_argument("--cpu", action="store_true",
+                    help="plumbing check only: run the same DP bench path on the CPU "
+                         "reference ops over gloo (tests/test_bench_cpu.py); not a measurement")
     ap.add_argument("--native-loop", action="store_true",
                     help="time the K steps with the native C++ serve loop (csrc/runtime) "
                          "instead of Python graph.replay() calls")
@@ -56,26 +59,31 @@ def main(argv=None):
     from kvedge_amd import ops, parallel
     from kvedge_amd.engine import InferenceEngine
 
-    di = parallel.init_from_env(prefer_gpu=True)
-    if di.device.type != "cuda":
+    di = parallel.init_from_env(prefer_gpu=not a.cpu)
+    on_gpu = di.device.type == "cuda"
+    if not on_gpu and not a.cpu:
         print("bench.py needs a GPU (MI355X); none visible", file=sys.stderr)
         return 2
-    if not ops.load():
+    if on_gpu and not ops.load():
         raise RuntimeError("kvedge native kernels not built: run python -m kvedge_amd._build")
 
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
     if a.batch <= 0:
-        a.batch = 640 if a.model == "resnet50" else 256
+        a.batch = (640 if a.model == "resnet50" else 256) if on_gpu else 1
     t_build = time.perf_counter()
     if a.model == "resnet50":
         from kvedge_amd.models.resnet import KvResNet50
 
-        model = KvResNet50.build(seed=a.seed, device=di.device)
+        model = KvResNet50.build(seed=a.seed, device=di.device, calibrate=on_gpu)
         model.microbatch, model.microbatch_blocks = a.microbatch, a.mb_blocks
         hw = KvResNet50.image_size
     else:
         from kvedge_amd.models.yolov8 import KvYoloV8n
 
-        model = KvYoloV8n.build(seed=a.seed, device=di.device)
+        model = KvYoloV8n.build(seed=a.seed, device=di.device, calibrate=on_gpu)
         hw = KvYoloV8n.image_size
     # C1: every replica serves rank 0's weights
     parallel.broadcast_tensors(parallel.model_tensors(model), src=0)
@@ -86,9 +94,9 @@ def main(argv=None):
 
     for _ in range(a.warmup):
         eng.run()
-    torch.cuda.synchronize()
+    sync()
     parallel.barrier()
-    torch.cuda.synchronize()
+    sync()
     lat_hist = None
     t0 = time.perf_counter()
     if a.native_loop and eng.graph is not None:
@@ -99,10 +107,10 @@ def main(argv=None):
     else:
         for _ in range(a.steps):
             eng.run()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     parallel.barrier()
-    torch.cuda.synchronize()
+    sync()
 
     # C3: job time = slowest rank; C4: replica checksums (sanity, not timed)
     (max_elapsed,) = parallel.allreduce_scalars([elapsed], op="max")
@@ -127,7 +135,8 @@ def main(argv=None):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (on-device uint8 frames), random-init seeded weights",
+        "data": ("synthetic (on-device uint8 frames), random-init seeded weights" if on_gpu
+                 else "CPU plumbing check (reference ops) -- NOT a measurement"),
         "config": {
             "model": a.model,
             "global_batch": world * a.batch,
