@@ -117,6 +117,46 @@ void conv_dual(const at::Tensor& x1, const at::Tensor& x2, const at::Tensor& w,
   TORCH_CHECK(rc == 0, "kvedge: conv_dual failed rc=", rc);
 }
 
+// Frames-in space-to-depth stem (preprocess fused): y = act(conv2x2_s2d(frames) + bias)
+// with frames uint8 [N, 2H, 2W, 3] and w the packed [Cout, 64] s2d stem weights, already
+// scaled for raw 0..255 inputs (kvedge_amd.ops.stem_from_frames).
+void conv_frames_s2d(const at::Tensor& frames, const at::Tensor& w,
+                     const c10::optional<at::Tensor>& bias, at::Tensor& y, int64_t act,
+                     int64_t tile) {
+  check_dev(frames, "frames");
+  TORCH_CHECK(frames.scalar_type() == at::kByte && frames.dim() == 4 && frames.size(3) == 3 &&
+                  frames.size(1) % 2 == 0 && frames.size(2) % 2 == 0,
+              "kvedge: frames must be uint8 [N, H, W, 3] with even H, W");
+  check_bf16(w, "w");
+  check_bf16(y, "y");
+  const int64_t N = frames.size(0), H = frames.size(1) / 2, W = frames.size(2) / 2;
+  const int64_t Cout = w.size(0);
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == 64, "kvedge: s2d stem weight must be [Cout, 64]");
+  TORCH_CHECK(y.dim() == 4 && y.size(0) == N && y.size(1) == H && y.size(2) == W &&
+                  y.size(3) == Cout, "kvedge: y must be [N, H/2, W/2, Cout]");
+  TORCH_CHECK(frames.numel() < (1ll << 31) && y.numel() < (1ll << 31), "kvedge: int32 indexing");
+  const c10::DeviceGuard g(frames.device());
+  KvConvParams p{};
+  p.x = frames.data_ptr();
+  p.w = w.data_ptr();
+  p.bias = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_dev(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= Cout, "kvedge: bias fp32[Cout]");
+    p.bias = bias->data_ptr<float>();
+  }
+  p.res = nullptr;
+  p.y = y.data_ptr();
+  p.N = (int)N; p.H = (int)H; p.W = (int)W; p.Cin = 16; p.ldx = 16; p.x_coff = 0;
+  p.Ho = (int)H; p.Wo = (int)W; p.Cout = (int)Cout;
+  p.KH = 2; p.KW = 2; p.stride = 1; p.pad = 1; p.K = 64; p.Kpad = 64;
+  p.M = (int)(N * H * W);
+  p.ldy = (int)Cout; p.y_coff = 0; p.ldr = 0; p.r_coff = 0;
+  p.act = (int)act; p.mode = 0; p.in_u8 = 1;
+  const int rc = kv_conv2d(&p, (int)tile, cur_stream(frames));
+  TORCH_CHECK(rc == 0, "kvedge: conv_frames_s2d failed rc=", rc);
+}
+
 void maxpool2d(const at::Tensor& x, at::Tensor& y, int64_t N, int64_t H, int64_t W, int64_t C,
                int64_t ldx, int64_t x_coff, int64_t ldy, int64_t y_coff, int64_t k, int64_t stride, int64_t pad,
                int64_t Ho, int64_t Wo) {
@@ -304,6 +344,8 @@ TORCH_LIBRARY(kvedge, m) {
         "int pad, int K, int ldy, int y_coff, int ldr, int r_coff, int act, int mode, int tile) -> ()");
   m.def("conv_dual(Tensor x1, Tensor x2, Tensor w, Tensor? bias, Tensor(a!) y, int stride2, int act, "
         "int tile) -> ()");
+  m.def("conv_frames_s2d(Tensor frames, Tensor w, Tensor? bias, Tensor(a!) y, int act, "
+        "int tile) -> ()");
   m.def("stem_pool(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int y_coff) -> ()");
   m.def("maxpool2d(Tensor x, Tensor(a!) y, int N, int H, int W, int C, int ldx, int x_coff, int ldy, "
         "int y_coff, int k, int stride, int pad, int Ho, int Wo) -> ()");
@@ -329,6 +371,7 @@ TORCH_LIBRARY_IMPL(kvedge, CUDA, m) {
   m.impl("conv_dual", conv_dual);
   m.impl("maxpool2d", maxpool2d);
   m.impl("stem_pool", stem_pool);
+  m.impl("conv_frames_s2d", conv_frames_s2d);
   m.impl("sppf_pool", sppf_pool);
   m.impl("global_avgpool", global_avgpool);
   m.impl("softmax_rows", softmax_rows);

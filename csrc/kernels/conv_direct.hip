@@ -54,9 +54,13 @@ struct DirectCfg {
 
 // KK = 3: 3x3, pad 1, stride S.  KK = 2: the space-to-depth form of a stride-2 3x3 stem
 // (DeployedConv.stem_s2d): 2x2, stride 1, top/left pad 1, bottom/right pad 0.
-template <int CIN, int COUT, int S, int KK, int ACT, bool RES>
+// U8: x is uint8 RGB frames [N, 2H, 2W, 3]; the s2d patch (CIN = 16, channel
+// (dy*2+dx)*4 + c, channel 3 zero) is built on the fly from raw bytes (exact in bf16; the
+// 1/255 scale is folded into the weights), fusing the preprocess pass away.
+template <int CIN, int COUT, int S, int KK, int ACT, bool RES, bool U8 = false>
 __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvParams p, int kR,
                                                                 int PW, int patch_rows) {
+  static_assert(!U8 || (CIN == 16 && KK == 2 && S == 1), "frames-in form: the 2x2 s2d stem");
   using C = DirectCfg<CIN, KK>;
   constexpr int NCB = (COUT + 31) / 32;  // 32-channel blocks
   static_assert(8 % NCB == 0, "waves split evenly over channel blocks");
@@ -95,8 +99,21 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
   const int nchunks = patch_rows * PW * C::CPP;
   uint4 pre[C::PRE];
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(p.x), (short)0, p.N * H * W * p.ldx * 2, 0x00020000);
+      const_cast<void*>(p.x), (short)0, U8 ? p.N * H * W * 12 : p.N * H * W * p.ldx * 2,
+      0x00020000);
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  // chunk q -> (patch pixel pp, 16-B chunk c).  U8: q = (pr*2 + c)*PW + pc, so consecutive
+  // lanes walk one raw frame row (coalesced 6-B groups); otherwise pixel-major.
+  auto chunk_of = [&](int q, int& pp, int& c) __attribute__((always_inline)) {
+    if constexpr (U8) {
+      const int rc = q / PW, pc = q - rc * PW;
+      c = rc & 1;
+      pp = (rc >> 1) * PW + pc;
+    } else {
+      pp = q / C::CPP;
+      c = q - pp * C::CPP;
+    }
+  };
   auto fetch = [&](int item) __attribute__((always_inline)) {
     const int n = item / nbands, band = item - n * nbands;
     const int iy0 = band * kR * S - 1;
@@ -104,20 +121,34 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
 #pragma unroll
     for (int i = 0; i < C::PRE; ++i) {
       const int q = tid + kNT * i;
-      const int pp = q / C::CPP, c = q - pp * C::CPP;
+      int pp, c;
+      chunk_of(q, pp, c);
       const int pr = pp / PW, pc = pp - pr * PW;
       const int iy = iy0 + pr, ix = pc - 1;
       const bool ok = live && q < nchunks && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-      const int off = ok ? (((n * H + iy) * W + ix) * p.ldx + p.x_coff + c * 8) * 2 : kOOB;
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
-      pre[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      if constexpr (U8) {
+        // s2d chunk c of pixel (iy, ix) = raw row 2*iy + c, raw cols 2*ix, 2*ix + 1, RGB:
+        // 6 bytes -> [r g b 0 r' g' b' 0] as bf16 (integers 0..255 are exact)
+        const int off = ok ? ((n * 2 * H + 2 * iy + c) * 2 * W + 2 * ix) * 3 : kOOB;
+        const unsigned a = __builtin_amdgcn_raw_buffer_load_b16(rx, off, 0, 0);
+        const unsigned b = __builtin_amdgcn_raw_buffer_load_b16(rx, off + 2, 0, 0);
+        const unsigned d = __builtin_amdgcn_raw_buffer_load_b16(rx, off + 4, 0, 0);
+        auto bfb = [](unsigned byte) { return __float_as_uint((float)byte) >> 16; };
+        pre[i] = make_uint4(bfb(a & 0xff) | (bfb(a >> 8) << 16), bfb(b & 0xff),
+                            bfb(b >> 8) | (bfb(d & 0xff) << 16), bfb(d >> 8));
+      } else {
+        const int off = ok ? (((n * H + iy) * W + ix) * p.ldx + p.x_coff + c * 8) * 2 : kOOB;
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+        pre[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
     }
   };
   auto commit = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < C::PRE; ++i) {
       const int q = tid + kNT * i;
-      const int pp = q / C::CPP, c = q - pp * C::CPP;
+      int pp, c;
+      chunk_of(q, pp, c);
       if (q < nchunks) *reinterpret_cast<uint4*>(patch + pp * C::PB + c * 16) = pre[i];
     }
   };
@@ -215,6 +246,7 @@ struct DirectEntry {
   int cin, cout, stride, kk, act;
   bool res;
   DirectFn fn;
+  bool u8 = false;
 };
 
 #define KV_DIRECT(CI, CO, S, A, R) {CI, CO, S, 3, A, R, conv3x3_direct_kernel<CI, CO, S, 3, A, R>}
@@ -237,6 +269,9 @@ static const DirectEntry kDirect[] = {
     KV_DIRECT(64, 16, 1, kActSilu, false),   //   128 + 16 (Cout split, direct_launch)
     // YOLO b0 stem in space-to-depth form: 2x2 over [N,320,320,16]
     {16, 16, 1, 2, kActSilu, false, conv3x3_direct_kernel<16, 16, 1, 2, kActSilu, false>},
+    // ... and its frames-in form (preprocess fused)
+    {16, 16, 1, 2, kActSilu, false, conv3x3_direct_kernel<16, 16, 1, 2, kActSilu, false, true>,
+     true},
 };
 #undef KV_DIRECT
 
@@ -260,16 +295,17 @@ static int direct_plan(const KvConvParams* p, int* kR, int* PW, int* rows, int* 
   for (int i = 0; i < (int)(sizeof(kDirect) / sizeof(kDirect[0])); ++i) {
     const DirectEntry& e = kDirect[i];
     if (e.cin == p->Cin && e.cout == p->Cout && e.stride == p->stride && e.kk == kk &&
-        e.act == act && e.res == res) {
+        e.act == act && e.res == res && e.u8 == (p->in_u8 != 0)) {
       idx = i;
       break;
     }
   }
   if (idx < 0) return -8;
   if (p->Kpad != (kk * kk * p->Cin + 63) / 64 * 64 || p->ldx % 8 || p->x_coff % 8) return -8;
+  if (p->in_u8 && (long long)p->N * p->H * p->W * 12 >= kOOB) return -9;
   if (kk == 3 && (p->Ho != (p->H - 1) / p->stride + 1 || p->Wo != (p->W - 1) / p->stride + 1))
     return -8;
-  if ((long long)p->N * p->H * p->W * p->ldx * 2 >= kOOB) return -9;
+  if (!p->in_u8 && (long long)p->N * p->H * p->W * p->ldx * 2 >= kOOB) return -9;
   const int S = p->stride;
   *PW = (p->Wo - 1) * S + kk;
   const int pb = direct_pb(p->Cin);

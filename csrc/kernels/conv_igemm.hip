@@ -351,7 +351,8 @@ static bool kv_in_alloc(const void* ptr, long long bytes) {
 
 static int kv_conv_check_extents(const KvConvParams* p) {
   const long long M = (long long)p->N * p->Ho * p->Wo;
-  if (!kv_in_alloc(p->x, (long long)p->N * p->H * p->W * p->ldx * 2)) return -20;
+  if (!kv_in_alloc(p->x, p->in_u8 ? (long long)p->N * p->H * p->W * 12
+                                    : (long long)p->N * p->H * p->W * p->ldx * 2)) return -20;
   if (!kv_in_alloc(p->w, (long long)p->Cout * p->Kpad * 2)) return -21;
   if (!kv_in_alloc(p->bias, (long long)p->Cout * 4)) return -22;
   if (!kv_in_alloc(p->y, M * p->ldy * 2)) return -23;
@@ -368,6 +369,11 @@ extern "C" int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream) {
   if (const int rc = kv_conv_check_extents(p)) return rc;
 #endif
   if (p->Kpad % BK != 0 || p->Cout % 8 != 0) return -1;
+  if (p->in_u8) {  // frames-in s2d stem: the direct family only
+    const int v4 = kNumTiles + glds_num_tiles() + stream_num_tiles();
+    if (tile >= 0 && tile < v4) return -8;
+    return direct_launch(p, tile < 0 ? 0 : tile - v4, stream);
+  }
   if (p->mode == 2 && (p->Cin != 4 || p->ldx != 4)) return -2;
   if (p->mode != 2 && (p->Cin % 8 != 0 || p->ldx % 8 != 0 || p->x_coff % 8 != 0)) return -3;
   if (p->mode == 1 && (p->KH != 1 || p->KW != 1 || p->stride != 1 || p->pad != 0)) return -4;

@@ -37,6 +37,10 @@ typedef struct KvConvParams {
   // (the bottleneck's input, i.e. the downsample branch folded in as extra K).
   const void* x2;
   int K1, H2, W2, ldx2, stride2;
+  // in_u8 = 1: x is uint8 RGB frames [N, 2H, 2W, 3] and the conv reads their
+  // space-to-depth image [N, H, W, 16] (channel (dy*2+dx)*4 + c, channel 3 zero) built on
+  // the fly -- the preprocess pass is fused away (v4 direct tile, 2x2 s2d stem only).
+  int in_u8;
 } KvConvParams;
 
 // tile: -1 = heuristic; otherwise an index into the tile table (kv_conv_num_tiles()).

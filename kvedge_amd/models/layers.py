@@ -69,7 +69,7 @@ class DeployedConv:
 
     @staticmethod
     def stem_s2d(conv: nn.Conv2d, bn: Optional[nn.BatchNorm2d], act: int,
-                 device="cpu") -> "DeployedConv":
+                 device="cpu", in_scale: float = 1.0) -> "DeployedConv":
         """Stride-2 KxK stem on RGB -> stride-1 ceil(K/2)... tap conv over the
         space-to-depth input [N, H/2, W/2, 16] written by ops.preprocess(s2d=True).
 
@@ -77,8 +77,12 @@ class DeployedConv:
         q = (p + 1) // 2:  r = 2a + dy + p - 2q, by = ho - q + a, a in [0, ka).
         Taps with r outside [0, K) get zero weight.  Top/left pad q; bottom/right pad
         ka - 1 - q keeps Ho = H/2.  Every 8-element MFMA k-chunk is then one aligned
-        16-B load (2 pixels x 4 channels), i.e. the general implicit-GEMM path."""
+        16-B load (2 pixels x 4 channels), i.e. the general implicit-GEMM path.
+
+        ``in_scale`` folds an input scale into the weights: 1/255 gives the frames-in
+        form (ops.stem_from_frames) that reads raw 0..255 pixel values."""
         wf, bf = fold_bn(conv, bn)
+        wf = wf * in_scale
         cout, cin, k, _ = wf.shape
         p, s = conv.padding[0], conv.stride[0]
         assert s == 2 and cin <= 4 and conv.padding[0] == conv.padding[1]

@@ -269,6 +269,9 @@ class KvYoloV8n:
         self.conf, self.iou, self.max_det = conf, iou, max_det
         d = self.device
         self.b0 = DeployedConv.stem_s2d(ref.b0.conv, ref.b0.bn, ACT_SILU, d)  # K12b s2d stem
+        # the same stem reading raw frames (preprocess fused into the conv, GPU path)
+        self.b0_frames = DeployedConv.stem_s2d(ref.b0.conv, ref.b0.bn, ACT_SILU, d,
+                                               in_scale=1.0 / 255)
         self.b1, self.b3, self.b5, self.b7 = (_dc(m, d) for m in (ref.b1, ref.b3, ref.b5, ref.b7))
         self._ref = ref
         self._flops = {}
@@ -284,7 +287,7 @@ class KvYoloV8n:
         return KvYoloV8n(init_yolov8n(seed, calibrate=calibrate), device)
 
     def convs(self) -> List[DeployedConv]:
-        out = [self.b0, self.b1, self.b3, self.b5, self.b7, self.h16, self.h19]
+        out = [self.b0, self.b0_frames, self.b1, self.b3, self.b5, self.b7, self.h16, self.h19]
         for m in (self.b2, self.b4, self.b6, self.b8, self.b9, self.h12, self.h15, self.h18,
                   self.h21):
             out += m.convs()
@@ -301,12 +304,22 @@ class KvYoloV8n:
     def preprocess(self, frames_u8: torch.Tensor) -> torch.Tensor:
         return ops.preprocess(frames_u8, mean=(0.0, 0.0, 0.0), std=(1.0, 1.0, 1.0), s2d=True)
 
-    def heads(self, x: torch.Tensor):
-        """x: preprocessed bf16 s2d [N,320,320,16] -> three [N,h,w,144] head outputs."""
+    fuse_preprocess: bool = True  # GPU: frames -> b0 output in one kernel
+
+    def stem(self, frames_u8: torch.Tensor) -> torch.Tensor:
+        """uint8 frames -> b0 output [N,320,320,16]."""
+        if self.fuse_preprocess and frames_u8.is_cuda:
+            b = self.b0_frames
+            return ops.stem_from_frames(frames_u8, b.spec, b.w, b.b)
+        return self.b0(self.preprocess(frames_u8))
+
+    def heads(self, x: torch.Tensor, stem_done: bool = False):
+        """x: preprocessed bf16 s2d [N,320,320,16] (or, with stem_done, the b0 output)
+        -> three [N,h,w,144] head outputs."""
         N = x.shape[0]
         dev = x.device
         bf = torch.bfloat16
-        x = self.b1(self.b0(x))                       # [N,160,160,32]
+        x = self.b1(x if stem_done else self.b0(x))   # [N,160,160,32]
         x = self.b2(x)
         x = self.b3(x)                                # [N,80,80,64]
         H3 = x.shape[1]
@@ -332,6 +345,6 @@ class KvYoloV8n:
         return [lv(p) for lv, p in zip(self.levels, (p3, p4, p5))]
 
     def __call__(self, frames_u8: torch.Tensor):
-        feats = self.heads(self.preprocess(frames_u8))
+        feats = self.heads(self.stem(frames_u8), stem_done=True)
         boxes, scores, cls = ops.yolo_decode(feats, STRIDES, self.nc)
         return ops.nms(boxes, scores, cls, self.conf, self.iou, self.max_det)

@@ -252,6 +252,27 @@ def stem_pool(x: torch.Tensor, spec: "ConvSpec", w: torch.Tensor, bias: torch.Te
     return out
 
 
+def stem_from_frames(frames: torch.Tensor, spec: "ConvSpec", w: torch.Tensor,
+                     bias: Optional[torch.Tensor], out: Optional[torch.Tensor] = None,
+                     tile: int = -1) -> torch.Tensor:
+    """Preprocess + space-to-depth + 2x2 s2d stem conv in ONE pass (YOLO b0).
+
+    frames: uint8 [N, H, W, 3]; spec/w/bias: a DeployedConv.stem_s2d(..., in_scale=1/255)
+    (weights scaled for raw 0..255 inputs, so the 1/255 normalisation costs nothing).
+    GPU: the frames-in v4 direct kernel (csrc/kernels/conv_direct.hip) builds the s2d
+    patch from raw bytes in LDS -- the [N, H/2, W/2, 16] bf16 image is never written.
+    CPU: the reference preprocess (values 0..255) then the reference conv."""
+    assert spec.kh == 2 and spec.stride == 1 and spec.cin == 16, spec
+    N, H, W, _ = frames.shape
+    if out is None:
+        out = empty(N, H // 2, W // 2, spec.cout, dtype=torch.bfloat16, device=frames.device)
+    if frames.is_cuda:
+        _native().conv_frames_s2d(frames, w, bias, out, spec.act, tile)
+        return out
+    x = preprocess(frames, mean=(0.0, 0.0, 0.0), std=(1.0 / 255,) * 3, s2d=True)
+    return conv2d(x, spec, w, bias, out=out)
+
+
 def maxpool2d(x: torch.Tensor, k: int, stride: int, pad: int, out: Optional[torch.Tensor] = None,
               C: Optional[int] = None, x_coff: int = 0, y_coff: int = 0) -> torch.Tensor:
     N, H, W, ldx = x.shape

@@ -109,3 +109,18 @@ def test_resnet50_microbatch_equivalence():
         kv.microbatch, kv.microbatch_blocks = 2, 4
         micro = kv.features(x).float()
     assert torch.equal(full, micro)
+
+
+def test_yolo_frames_in_stem_matches_preprocess_path():
+    """ops.stem_from_frames (1/255 folded into the weights, raw 0..255 inputs) == the
+    unfused preprocess -> s2d stem conv, on the CPU reference ops."""
+    from kvedge_amd.models.yolov8 import KvYoloV8n, init_yolov8n
+
+    kv = KvYoloV8n(init_yolov8n(seed=1, calibrate=False), "cpu")
+    fr = torch.randint(0, 256, (2, 64, 96, 3), dtype=torch.uint8,
+                       generator=torch.Generator().manual_seed(4))
+    with torch.no_grad():
+        fused = kv.stem(fr).float()
+        plain = kv.b0(kv.preprocess(fr)).float()
+    assert fused.shape == plain.shape == (2, 32, 48, 16)
+    assert (fused - plain).abs().max().item() <= 0.02 * plain.abs().max().item() + 0.02

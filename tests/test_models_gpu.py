@@ -94,3 +94,31 @@ def test_yolov8n_pipeline_graph(yolo):
     o_c, n_c = ops.nms(b.cpu(), s.cpu(), c.cpu(), 0.05, 0.7, 300)
     assert torch.equal(n_g.cpu(), n_c)
     assert (o_g.cpu() - o_c).abs().max() < 1e-3
+
+
+@pytest.mark.parametrize("hw", [(64, 96), (22, 10)])
+def test_stem_from_frames_kernel(hw):
+    """Frames-in v4 kernel (preprocess + s2d + 2x2 stem in one pass) vs the CPU reference."""
+    from kvedge_amd.models.yolov8 import KvYoloV8n, init_yolov8n
+
+    kv = KvYoloV8n(init_yolov8n(seed=1, calibrate=False), "cpu")
+    b = kv.b0_frames
+    fr = torch.randint(0, 256, (3, hw[0], hw[1], 3), dtype=torch.uint8,
+                       generator=torch.Generator().manual_seed(7))
+    ref = ops.stem_from_frames(fr, b.spec, b.w, b.b).float()
+    got = ops.stem_from_frames(fr.cuda(), b.spec, b.w.cuda(), b.b.cuda())
+    torch.cuda.synchronize()
+    err = (got.cpu().float() - ref).abs().max().item()
+    assert err <= 0.02 * ref.abs().max().item() + 0.02, err
+
+
+def test_yolov8n_fused_stem_parity(yolo):
+    _, kv, kv_cpu = yolo
+    fr = _frames(2, 6, hw=320)
+    with torch.no_grad():
+        hg = kv.heads(kv.stem(fr.cuda()), stem_done=True)
+        hc = kv_cpu.heads(kv_cpu.preprocess(fr))
+    for g, c in zip(hg, hc):
+        cos = torch.nn.functional.cosine_similarity(g.float().cpu().flatten(), c.float().flatten(),
+                                                    dim=0)
+        assert cos > 0.999, float(cos)
