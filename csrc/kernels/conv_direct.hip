@@ -41,6 +41,7 @@ namespace {
 constexpr int kNT = 512;
 constexpr int kOOB = 0x7ffffff0;
 constexpr int kLds = 160 * 1024;
+constexpr int kBiasBytes = 4 * 128;  // bias slot at the top of the LDS allocation
 
 template <int CIN, int KK>
 struct DirectCfg {
@@ -57,6 +58,11 @@ struct DirectCfg {
 // U8: x is uint8 RGB frames [N, 2H, 2W, 3]; the s2d patch (CIN = 16, channel
 // (dy*2+dx)*4 + c, channel 3 zero) is built on the fly from raw bytes (exact in bf16; the
 // 1/255 scale is folded into the weights), fusing the preprocess pass away.
+#ifndef KV_DIRECT_PD
+#define KV_DIRECT_PD 2
+#endif
+constexpr int KPD = KV_DIRECT_PD;  // LDS fragment reads in flight ahead of the MFMA
+
 template <int CIN, int COUT, int S, int KK, int ACT, bool RES, bool U8 = false>
 __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvParams p, int kR,
                                                                 int PW, int patch_rows) {
@@ -87,13 +93,10 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
     if (wrow < COUT) v = *reinterpret_cast<const bf16x8*>(wp + wrow * p.Kpad + kk * 16 + fh * 8);
     wreg[kk] = v;
   }
-  float4 bv[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int ch = cb * 32 + g * 8 + fh * 4;
-    bv[g] = (p.bias && ch < COUT) ? *reinterpret_cast<const float4*>(p.bias + ch)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
+  // bias staged once in LDS (not 16 live VGPRs: the CIN = 64 forms sit at the 256 cap)
+  float* lbias = reinterpret_cast<float*>(
+      lds + ((patch_rows * PW * C::PB + 15) & ~15) + ((kR * p.Wo * OS * 2 + 15) & ~15));
+  if (tid < NCB * 32) lbias[tid] = (p.bias && tid < COUT) ? p.bias[tid] : 0.f;
 
   // ---- band patch prefetch: 16-B chunk q -> patch pixel q / CPP (row-major, pitch PW)
   const int nchunks = patch_rows * PW * C::CPP;
@@ -177,28 +180,34 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
       floatx16 acc;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        acc[4 * g + 0] = bv[g].x;
-        acc[4 * g + 1] = bv[g].y;
-        acc[4 * g + 2] = bv[g].z;
-        acc[4 * g + 3] = bv[g].w;
+        const float4 bv = *reinterpret_cast<const float4*>(lbias + cb * 32 + g * 8 + fh * 4);
+        acc[4 * g + 0] = bv.x;
+        acc[4 * g + 1] = bv.y;
+        acc[4 * g + 2] = bv.z;
+        acc[4 * g + 3] = bv.w;
       }
-      bf16x8 af[2];
+      // fragment ring: the read for step kk + PD is issued before the MFMA of step kk, so
+      // PD LDS reads are in flight behind the MFMA pipe (PD = 1 left the MFMAs waiting on
+      // ds_read latency: 29 % MFMA busy in PMC)
+      constexpr int PD = KPD;
+      bf16x8 af[PD + 1];
       auto load = [&](int buf, int kk) __attribute__((always_inline)) {
         const int tap = kk / C::KPT, s4 = kk - (kk / C::KPT) * C::KPT;
         const int r = tap / KK, s = tap - (tap / KK) * KK;
         af[buf] = *reinterpret_cast<const bf16x8*>(pa[r] + s * C::PB + s4 * 32);
       };
-      load(0, 0);
+#pragma unroll
+      for (int kk = 0; kk < PD; ++kk) load(kk, kk);
 #pragma unroll
       for (int kk = 0; kk < C::KS; ++kk) {
-        if (kk + 1 < C::KS) load((kk + 1) & 1, kk + 1);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wreg[kk], af[kk & 1], acc, 0, 0, 0);
+        if (kk + PD < C::KS) load((kk + PD) % (PD + 1), kk + PD);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wreg[kk], af[kk % (PD + 1)], acc, 0, 0, 0);
       }
-      // reads(0) | reads(k+1) MFMA(k) ...: one fragment read in flight per MFMA
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      // reads(0..PD-1) | reads(k+PD) MFMA(k) ...
+      __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);
 #pragma unroll
       for (int kk = 0; kk < C::KS; ++kk) {
-        if (kk + 1 < C::KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        if (kk + PD < C::KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       }
       const int jr = b * 32 + fr;
@@ -216,6 +225,9 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
       }
     }
     __syncthreads();  // output tile complete; patch no longer read
+    // next band's patch BEFORE this band's stores: on gfx9 vmcnt counts stores too, so a
+    // commit after the store pass made its vmcnt(0) wait for this band's stores to land
+    commit();
 
     // ---- store the band (+ residual after the activation): 16-B channel chunks
     constexpr int OCH = COUT / 8;
@@ -235,7 +247,6 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
       }
       *reinterpret_cast<uint4*>(Y + m * p.ldy + p.y_coff + c * 8) = v;
     }
-    commit();         // next band's patch (landed during the MFMAs)
     __syncthreads();  // patch ready, output tile free
   }
 }
@@ -316,13 +327,15 @@ static int direct_plan(const KvConvParams* p, int* kR, int* PW, int* rows, int* 
     const int prows = (r - 1) * S + kk;
     const int patch = prows * *PW * pb;
     const int ob = r * p->Wo * os * 2;
-    if (patch <= direct_max_patch(p->Cin) && ((patch + 15) & ~15) + ob <= kLds) break;
+    if (patch <= direct_max_patch(p->Cin) &&
+        ((patch + 15) & ~15) + ((ob + 15) & ~15) + kBiasBytes <= kLds)
+      break;
   }
   if (r < 1) return -11;
   if (r > p->Ho) r = p->Ho;
   *kR = r;
   *rows = (r - 1) * S + kk;
-  *lds = ((*rows * *PW * pb + 15) & ~15) + r * p->Wo * os * 2;
+  *lds = ((*rows * *PW * pb + 15) & ~15) + ((r * p->Wo * os * 2 + 15) & ~15) + kBiasBytes;
   return idx;
 }
 

@@ -192,6 +192,9 @@ __global__ __launch_bounds__(NT, 1) void stem_pool_kernel(
       }
     }
     __syncthreads();  // stem tile complete; patch no longer read
+    // next band's patch BEFORE the pool's stores (vmcnt counts stores on gfx9: a commit
+    // after them waited for this band's stores to land)
+    commit();
 
     // ---- 3x3/2 max pool (pad 1) of the band -> global, 16 B per thread-iteration
 #pragma unroll
@@ -220,7 +223,6 @@ __global__ __launch_bounds__(NT, 1) void stem_pool_kernel(
         *reinterpret_cast<uint4*>(yrow + px * ldy + c8 * 8) = m;
       }
     }
-    commit();         // next band's patch (its loads have landed by now)
     __syncthreads();  // tile free, patch ready
   }
 }
