@@ -117,6 +117,77 @@ void conv_dual(const at::Tensor& x1, const at::Tensor& x2, const at::Tensor& w,
   TORCH_CHECK(rc == 0, "kvedge: conv_dual failed rc=", rc);
 }
 
+// Fused bottleneck tail: y = act(x . W^T [+ x2 . W2^T] + bias [+ res]) (conv3, optionally
+// with the fused downsample), then z = ReLU(y . w1^T + b1) -- the next block's 1x1 reduce --
+// from the y tile still in LDS, so y is written once and never re-read.
+void conv_tail(const at::Tensor& x, const c10::optional<at::Tensor>& x2, const at::Tensor& w,
+               const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res,
+               at::Tensor& y, const at::Tensor& w1, const c10::optional<at::Tensor>& b1,
+               at::Tensor& z, int64_t stride2, int64_t act, int64_t tile) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_bf16(y, "y");
+  check_bf16(w1, "w1");
+  check_bf16(z, "z");
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && z.dim() == 4, "kvedge: NHWC tensors");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), K1 = x.size(3);
+  const int64_t Cout = y.size(3), Nt = w1.size(0);
+  TORCH_CHECK(y.size(0) == N && y.size(1) == H && y.size(2) == W, "kvedge: y shape");
+  TORCH_CHECK(z.size(0) == N && z.size(1) == H && z.size(2) == W && z.size(3) == Nt,
+              "kvedge: z shape");
+  TORCH_CHECK(w1.dim() == 2 && w1.size(1) == Cout, "kvedge: w1 must be [n_t, Cout]");
+  TORCH_CHECK(K1 % 64 == 0, "kvedge: conv_tail K1 multiple of 64");
+  const c10::DeviceGuard g(x.device());
+  KvConvParams p{};
+  p.x = x.data_ptr();
+  p.w = w.data_ptr();
+  p.bias = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_dev(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= Cout, "kvedge: bias fp32[Cout]");
+    p.bias = bias->data_ptr<float>();
+  }
+  p.y = y.data_ptr();
+  p.N = (int)N; p.H = (int)H; p.W = (int)W; p.Cin = (int)K1; p.ldx = (int)K1; p.x_coff = 0;
+  p.Ho = (int)H; p.Wo = (int)W; p.Cout = (int)Cout;
+  p.KH = 1; p.KW = 1; p.stride = 1; p.pad = 0;
+  p.M = (int)(N * H * W);
+  p.ldy = (int)Cout; p.y_coff = 0; p.r_coff = 0;
+  p.act = (int)act;
+  if (x2.has_value() && x2->defined()) {
+    check_bf16(*x2, "x2");
+    TORCH_CHECK(!(res.has_value() && res->defined()), "kvedge: conv_tail dual form takes no res");
+    const int64_t K2 = x2->size(3);
+    TORCH_CHECK(x2->dim() == 4 && x2->size(0) == N && (x2->size(1) + stride2 - 1) / stride2 == H &&
+                    (x2->size(2) + stride2 - 1) / stride2 == W && K2 % 64 == 0,
+                "kvedge: x2 geometry vs stride");
+    TORCH_CHECK(w.dim() == 2 && w.size(0) == Cout && w.size(1) == K1 + K2, "kvedge: w [Cout, K1+K2]");
+    p.mode = 4; p.K = (int)(K1 + K2); p.Kpad = (int)(K1 + K2);
+    p.x2 = x2->data_ptr(); p.K1 = (int)K1; p.H2 = (int)x2->size(1); p.W2 = (int)x2->size(2);
+    p.ldx2 = (int)K2; p.stride2 = (int)stride2;
+    p.res = nullptr; p.ldr = 0;
+  } else {
+    TORCH_CHECK(res.has_value() && res->defined(), "kvedge: conv_tail plain form needs res");
+    check_bf16(*res, "res");
+    TORCH_CHECK(res->sizes() == y.sizes(), "kvedge: res shape");
+    TORCH_CHECK(w.dim() == 2 && w.size(0) == Cout && w.size(1) == K1, "kvedge: w [Cout, K1]");
+    p.mode = 1; p.K = (int)K1; p.Kpad = (int)K1;
+    p.res = res->data_ptr(); p.ldr = (int)Cout;
+  }
+  p.w_t = w1.data_ptr();
+  p.bias_t = nullptr;
+  if (b1.has_value() && b1->defined()) {
+    check_dev(*b1, "b1");
+    TORCH_CHECK(b1->scalar_type() == at::kFloat && b1->numel() >= Nt, "kvedge: b1 fp32[n_t]");
+    p.bias_t = b1->data_ptr<float>();
+  }
+  p.z = z.data_ptr(); p.n_t = (int)Nt; p.ldz = (int)Nt; p.z_coff = 0; p.act_t = 1;
+  TORCH_CHECK(x.numel() < (1ll << 30) && y.numel() < (1ll << 31) && z.numel() < (1ll << 31),
+              "kvedge: tensor too large for 32-bit buffer offsets");
+  const int rc = kv_conv2d(&p, (int)tile, cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: conv_tail failed rc=", rc);
+}
+
 // Frames-in space-to-depth stem (preprocess fused): y = act(conv2x2_s2d(frames) + bias)
 // with frames uint8 [N, 2H, 2W, 3] and w the packed [Cout, 64] s2d stem weights, already
 // scaled for raw 0..255 inputs (kvedge_amd.ops.stem_from_frames).
@@ -344,6 +415,8 @@ TORCH_LIBRARY(kvedge, m) {
         "int pad, int K, int ldy, int y_coff, int ldr, int r_coff, int act, int mode, int tile) -> ()");
   m.def("conv_dual(Tensor x1, Tensor x2, Tensor w, Tensor? bias, Tensor(a!) y, int stride2, int act, "
         "int tile) -> ()");
+  m.def("conv_tail(Tensor x, Tensor? x2, Tensor w, Tensor? bias, Tensor? res, Tensor(a!) y, "
+        "Tensor w1, Tensor? b1, Tensor(b!) z, int stride2, int act, int tile) -> ()");
   m.def("conv_frames_s2d(Tensor frames, Tensor w, Tensor? bias, Tensor(a!) y, int act, "
         "int tile) -> ()");
   m.def("stem_pool(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int y_coff) -> ()");
@@ -372,6 +445,7 @@ TORCH_LIBRARY_IMPL(kvedge, CUDA, m) {
   m.impl("maxpool2d", maxpool2d);
   m.impl("stem_pool", stem_pool);
   m.impl("conv_frames_s2d", conv_frames_s2d);
+  m.impl("conv_tail", conv_tail);
   m.impl("sppf_pool", sppf_pool);
   m.impl("global_avgpool", global_avgpool);
   m.impl("softmax_rows", softmax_rows);

@@ -306,6 +306,7 @@ int glds_tile_bn(int tile);
 // v3 persistent streaming family (conv_stream.hip, 1x1 GEMM / dual only): indices after v2
 int stream_num_tiles();
 int stream_launch(const KvConvParams* p, int tile, hipStream_t stream);
+int stream_tail_tile(int n_t);
 // v4 family (conv_direct.hip): persistent direct 3x3 conv for narrow channel counts
 int direct_num_tiles();
 int direct_launch(const KvConvParams* p, int tile, hipStream_t stream);
@@ -357,6 +358,10 @@ static int kv_conv_check_extents(const KvConvParams* p) {
   if (!kv_in_alloc(p->bias, (long long)p->Cout * 4)) return -22;
   if (!kv_in_alloc(p->y, M * p->ldy * 2)) return -23;
   if (p->res && !kv_in_alloc(p->res, M * p->ldr * 2)) return -24;
+  if (p->n_t && (!kv_in_alloc(p->z, M * p->ldz * 2) ||
+                 !kv_in_alloc(p->w_t, (long long)p->n_t * p->Cout * 2) ||
+                 !kv_in_alloc(p->bias_t, (long long)p->n_t * 4)))
+    return -28;
   if (p->mode == 4 && !kv_in_alloc(p->x2, (long long)p->N * p->H2 * p->W2 * p->ldx2 * 2)) return -25;
   if (p->x_coff + p->Cin > p->ldx || p->y_coff + p->Cout > p->ldy) return -26;
   if (p->res && p->r_coff + p->Cout > p->ldr) return -27;
@@ -369,6 +374,12 @@ extern "C" int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream) {
   if (const int rc = kv_conv_check_extents(p)) return rc;
 #endif
   if (p->Kpad % BK != 0 || p->Cout % 8 != 0) return -1;
+  if (p->n_t) {  // fused bottleneck tail: the v3 tail tile only
+    const int v3 = kNumTiles + glds_num_tiles();
+    if (tile < 0) tile = v3 + stream_tail_tile(p->n_t);
+    if (tile < v3 || tile >= v3 + stream_num_tiles()) return -8;
+    return stream_launch(p, tile - v3, stream);
+  }
   if (p->in_u8) {  // frames-in s2d stem: the direct family only
     const int v4 = kNumTiles + glds_num_tiles() + stream_num_tiles();
     if (tile >= 0 && tile < v4) return -8;

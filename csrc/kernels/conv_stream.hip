@@ -61,12 +61,18 @@ __device__ __forceinline__ void wait_vm() {
 
 // LDS bytes of one variant (host + device agree on the layout)
 __host__ __device__ constexpr int stream_lds_bytes(int bm, int bn, int d, bool res, bool bres,
-                                                   int kpad) {
-  return 2 * (d * (bm * BK + (bres ? 0 : bn * BK)) + (bres ? bn * kpad : 0) + bm * (bn + 8));
+                                                   int kpad, int nt1 = 0) {
+  return 2 * (d * (bm * BK + (bres ? 0 : bn * BK)) + (bres ? bn * kpad : 0) + bm * (bn + 8) +
+              nt1 * bn);
 }
 
-template <int BM, int BN, int D, int MODE, bool RES, bool BRES, int POL>
-__global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams p) {
+// NT1 > 0: fused bottleneck tail -- after the y tile is written, z = ReLU(y . Wt^T + bt)
+// (the next block's 1x1 reduce, NT1 output channels) is computed from the y tile in LDS.
+template <int BM, int BN, int D, int MODE, bool RES, bool BRES, int POL, int NT1 = 0>
+// 128x128 resident-weight tiles (and the tail tiles) hold >100 KB of weights: one
+// workgroup per CU, so they may use the whole 512-entry register file
+__global__ __launch_bounds__(256, (NT1 || (BM * BN >= 128 * 128 && BRES)) ? 1 : 2)
+void conv_stream_kernel(const KvConvParams p) {
   constexpr int WM = 2, WN = 2;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -78,7 +84,9 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams 
   constexpr int SLOT = SA + SB;
   // VMEM ops per stage per wave, and per epilogue (stores)
   constexpr int SI = A_INS + (BRES ? 0 : B_INS) + (RES ? PER : 0);
-  constexpr int EPI = PER;
+  constexpr int PERZ = NT1 ? BM * NT1 / 8 / 256 : 0;  // 16-B z chunks per thread (tail)
+  constexpr int EPI = PER + PERZ;
+  static_assert(NT1 == 0 || (BM == 64 && BRES && NT1 % 64 == 0 && PERZ >= 1), "tail tile");
   // cache policy of the streamed (read-once / write-once) bytes: 0 default, 2 = nt
   constexpr int SP = POL;
   static_assert(TM >= 1 && TN >= 1 && PER >= 1 && D >= 2 && D <= 6, "tile");
@@ -87,6 +95,7 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams 
   const int nk = p.Kpad / BK;
   bf16* const Bres = smem + D * SLOT;
   bf16* const Cs = Bres + (BRES ? BN * p.Kpad : 0);
+  bf16* const W1s = Cs + BM * CS;  // tail: resident [BN/64][NT1][64] swizzled blocks
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -238,6 +247,80 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams 
                                              : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 
+  // tail GEMM: 2 x 2 waves, wave tile 32 pixels x NT1/2 channels, bias in registers
+  constexpr int TN1 = NT1 ? NT1 / 64 : 1;
+  float4 bias1_r[TN1][4];
+  const __amdgpu_buffer_rsrc_t rz = mk_rsrc(NT1 ? p.z : p.y, NT1 ? p.M * p.ldz * 2 : 0);
+  if constexpr (NT1 > 0) {
+#pragma unroll
+    for (int tn = 0; tn < TN1; ++tn)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = (wv & 1) * (NT1 / 2) + tn * 32 + g * 8 + fh * 4;
+        bias1_r[tn][g] = p.bias_t ? *reinterpret_cast<const float4*>(p.bias_t + n)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+  }
+
+  // ---- tail: z = ReLU(y_tile . Wt^T + bt) from the y tile (post residual + act) in Cs
+  auto tail = [&](int m0) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // y tile complete in Cs
+    asm volatile("" ::: "memory");
+    const int wm2 = wv >> 1, wn2 = wv & 1;
+    floatx16 acc2[TN1];
+#pragma unroll
+    for (int tn = 0; tn < TN1; ++tn)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        acc2[tn][4 * g + 0] = bias1_r[tn][g].x;
+        acc2[tn][4 * g + 1] = bias1_r[tn][g].y;
+        acc2[tn][4 * g + 2] = bias1_r[tn][g].z;
+        acc2[tn][4 * g + 3] = bias1_r[tn][g].w;
+      }
+#pragma unroll
+    for (int kk = 0; kk < BN / 16; ++kk) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(Cs + (wm2 * 32 + fr) * CS + kk * 16 + fh * 8);
+      const int kt = kk >> 2, q = (kk & 3) * 2 + fh;
+#pragma unroll
+      for (int tn = 0; tn < TN1; ++tn) {
+        const int row = wn2 * (NT1 / 2) + tn * 32 + fr;
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(
+            W1s + kt * NT1 * BK + row * BK + ((q ^ ((row >> 1) & 7)) << 3));
+        acc2[tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, a, acc2[tn], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave done reading the y tile: reuse Cs for z
+    asm volatile("" ::: "memory");
+    constexpr int CZ = NT1 + 8;
+#pragma unroll
+    for (int tn = 0; tn < TN1; ++tn)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int nl = wn2 * (NT1 / 2) + tn * 32 + g * 8 + fh * 4;
+        bf16x4 o;
+        o[0] = f2bf(fmaxf(acc2[tn][4 * g + 0], 0.f));
+        o[1] = f2bf(fmaxf(acc2[tn][4 * g + 1], 0.f));
+        o[2] = f2bf(fmaxf(acc2[tn][4 * g + 2], 0.f));
+        o[3] = f2bf(fmaxf(acc2[tn][4 * g + 3], 0.f));
+        *reinterpret_cast<bf16x4*>(Cs + (wm2 * 32 + fr) * CZ + nl) = o;
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    constexpr int ZPR = NT1 ? NT1 / 8 : 1;
+#pragma unroll
+    for (int j = 0; j < PERZ; ++j) {
+      const int idx = tid + 256 * j;
+      const int ml = idx / ZPR, ch = idx % ZPR;
+      const int m = m0 + ml;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(Cs + ml * CZ + ch * 8);
+      const int off = m < p.M ? (m * p.ldz + p.z_coff + ch * 8) * 2 : kOOB;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rz, off, 0, SP);
+    }
+  };
+
   // act1/act2 compile-time: instantiated per activation pair by dispatch_act() below
   auto epilogue = [&](int ti, const ResRegs& rres, auto A1, auto A2) __attribute__((always_inline)) {
     constexpr int act1 = decltype(A1)::value, act2 = decltype(A2)::value;
@@ -278,7 +361,9 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams 
       }
       const int off = (m < p.M && n < p.Cout) ? (m * p.ldy + p.y_coff + n) * 2 : kOOB;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ry, off, 0, SP);
+      if constexpr (NT1 > 0) *reinterpret_cast<bf16x8*>(Cs + ml * CS + ch * 8) = v;
     }
+    if constexpr (NT1 > 0) tail(m0);
   };
 
   if (BRES) {  // the weight slice, once: nk x [BN][BK] swizzled blocks
@@ -286,6 +371,18 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams 
 #pragma unroll
       for (int i = 0; i < B_INS; ++i)
         dma16(rw, Bres + kt * BN * BK + (wv * B_INS + i) * 512, b_off[i], kt * BK * 2);
+  }
+  if constexpr (NT1 > 0) {  // tail weights [n_t][Cout = BN], once, swizzled like Bres
+    const __amdgpu_buffer_rsrc_t rw1 = mk_rsrc(p.w_t, p.n_t * p.Cout * 2);
+    constexpr int B1 = NT1 / 32;
+#pragma unroll
+    for (int kt = 0; kt < BN / BK; ++kt)
+#pragma unroll
+      for (int i = 0; i < B1; ++i) {
+        const int row = (wv * B1 + i) * 8 + lrow;
+        const int off = row < p.n_t ? (row * p.Cout + (pch ^ ((row >> 1) & 7)) * 8) * 2 : kOOB;
+        dma16(rw1, W1s + kt * NT1 * BK + (wv * B1 + i) * 512, off, kt * BK * 2);
+      }
   }
   ResRegs rres[D];
   static_for<D - 1>([&](auto S) __attribute__((always_inline)) {
@@ -333,16 +430,33 @@ __global__ __launch_bounds__(256, 2) void conv_stream_kernel(const KvConvParams 
 typedef void (*StreamFn)(const KvConvParams);
 
 template <int BM, int BN, int D, bool BRES, int POL = 0>
-StreamFn stream_get(int mode, bool res) {
+StreamFn stream_get(int mode, bool res, int nt) {
+  if (nt) return nullptr;
   if (mode == 4) return conv_stream_kernel<BM, BN, D, 4, false, BRES, POL>;
   return res ? conv_stream_kernel<BM, BN, D, 1, true, BRES, POL>
              : conv_stream_kernel<BM, BN, D, 1, false, BRES, POL>;
 }
 
+// tail-capable tile: plain BRES tile for nt == 0, fused bottleneck tail for nt = 64 / 128
+// (conv3 + residual -> next conv1, or the fused-downsample dual GEMM -> next conv1)
+template <int BM, int BN, int D>
+StreamFn stream_get_tail(int mode, bool res, int nt) {
+  if (nt == 0) return stream_get<BM, BN, D, true>(mode, res, 0);
+  if constexpr (D == 3) if (nt == 64) {
+    if (mode == 4) return conv_stream_kernel<BM, BN, D, 4, false, true, 0, 64>;
+    return res ? conv_stream_kernel<BM, BN, D, 1, true, true, 0, 64> : nullptr;
+  }
+  if constexpr (D == 2) if (nt == 128) {
+    if (mode == 4) return conv_stream_kernel<BM, BN, D, 4, false, true, 0, 128>;
+    return res ? conv_stream_kernel<BM, BN, D, 1, true, true, 0, 128> : nullptr;
+  }
+  return nullptr;
+}
+
 struct StreamTile {
   int bm, bn, d;
   bool bres;
-  StreamFn (*get)(int, bool);
+  StreamFn (*get)(int, bool, int);
 };
 
 static const StreamTile kStreamTiles[] = {
@@ -361,6 +475,15 @@ static const StreamTile kStreamTiles[] = {
     {64, 128, 3, true, &stream_get<64, 128, 3, true, 2>},
     {64, 64, 4, true, &stream_get<64, 64, 4, true, 2>},
     {128, 128, 3, false, &stream_get<128, 128, 3, false, 2>},
+    // 128x128 with the weight slice resident (stage-3/4 expand: K = 256..512, N = 1024+):
+    // half the A re-reads of BN = 64 across the N slices
+    {128, 128, 3, true, &stream_get<128, 128, 3, true>},
+    {128, 128, 2, true, &stream_get<128, 128, 2, true>},
+    {128, 128, 3, true, &stream_get<128, 128, 3, true, 2>},
+    // 64 x 256 resident slice; also the fused bottleneck-tail tiles (stream_tail_tile):
+    // D = 3 for a 64-channel tail, D = 2 for a 128-channel one (register budget)
+    {64, 256, 3, true, &stream_get_tail<64, 256, 3>},
+    {64, 256, 2, true, &stream_get_tail<64, 256, 2>},
 };
 
 }  // namespace kvedge
@@ -368,6 +491,7 @@ static const StreamTile kStreamTiles[] = {
 namespace kvedge {
 
 int stream_num_tiles() { return (int)(sizeof(kStreamTiles) / sizeof(kStreamTiles[0])); }
+int stream_tail_tile(int n_t) { return stream_num_tiles() - (n_t > 64 ? 1 : 2); }
 
 int stream_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   if (tile < 0 || tile >= stream_num_tiles()) return -6;
@@ -384,7 +508,13 @@ int stream_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   }
   const StreamTile& e = kStreamTiles[tile];
   const bool res = p->res != nullptr;
-  const int lds = stream_lds_bytes(e.bm, e.bn, e.d, res, e.bres, p->Kpad);
+  if (p->n_t) {  // fused tail: the whole y row (all Cout channels) in one workgroup
+    if ((p->n_t != 64 && p->n_t != 128) || e.bn != p->Cout || !p->z || !p->w_t ||
+        p->act_t != 1 || p->ldz % 8 || p->z_coff % 8 || p->ldz < p->z_coff + p->n_t)
+      return -8;
+    if ((long long)p->M * p->ldz * 2 >= kOOB) return -9;
+  }
+  const int lds = stream_lds_bytes(e.bm, e.bn, e.d, res, e.bres, p->Kpad, p->n_t);
   if (lds > kLdsMax) return -11;  // resident weight slice does not fit
   const int nbm = (p->M + e.bm - 1) / e.bm, nbn = (p->Cout + e.bn - 1) / e.bn;
   if (nbm <= 0 || nbn <= 0) return 0;
@@ -398,7 +528,8 @@ int stream_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   int mgroups = (256 * per_cu + nbn - 1) / nbn;  // ~per_cu workgroups on every CU
   if (mgroups > nbm) mgroups = nbm;
   if (mgroups < 1) mgroups = 1;
-  StreamFn fn = e.get(p->mode, res);
+  StreamFn fn = e.get(p->mode, res, p->n_t);
+  if (!fn) return -8;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
     return -7;

@@ -41,6 +41,14 @@ typedef struct KvConvParams {
   // space-to-depth image [N, H, W, 16] (channel (dy*2+dx)*4 + c, channel 3 zero) built on
   // the fly -- the preprocess pass is fused away (v4 direct tile, 2x2 s2d stem only).
   int in_u8;
+  // Fused bottleneck tail (v3 streaming tail tile, BN == Cout): after y is written,
+  // z = ReLU(y . w_t^T + bias_t) -- the NEXT block's 1x1 reduce conv -- is computed from
+  // the y tile still in LDS (w_t: bf16 [n_t][Cout], resident) and written to
+  // z[m * ldz + z_coff + n]: y is never re-read from HBM.  n_t = 0: no tail.
+  const void* w_t;
+  const float* bias_t;
+  void* z;
+  int n_t, ldz, z_coff, act_t;
 } KvConvParams;
 
 // tile: -1 = heuristic; otherwise an index into the tile table (kv_conv_num_tiles()).

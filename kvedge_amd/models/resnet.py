@@ -124,13 +124,35 @@ class DeployedBottleneck:
                 self.dual = DeployedDualConv.from_modules(b.conv3, b.bn3, b.downsample[0],
                                                           b.downsample[1], ACT_RELU, device)
 
-    def __call__(self, x, out=None):
-        y = self.c1(x)
+    def __call__(self, x, out=None, t1=None):
+        """t1: this block's conv1 output when a previous fused tail already computed it."""
+        y = self.c1(x) if t1 is None else t1
         y = self.c2(y)
         if self.dual is not None:
             return self.dual(y, x, out=out)
         idt = x if self.down is None else self.down(x)
         return self.c3(y, res=idt, out=out)
+
+    def can_tail(self, nxt: "DeployedBottleneck") -> bool:
+        """conv3 (or the fused downsample GEMM) + the next block's conv1 as one fused tail:
+        the tail kernel holds a whole y row (Cout = 256) and both weight slices in LDS."""
+        c1 = nxt.c1.spec
+        cout = self.c3.spec.cout
+        k = self.c3.spec.cin + (self.dual.w.shape[1] - self.dual.k1 if self.dual is not None else 0)
+        return (cout == 256 and c1.kh == 1 and c1.stride == 1 and c1.pad == 0 and
+                c1.cin == cout and c1.cout in (64, 128) and c1.act == ACT_RELU and
+                self.c3.spec.act == ACT_RELU and (self.dual is not None or self.down is None) and
+                (self.dual is None or c1.cout == 64) and k <= 128)
+
+    def call_tail(self, x, nxt: "DeployedBottleneck", t1=None):
+        """-> (this block's output y, the next block's conv1 output z) in one fused pass."""
+        y = self.c1(x) if t1 is None else t1
+        y = self.c2(y)
+        c1 = nxt.c1
+        if self.dual is not None:
+            d = self.dual
+            return ops.conv_tail(y, d.w, d.b, d.act, c1.w, c1.b, x2=x, stride2=d.stride2)
+        return ops.conv_tail(y, self.c3.w, self.c3.b, self.c3.spec.act, c1.w, c1.b, res=x)
 
     def out_shape(self, x_shape):
         N, H, W, _ = x_shape
@@ -186,6 +208,9 @@ class KvResNet50:
     microbatch: int = 0          # 0 = off
     microbatch_blocks: int = 3   # bottlenecks (from the start) run per micro-batch
     fuse_stem_pool: bool = True  # stem conv + max pool as one kernel (stem_pool.hip)
+    # conv3 (+ fused downsample) and the NEXT block's conv1 as one kernel wherever the
+    # tail tile fits (layer1 -> layer2 boundary included): y is never re-read from HBM
+    fuse_tail: bool = True
 
     def stem_and_pool(self, x: torch.Tensor) -> torch.Tensor:
         if self.fuse_stem_pool:
@@ -213,8 +238,13 @@ class KvResNet50:
         else:
             x = self.stem_and_pool(x)
             rest = self.blocks
-        for b in rest:
-            x = b(x)
+        t1 = None
+        for i, b in enumerate(rest):
+            nxt = rest[i + 1] if i + 1 < len(rest) else None
+            if self.fuse_tail and x.is_cuda and nxt is not None and b.can_tail(nxt):
+                x, t1 = b.call_tail(x, nxt, t1=t1)
+            else:
+                x, t1 = b(x, t1=t1), None
         return x
 
     def logits(self, x: torch.Tensor) -> torch.Tensor:

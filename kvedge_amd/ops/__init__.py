@@ -230,6 +230,34 @@ def conv_dual(x1: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, bias: Optiona
     return out
 
 
+def conv_tail(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], act: int,
+              w1: torch.Tensor, b1: Optional[torch.Tensor], res: Optional[torch.Tensor] = None,
+              x2: Optional[torch.Tensor] = None, stride2: int = 1,
+              out: Optional[torch.Tensor] = None, z: Optional[torch.Tensor] = None,
+              tile: int = -1):
+    """Fused bottleneck tail: y = act(x . W^T + bias + res) -- or, with ``x2``, the dual
+    conv3 + downsample GEMM of :func:`conv_dual` -- AND z = ReLU(y . w1^T + b1), the next
+    block's 1x1 reduce conv, in one pass: y is written once and never re-read from HBM.
+    w: packed [Cout, K] (1x1); w1: packed [n_t, Cout].  Returns (y, z)."""
+    N, H, W, _ = x.shape
+    cout, nt = w.shape[0], w1.shape[0]
+    if out is None:
+        out = empty(N, H, W, cout, dtype=torch.bfloat16, device=x.device)
+    if z is None:
+        z = empty(N, H, W, nt, dtype=torch.bfloat16, device=x.device)
+    if x.is_cuda:
+        _native().conv_tail(x, x2, w, bias, res, out, w1, b1, z, stride2, act, tile)
+        return out, z
+    if x2 is not None:
+        _ref.conv_dual(x, x2, w, bias, act, stride2, out)
+    else:
+        spec = ConvSpec.auto(x.shape[3], cout, 1, 1, 0, act)
+        _ref.conv2d(x, spec, w, bias, res, out, 0, 0, 0)
+    spec1 = ConvSpec.auto(cout, nt, 1, 1, 0, ACT_RELU)
+    _ref.conv2d(out, spec1, w1, b1, None, z, 0, 0, 0)
+    return out, z
+
+
 def stem_pool(x: torch.Tensor, spec: "ConvSpec", w: torch.Tensor, bias: torch.Tensor,
               out: Optional[torch.Tensor] = None, y_coff: int = 0) -> torch.Tensor:
     """Fused ResNet stem + max pool: maxpool3x3/2(relu(conv_s2d(x) + bias)).

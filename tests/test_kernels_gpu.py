@@ -82,13 +82,15 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale + 0.02
 
 
-N_TILES = 35  # v1 register-staged (0-5) + v2 LDS-DMA (6-21) + v3 streaming (22-33) + v4 direct (34)
+N_TILES = 40  # v1 register-staged (0-5) + v2 LDS-DMA (6-21) + v3 streaming (22-38) + v4 direct (39)
 STREAM0 = 22  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
-DIRECT0 = 34  # v4 direct 3x3 (conv_direct.hip): its instantiation table only
+DIRECT0 = 39  # v4 direct 3x3 (conv_direct.hip): its instantiation table only
 # v3 (bm, bn, ring depth, weight slice resident in LDS) -- conv_stream.hip kStreamTiles
 STREAM_TILES = [(64, 64, 4, True), (64, 128, 4, True), (128, 64, 4, True), (64, 64, 6, True),
                 (64, 128, 3, True), (64, 64, 4, False), (128, 64, 4, False), (128, 128, 3, False),
-                (64, 128, 4, False), (64, 128, 3, True), (64, 64, 4, True), (128, 128, 3, False)]
+                (64, 128, 4, False), (64, 128, 3, True), (64, 64, 4, True), (128, 128, 3, False),
+                (128, 128, 3, True), (128, 128, 2, True), (128, 128, 3, True),
+                (64, 256, 3, True), (64, 256, 2, True)]
 
 
 def _stream_fits(tile, kpad, res):
@@ -259,6 +261,10 @@ def test_conv_dual_fused_downsample(tile, geom):
     w = (torch.randn(cout, K1 + K2, generator=g) * 0.05).to(torch.bfloat16)
     b = torch.randn(cout, generator=g)
     ref = ops.conv_dual(x1, x2, w, b, ops.ACT_RELU, s)
+    if tile >= STREAM0 and not _stream_fits(tile, K1 + K2, False):
+        with pytest.raises(RuntimeError):  # resident weight slice exceeds 160 KiB of LDS
+            ops.conv_dual(x1.cuda(), x2.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, s, tile=tile)
+        return
     got = ops.conv_dual(x1.cuda(), x2.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, s, tile=tile)
     torch.cuda.synchronize()
     err = (got.cpu().float() - ref.float()).abs().max().item()
@@ -383,3 +389,38 @@ def test_stem_pool_fused(shape):
     assert torch.isnan(got[..., :8]).all()
     err = (got[..., 8:] - ref.float()).abs().max().item()
     assert err <= 0.02 * ref.float().abs().max().item() + 0.02, err
+
+
+@pytest.mark.parametrize("case", [
+    # (N, H, W, k1, k2 (0 = plain conv3 + residual), stride2, n_t)
+    (2, 56, 56, 64, 0, 1, 64),     # layer1 conv3 + res -> next conv1 (64)
+    (2, 56, 56, 64, 0, 1, 128),    # layer1 -> layer2 conv1 (128)
+    (3, 13, 11, 64, 0, 1, 64),     # M tail (M % 64 != 0)
+    (2, 28, 28, 64, 64, 1, 64),    # fused downsample dual form (layer1 block 0)
+    (1, 9, 7, 64, 64, 2, 64),      # dual with a strided second source
+])
+def test_conv_tail_fused(case):
+    """v3 fused bottleneck tail: y = ReLU(t . W3 (+ x . Wd) + b (+ res)) and the next
+    block's conv1 z = ReLU(y . W1 + b1) in one kernel, vs the reference composition."""
+    N, H, W, k1, k2, s2, nt = case
+    cout = 256
+    g = torch.Generator().manual_seed(nt + k2 + H)
+    t = _rand((N, H, W, k1), 1)
+    w = (torch.randn(cout, k1 + k2, generator=g) * (2.0 / (k1 + k2)) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(cout, generator=g) * 0.1
+    w1 = (torch.randn(nt, cout, generator=g) * (2.0 / cout) ** 0.5).to(torch.bfloat16)
+    b1 = torch.randn(nt, generator=g) * 0.1
+    if k2:
+        x2 = _rand((N, H * s2, W * s2, k2), 2)
+        y_ref, z_ref = ops.conv_tail(t, w, b, ops.ACT_RELU, w1, b1, x2=x2, stride2=s2)
+        y, z = ops.conv_tail(t.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, w1.cuda(), b1.cuda(),
+                             x2=x2.cuda(), stride2=s2)
+    else:
+        r = _rand((N, H, W, cout), 3)
+        y_ref, z_ref = ops.conv_tail(t, w, b, ops.ACT_RELU, w1, b1, res=r)
+        y, z = ops.conv_tail(t.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, w1.cuda(), b1.cuda(),
+                             res=r.cuda())
+    torch.cuda.synchronize()
+    for got, ref in ((y, y_ref), (z, z_ref)):
+        err = (got.cpu().float() - ref.float()).abs().max().item()
+        assert err <= 0.02 * ref.float().abs().max().item() + 0.02, (case, err)
