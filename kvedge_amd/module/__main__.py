@@ -30,6 +30,9 @@ def main(argv=None):
     ap.add_argument("--image-size", type=int, default=d.image_size)
     ap.add_argument("--fps", type=float, default=d.fps)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--source", default=d.source, choices=["synthetic", "camera"])
+    ap.add_argument("--no-native-loop", action="store_true")
+    ap.add_argument("--steps-per-poll", type=int, default=d.steps_per_poll)
     ap.add_argument("--steps", type=int, default=None, help="stop after N steps")
     ap.add_argument("--duration-s", type=float, default=None)
     ap.add_argument("--state", default=os.environ.get("KVEDGE_STATE", "/var/lib/kvedge/module-state.json"))
@@ -37,7 +40,9 @@ def main(argv=None):
     di = parallel.init_from_env(prefer_gpu=True)
     cfg = ModuleConfig(model=a.model, batch=a.batch, dtype=a.dtype, seed=a.seed,
                        report_interval_s=a.report_interval_s, image_size=a.image_size,
-                       fps=a.fps, use_graph=not a.no_graph, world_size=di.world_size).validate()
+                       fps=a.fps, use_graph=not a.no_graph, world_size=di.world_size,
+                       source=a.source, native_loop=not a.no_native_loop,
+                       steps_per_poll=a.steps_per_poll).validate()
     app = ModuleApp(make_transport(a.transport), cfg, state_path=a.state)
     stop = {"flag": False}
     signal.signal(signal.SIGTERM, lambda *_: stop.update(flag=True))

@@ -50,6 +50,43 @@ class _SimTempModel:
                 "timeCreated": now_iso()}
 
 
+class _CameraSource:
+    """Host frame producer for source="camera": cycles a few pre-rendered uint8 batches
+    into a pinned FrameRing (drop-oldest when paced and the GPU falls behind), at ``fps``
+    frames/s (0 = as fast as the ring drains).  Stands in for a camera / RTSP decoder
+    thread; the hand-off path (pinned ring -> DMA in the native serve loop) is the
+    production one."""
+
+    def __init__(self, ring, batch: int, hw: int, fps: float, seed: int):
+        import threading
+
+        g = torch.Generator().manual_seed(seed)
+        self.frames = [torch.randint(0, 256, (batch, hw, hw, 3), dtype=torch.uint8, generator=g)
+                       for _ in range(3)]
+        self.ring, self.batch, self.fps = ring, batch, fps
+        self.seq = 0
+        self._stop = threading.Event()
+        self.thread = threading.Thread(target=self._run, name="kvedge-camera", daemon=True)
+        self.thread.start()
+
+    def _run(self):
+        period = self.batch / self.fps if self.fps > 0 else 0.0
+        nxt = time.perf_counter()
+        while not self._stop.is_set():
+            if not self.ring.put(self.frames[self.seq % len(self.frames)], self.seq,
+                                 timeout_ms=100, drop_oldest=period > 0):
+                continue
+            self.seq += 1
+            if period:
+                nxt += period
+                time.sleep(max(0.0, nxt - time.perf_counter()))
+
+    def stop(self):
+        self._stop.set()
+        self.ring.close()
+        self.thread.join(timeout=5)
+
+
 class ModuleApp:
     def __init__(self, transport: Transport, config: Optional[ModuleConfig] = None,
                  device: Optional[str] = None, state_path: Optional[str] = None,
@@ -61,6 +98,8 @@ class ModuleApp:
         self.clock = clock
         self.engine = None
         self.model = None
+        self.ring = None
+        self.camera: Optional[_CameraSource] = None
         self.sim: Optional[_SimTempModel] = None
         self.state = {"total_images": 0, "total_steps": 0, "restarts": 0, "rebuilds": 0,
                       "rejected_patches": 0, "messages": 0}
@@ -98,8 +137,15 @@ class ModuleApp:
         return self
 
     def stop(self):
+        self._stop_camera()
         self._save_state()
         self.tr.disconnect()
+
+    def _stop_camera(self):
+        if self.camera is not None:
+            self.camera.stop()
+        self.camera = None
+        self.ring = None
 
     def _load_state(self):
         if self.state_path and os.path.exists(self.state_path):
@@ -123,6 +169,7 @@ class ModuleApp:
 
     def _build(self):
         cfg = self.cfg
+        self._stop_camera()
         self.engine = None
         self.model = None
         self.sim = None
@@ -144,9 +191,17 @@ class ModuleApp:
                                    conf=cfg.conf, iou=cfg.iou, max_det=cfg.max_det)
         if self.world > 1:
             parallel.broadcast_tensors(parallel.model_tensors(self.model), src=0)
+        camera = cfg.source == "camera"
         self.engine = InferenceEngine(self.model, cfg.batch, cfg.resolved_image_size(), device=dev,
-                                      seed=cfg.seed + self.rank, use_graph=cfg.use_graph)
+                                      seed=cfg.seed + self.rank, use_graph=cfg.use_graph,
+                                      synthetic=not camera)
         self.engine.prepare(warmup=1, autotune=dev.type == "cuda")
+        if camera:
+            from ..runtime import FrameRing
+
+            self.ring = FrameRing(3, self.engine.frames.numel())
+            self.camera = _CameraSource(self.ring, cfg.batch, cfg.resolved_image_size(), cfg.fps,
+                                        cfg.seed + self.rank)
 
     def _report_config(self):
         self.tr.patch_reported({"config": self.cfg.to_dict(), "status": "running",
@@ -159,19 +214,35 @@ class ModuleApp:
         if self.sim is not None:
             self._sim_step()
             return
+        native = (self.cfg.native_loop and self.engine.graph is not None and
+                  self._hist is not None)
         t0 = self.clock()
-        self.engine.run()
-        if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
-        dt = self.clock() - t0
-        if self._hist is not None:
-            self._hist.add_ms(dt * 1e3)
+        if native:
+            # C++ serve loop: per-step device time straight into the histogram; with a
+            # camera source each replay first DMAs one pinned batch from the ring
+            r = self.engine.serve_native(self.cfg.steps_per_poll, depth=2, hist=self._hist,
+                                         ring=self.ring, ring_timeout_ms=1000)
+            nsteps = r.steps
         else:
-            self._lat_ms.append(dt * 1e3)
-        self._win_imgs += self.cfg.batch
-        self.state["total_images"] += self.cfg.batch
-        self.state["total_steps"] += 1
-        if self.cfg.fps > 0:
+            if self.ring is not None:  # host path: take one ring batch, feed it, release
+                slot, _ = self.ring.acquire_read(1000)
+                if slot >= 0:
+                    self.engine.frames.copy_(self.ring.slot(slot).view(self.engine.frames.shape))
+                    self.ring.release(slot)
+            self.engine.run()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            nsteps = 1
+        dt = self.clock() - t0
+        if not native:
+            if self._hist is not None:
+                self._hist.add_ms(dt * 1e3)
+            else:
+                self._lat_ms.append(dt * 1e3)
+        self._win_imgs += self.cfg.batch * nsteps
+        self.state["total_images"] += self.cfg.batch * nsteps
+        self.state["total_steps"] += nsteps
+        if self.cfg.fps > 0 and self.ring is None:
             budget = self.cfg.batch / self.cfg.fps
             if dt < budget:
                 time.sleep(budget - dt)
@@ -223,7 +294,10 @@ class ModuleApp:
                "images_per_s_rank": round(s["images_per_s"], 2),
                "latency_ms": {"p50": round(s["p50_ms"], 3), "p99": round(lat_max, 3)},
                "total_images": self.state["total_images"], "rank": self.rank,
-               "world_size": self.world, "heartbeat": self.state["total_steps"]}
+               "world_size": self.world, "heartbeat": self.state["total_steps"],
+               "source": self.cfg.source}
+        if self.ring is not None:
+            msg["frames_dropped"] = self.ring.dropped
         msg.update(self._outputs_summary())
         if self.rank == 0:
             self.tr.send_message("telemetry", msg)

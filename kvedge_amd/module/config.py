@@ -12,6 +12,7 @@ from dataclasses import asdict, dataclass, fields, replace
 from typing import Any, Dict
 
 MODELS = ("resnet50", "yolov8n", "simulated-temperature")
+SOURCES = ("synthetic", "camera")
 DTYPES = ("bf16",)
 
 
@@ -29,13 +30,18 @@ class ModuleConfig:
     max_det: int = 300
     fps: float = 0.0             # 0 = run flat out; > 0 throttles batches/s*batch
     use_graph: bool = True
+    # frame source: "synthetic" = on-device generator inside the graph; "camera" = a host
+    # producer thread feeding a pinned FrameRing that the native serve loop DMAs from
+    source: str = "synthetic"
+    native_loop: bool = True     # GPU: replay the graph from the C++ serve loop
+    steps_per_poll: int = 1      # graph replays per module step (native loop)
     # SimulatedTemperatureSensor compatibility (BASELINE config 1, CPU-only plumbing)
     send_interval_s: float = 5.0
     max_messages: int = 500
 
     # keys that force an engine rebuild when they change
     REBUILD = ("model", "batch", "dtype", "seed", "image_size", "conf", "iou", "max_det",
-               "use_graph")
+               "use_graph", "source")
 
     def validate(self) -> "ModuleConfig":
         if self.model not in MODELS:
@@ -54,6 +60,10 @@ class ModuleConfig:
             raise ValueError("conf/iou must be in [0, 1]")
         if not 1 <= self.max_det <= 300:
             raise ValueError("max_det must be 1..300")
+        if self.source not in SOURCES:
+            raise ValueError(f"source must be one of {SOURCES}, got {self.source!r}")
+        if not 1 <= self.steps_per_poll <= 1000:
+            raise ValueError("steps_per_poll must be 1..1000")
         return self
 
     def apply_patch(self, patch: Dict[str, Any]) -> "ModuleConfig":

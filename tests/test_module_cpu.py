@@ -91,3 +91,26 @@ def test_stdout_transport(capsys):
     lines = [json.loads(l) for l in capsys.readouterr().out.strip().splitlines()]
     assert any("reported" in l for l in lines)
     assert any(l.get("output") == "temperatureOutput" for l in lines)
+
+
+def test_camera_source_ring_feeds_engine(tmp_path):
+    """source="camera": a host producer thread fills the pinned FrameRing and every module
+    step consumes one batch from it (CPU: host copy path; GPU: the native serve loop)."""
+    from kvedge_amd import ops
+
+    if not ops.load():
+        import pytest
+
+        pytest.skip("native runtime not built")
+    tr = FakeTransport({"model": "resnet50", "batch": 1, "report_interval_s": 1.0,
+                        "image_size": 64, "source": "camera"})
+    app = ModuleApp(tr, device="cpu", clock=Clock()).start()
+    assert app.ring is not None and app.camera is not None and not app.engine.synthetic
+    app.run(max_steps=4)
+    tel = tr.outputs("telemetry")
+    assert tel and tel[-1]["source"] == "camera" and "frames_dropped" in tel[-1]
+    assert app.state["total_images"] == 4 and app.camera.seq >= 4
+    tr.push_twin_patch({"source": "synthetic"})  # rebuild key: camera thread stopped
+    app.run(max_steps=1)
+    assert app.ring is None and app.camera is None and app.engine.synthetic
+    app.stop()

@@ -77,3 +77,24 @@ def test_ring_fed_serving_equals_set_frames(kv):
     torch.cuda.synchronize()
     assert torch.allclose(probs_ring, out[0], atol=1e-3)
     ring.close()
+
+
+@pytest.mark.parametrize("source", ["camera", "synthetic"])
+def test_module_native_serving(source):
+    """The edge module on the GPU: native serve loop (4 graph replays per poll), fed by the
+    camera thread through the pinned ring or by the on-device generator."""
+    from kvedge_amd.module.app import ModuleApp
+    from kvedge_amd.module.transport import FakeTransport
+
+    tr = FakeTransport({"model": "resnet50", "batch": 8, "report_interval_s": 0.01,
+                        "source": source, "steps_per_poll": 4})
+    app = ModuleApp(tr, device="cuda").start()
+    assert app.engine.graph is not None
+    app.run(max_steps=3)
+    app.report()
+    t = tr.outputs("telemetry")[-1]
+    assert t["source"] == source and t["images_per_s"] > 0
+    assert app.state["total_images"] == 3 * 4 * 8
+    if source == "camera":
+        assert app.ring.pinned and app.camera.seq >= 12
+    app.stop()
