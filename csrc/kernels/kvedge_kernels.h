@@ -62,6 +62,9 @@ int kv_conv_pick_tile(const KvConvParams* p);
 int kv_stem_pool(const void* x, const void* w, const float* bias, void* y, int N, int H, int W,
                  int ldy, int y_coff, hipStream_t s);
 int kv_stem_pool_lds_bytes(int W);
+int kv_stem_pool_frames(const void* frames, const void* w, const float* bias, void* y, int N,
+                        int H0, int W0, const float* mean3, const float* inv_std3, int ldy,
+                        int y_coff, hipStream_t s);
 
 int kv_maxpool2d(const void* x, void* y, int N, int H, int W, int C, int ldx, int x_coff,
                  int ldy, int y_coff, int k, int stride, int pad, int Ho, int Wo, hipStream_t s);

@@ -65,10 +65,21 @@ __device__ __forceinline__ unsigned pk_max_u16(unsigned a, unsigned b) {
   return __builtin_bit_cast(unsigned, r);
 }
 
-template <int NT>  // threads per workgroup: 256 (1 wave/SIMD) or 512 (2 waves/SIMD)
+// frames-in mode: per-channel normalisation of raw bytes, v = byte * a[c] + b[c]
+struct StemNorm {
+  float a[3], b[3];
+};
+
+// U8 = false: x is the bf16 s2d image [N,H,W,16] (ops.preprocess(s2d=True)).
+// U8 = true : x is the raw uint8 frame [N,2H,2W,3]; the patch fetch reads 12 contiguous
+//             bytes (two s2d pixels of one source row, 4-B aligned: one buffer_load_dwordx3)
+//             and normalises + space-to-depths them in registers at commit time, so the
+//             preprocess kernel and its 32 B/px bf16 image disappear from the step.
+template <int NT, bool U8>  // threads per workgroup: 256 (1 wave/SIMD) or 512 (2 waves/SIMD)
 __global__ __launch_bounds__(NT, 1) void stem_pool_kernel(
-    const bf16* __restrict__ x, const bf16* __restrict__ w, const float* __restrict__ bias,
-    bf16* __restrict__ y, int N, int H, int W, int Hp, int Wp, int ldy, int y_coff) {
+    const void* __restrict__ xv, const bf16* __restrict__ w, const float* __restrict__ bias,
+    bf16* __restrict__ y, int N, int H, int W, int Hp, int Wp, int ldy, int y_coff,
+    StemNorm nrm) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   constexpr int kPatchBytes = kPR * kPW * kPB;
   unsigned char* patch = lds;                                // kPR x kPW pixels
@@ -102,31 +113,74 @@ __global__ __launch_bounds__(NT, 1) void stem_pool_kernel(
   constexpr int kChunks = kPR * kPW * 2;
   constexpr int kPre = kChunks / NT;
   static_assert(kChunks % NT == 0, "patch chunks per thread");
-  uint4 pre[kPre];
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16*>(x), (short)0, N * H * W * kCin * 2, 0x00020000);
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+  constexpr int kPreU = U8 ? kPre / 2 : 1;
+  uint4 pre[U8 ? 1 : kPre];
+  u32x3 preu[kPreU];  // U8: 12 raw bytes = s2d pixels (p, p+1), one source row h
+  unsigned okm = 0;   // U8: bit i = pair i inside the image (padding must be 0, not -mean)
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(xv), (short)0, U8 ? N * H * W * 12 : N * H * W * kCin * 2, 0x00020000);
   auto fetch = [&](int item) __attribute__((always_inline)) {
     const int n = item / nbands, band = item - n * nbands;
     const int iy0 = 2 * band * kRB - 3;
     const bool live = item < total;
+    if constexpr (U8) {
+      okm = 0;
 #pragma unroll
-    for (int i = 0; i < kPre; ++i) {
-      const int q = tid + NT * i;
-      const int p = q >> 1, h = q & 1;
-      const int pr = p / kPW, pc = p % kPW;
-      const int iy = iy0 + pr, ix = pc - 2;
-      const bool ok = live && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
-      const int off = ok ? (((n * H + iy) * W + ix) * kCin + h * 8) * 2 : 0x7ffffff0;
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
-      pre[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      for (int i = 0; i < kPreU; ++i) {
+        const int q = tid + NT * i;          // pair index: (pixel pair, source row h)
+        const int p = (q >> 1) * 2, h = q & 1;
+        const int pr = p / kPW, pc = p % kPW;
+        const int iy = iy0 + pr, ix = pc - 2;  // ix even, W even: both pixels in or out
+        const bool ok = live && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        const int off = ok ? ((n * 2 * H + 2 * iy + h) * 2 * W + 2 * ix) * 3 : 0x7ffffff0;
+        preu[i] = __builtin_amdgcn_raw_buffer_load_b96(rx, off, 0, 0);
+        okm |= ok ? 1u << i : 0u;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kPre; ++i) {
+        const int q = tid + NT * i;
+        const int p = q >> 1, h = q & 1;
+        const int pr = p / kPW, pc = p % kPW;
+        const int iy = iy0 + pr, ix = pc - 2;
+        const bool ok = live && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        const int off = ok ? (((n * H + iy) * W + ix) * kCin + h * 8) * 2 : 0x7ffffff0;
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+        pre[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
     }
   };
-  auto commit = [&]() __attribute__((always_inline)) {
+  // U8: 6 bytes (2 source pixels x rgb) -> one 16-B s2d chunk [r g b 0 r g b 0] in bf16
+  auto norm_chunk = [&](unsigned lo, unsigned hi, int sh, bool ok) __attribute__((always_inline)) {
+    // bytes sh..sh+5 of the 8-byte word (lo | hi << 32), sh in {0, 2}
+    const unsigned long long v = ((unsigned long long)hi << 32 | lo) >> (8 * sh);
+    float f[6];
 #pragma unroll
-    for (int i = 0; i < kPre; ++i) {
-      const int q = tid + NT * i;
-      *reinterpret_cast<uint4*>(patch + patch_off(q >> 1, q & 1)) = pre[i];
+    for (int j = 0; j < 6; ++j)
+      f[j] = ok ? (float)((unsigned)(v >> (8 * j)) & 0xffu) * nrm.a[j % 3] + nrm.b[j % 3] : 0.f;
+    bf16x8 o;
+    o[0] = f2bf(f[0]); o[1] = f2bf(f[1]); o[2] = f2bf(f[2]); o[3] = f2bf(0.f);
+    o[4] = f2bf(f[3]); o[5] = f2bf(f[4]); o[6] = f2bf(f[5]); o[7] = f2bf(0.f);
+    return __builtin_bit_cast(uint4, o);
+  };
+  auto commit = [&]() __attribute__((always_inline)) {
+    if constexpr (U8) {
+#pragma unroll
+      for (int i = 0; i < kPreU; ++i) {
+        const int q = tid + NT * i;
+        const int p = (q >> 1) * 2, h = q & 1;
+        const bool ok = (okm >> i) & 1u;
+        *reinterpret_cast<uint4*>(patch + patch_off(p, h)) = norm_chunk(preu[i][0], preu[i][1], 0, ok);
+        *reinterpret_cast<uint4*>(patch + patch_off(p + 1, h)) = norm_chunk(preu[i][1], preu[i][2], 2, ok);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kPre; ++i) {
+        const int q = tid + NT * i;
+        *reinterpret_cast<uint4*>(patch + patch_off(q >> 1, q & 1)) = pre[i];
+      }
     }
   };
 
@@ -234,13 +288,16 @@ using namespace kvedge;
 
 extern "C" int kv_stem_pool_lds_bytes(int W) { return kPR * kPW * kPB + kSR * W * kTS * 2; }
 
-extern "C" int kv_stem_pool(const void* x, const void* w, const float* bias, void* y, int N, int H,
-                            int W, int ldy, int y_coff, hipStream_t s) {
+namespace {
+template <bool U8>
+int stem_launch(const void* x, const void* w, const float* bias, void* y, int N, int H, int W,
+                int ldy, int y_coff, const StemNorm& nrm, hipStream_t s) {
   if (N <= 0) return 0;
   if (H <= 0 || W <= 0 || ldy % 8 || y_coff % 8 || ldy < y_coff + kCo || !bias) return -1;
   const int lds = kv_stem_pool_lds_bytes(W);
   if (lds > 160 * 1024 || W + 3 > kPW) return -2;                // patch row pitch: W <= 125
   if ((long long)N * H * W * 16 * 2 >= 0x7ffffff0LL) return -4;   // buffer range (2 GiB)
+  if (U8 && W % 2) return -5;                                     // pixel-pair fetch
   const int Hp = (H - 1) / 2 + 1, Wp = (W - 1) / 2 + 1;  // 3x3 / 2, pad 1
   const long long items = (long long)N * ((Hp + kRB - 1) / kRB);
   int dev = 0, ncu = 256;
@@ -252,15 +309,34 @@ extern "C" int kv_stem_pool(const void* x, const void* w, const float* bias, voi
     const char* e = getenv("KVEDGE_STEM_THREADS");
     return (e && atoi(e) == 256) ? 256 : 512;
   }();
-  const void* fn = nt == 256 ? reinterpret_cast<const void*>(stem_pool_kernel<256>)
-                             : reinterpret_cast<const void*>(stem_pool_kernel<512>);
+  const void* fn = nt == 256 ? reinterpret_cast<const void*>(stem_pool_kernel<256, U8>)
+                             : reinterpret_cast<const void*>(stem_pool_kernel<512, U8>);
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
     return -3;
   if (nt == 256)
-    hipLaunchKernelGGL(stem_pool_kernel<256>, dim3((unsigned)g), dim3(256), (unsigned)lds, s,
-                       (const bf16*)x, (const bf16*)w, bias, (bf16*)y, N, H, W, Hp, Wp, ldy, y_coff);
+    hipLaunchKernelGGL((stem_pool_kernel<256, U8>), dim3((unsigned)g), dim3(256), (unsigned)lds, s,
+                       x, (const bf16*)w, bias, (bf16*)y, N, H, W, Hp, Wp, ldy, y_coff, nrm);
   else
-    hipLaunchKernelGGL(stem_pool_kernel<512>, dim3((unsigned)g), dim3(512), (unsigned)lds, s,
-                       (const bf16*)x, (const bf16*)w, bias, (bf16*)y, N, H, W, Hp, Wp, ldy, y_coff);
+    hipLaunchKernelGGL((stem_pool_kernel<512, U8>), dim3((unsigned)g), dim3(512), (unsigned)lds, s,
+                       x, (const bf16*)w, bias, (bf16*)y, N, H, W, Hp, Wp, ldy, y_coff, nrm);
   return hipGetLastError() == hipSuccess ? 0 : -100;
+}
+}  // namespace
+
+extern "C" int kv_stem_pool(const void* x, const void* w, const float* bias, void* y, int N, int H,
+                            int W, int ldy, int y_coff, hipStream_t s) {
+  return stem_launch<false>(x, w, bias, y, N, H, W, ldy, y_coff, StemNorm{}, s);
+}
+
+// frames: uint8 [N, H0, W0, 3] (H0, W0 even); v = (byte/255 - mean) * inv_std per channel
+extern "C" int kv_stem_pool_frames(const void* frames, const void* w, const float* bias, void* y,
+                                   int N, int H0, int W0, const float* mean3,
+                                   const float* inv_std3, int ldy, int y_coff, hipStream_t s) {
+  if (H0 % 2 || W0 % 2) return -5;
+  StemNorm nrm;
+  for (int c = 0; c < 3; ++c) {
+    nrm.a[c] = inv_std3[c] / 255.f;
+    nrm.b[c] = -mean3[c] * inv_std3[c];
+  }
+  return stem_launch<true>(frames, w, bias, y, N, H0 / 2, W0 / 2, ldy, y_coff, nrm, s);
 }

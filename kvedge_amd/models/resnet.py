@@ -6,9 +6,11 @@ random-init with a fixed seed (no checkpoints / no network), optionally with BN
 statistics calibrated on synthetic frames so activations stay well scaled.
 
 Deployed forward (all HIP kernels on GPU):
-  frames u8 NHWC3 -> K12 preprocess (bf16 NHWC4) -> K2 stem 7x7/2 (+BN+ReLU fused)
-  -> K5 maxpool 3x3/2 -> 16 bottlenecks of K3/K2 convs with bias+residual+ReLU
-  fused into the conv epilogue -> K6 global avgpool -> K1 FC GEMM -> K7 softmax+argmax.
+  frames u8 NHWC3 -> ONE stem kernel (normalise + space-to-depth in its fetch, 7x7/2 conv
+  as a 4x4 s2d conv with BN+ReLU, 3x3/2 max pool; stem_pool.hip) -> 16 bottlenecks of
+  direct / streaming implicit-GEMM convs with bias+residual+ReLU in the epilogue (conv3 and
+  the next block's conv1 fused where they fit) -> K6 global avgpool -> K1 FC GEMM ->
+  K7 softmax+argmax.
 """
 from __future__ import annotations
 
@@ -208,24 +210,29 @@ class KvResNet50:
     microbatch: int = 0          # 0 = off
     microbatch_blocks: int = 3   # bottlenecks (from the start) run per micro-batch
     fuse_stem_pool: bool = True  # stem conv + max pool as one kernel (stem_pool.hip)
+    # GPU: raw frames straight into the stem kernel (preprocess fused into its fetch)
+    fuse_preprocess: bool = True
     # conv3 (+ fused downsample) and the NEXT block's conv1 as one kernel wherever the
     # tail tile fits (layer1 -> layer2 boundary included): y is never re-read from HBM
     fuse_tail: bool = True
 
-    def stem_and_pool(self, x: torch.Tensor) -> torch.Tensor:
+    def stem_and_pool(self, x: torch.Tensor, frames_in: bool = False) -> torch.Tensor:
+        if frames_in:
+            return ops.stem_pool_frames(x, self.stem.spec, self.stem.w, self.stem.b)
         if self.fuse_stem_pool:
             return ops.stem_pool(x, self.stem.spec, self.stem.w, self.stem.b)
         return ops.maxpool2d(self.stem(x), 3, 2, 1)
 
-    def features(self, x: torch.Tensor) -> torch.Tensor:
-        """x: preprocessed bf16 s2d [B,112,112,16] -> final feature map [B,7,7,2048] bf16."""
+    def features(self, x: torch.Tensor, frames_in: bool = False) -> torch.Tensor:
+        """x: preprocessed bf16 s2d [B,112,112,16] (or, with ``frames_in``, the raw uint8
+        frames [B,224,224,3]) -> final feature map [B,7,7,2048] bf16."""
         B = x.shape[0]
         mb = self.microbatch
         nb = self.microbatch_blocks
         if mb and B > mb and B % mb == 0 and nb > 0:
             full = None
             for i in range(0, B, mb):
-                y = self.stem_and_pool(x[i:i + mb])
+                y = self.stem_and_pool(x[i:i + mb], frames_in)
                 for b in self.blocks[:nb - 1]:
                     y = b(y)
                 last = self.blocks[nb - 1]
@@ -236,7 +243,7 @@ class KvResNet50:
             x = full
             rest = self.blocks[nb:]
         else:
-            x = self.stem_and_pool(x)
+            x = self.stem_and_pool(x, frames_in)
             rest = self.blocks
         t1 = None
         for i, b in enumerate(rest):
@@ -247,14 +254,16 @@ class KvResNet50:
                 x, t1 = b(x, t1=t1), None
         return x
 
-    def logits(self, x: torch.Tensor) -> torch.Tensor:
-        f = self.features(x)
+    def logits(self, x: torch.Tensor, frames_in: bool = False) -> torch.Tensor:
+        f = self.features(x, frames_in)
         B = f.shape[0]
         pooled = ops.global_avgpool(f).view(B, 1, 1, 2048)
         return self.fc(pooled).view(B, self.num_classes)
 
     def __call__(self, frames_u8: torch.Tensor, out: Optional[dict] = None):
-        x = self.preprocess(frames_u8)
-        lg = self.logits(x)
+        if self.fuse_preprocess and self.fuse_stem_pool and frames_u8.is_cuda:
+            lg = self.logits(frames_u8, frames_in=True)
+        else:
+            lg = self.logits(self.preprocess(frames_u8))
         probs, top1 = ops.softmax_rows(lg)
         return probs, top1

@@ -280,6 +280,32 @@ def stem_pool(x: torch.Tensor, spec: "ConvSpec", w: torch.Tensor, bias: torch.Te
     return out
 
 
+def stem_pool_frames(frames: torch.Tensor, spec: "ConvSpec", w: torch.Tensor,
+                     bias: torch.Tensor, out: Optional[torch.Tensor] = None, y_coff: int = 0,
+                     mean=None, std=None) -> torch.Tensor:
+    """Frames-in ResNet stem + pool: preprocess(s2d) fused into :func:`stem_pool`.
+
+    frames: uint8 [N, H, W, 3] (H even, W % 4 == 0) -> [N, H/4, W/4, 64] (224 -> 56).
+    GPU: stem_pool.hip's U8 instantiation -- the patch fetch reads the raw bytes (one
+    12-B load per two s2d pixels), normalises and space-to-depths them in registers; the
+    bf16 s2d image (32 B/px) is never written.  CPU: the reference preprocess + stem_pool."""
+    assert frames.dtype == torch.uint8 and frames.dim() == 4 and frames.shape[3] == 3
+    mean = IMAGENET_MEAN if mean is None else mean
+    std = IMAGENET_STD if std is None else std
+    if not frames.is_cuda:
+        return stem_pool(preprocess(frames, mean=mean, std=std, s2d=True), spec, w, bias,
+                         out=out, y_coff=y_coff)
+    assert spec.cin == 16 and spec.cout == 64 and spec.kh == 4 and spec.stride == 1
+    assert spec.pad == 2 and spec.pad_end == 1 and spec.act == ACT_RELU and spec.Kpad == 256
+    N, H0, W0, _ = frames.shape
+    H, W = H0 // 2, W0 // 2
+    if out is None:
+        out = empty(N, (H - 1) // 2 + 1, (W - 1) // 2 + 1, 64, dtype=torch.bfloat16,
+                    device=frames.device)
+    _native().stem_pool_frames(frames, w, bias, out, list(mean), list(std), y_coff)
+    return out
+
+
 def stem_from_frames(frames: torch.Tensor, spec: "ConvSpec", w: torch.Tensor,
                      bias: Optional[torch.Tensor], out: Optional[torch.Tensor] = None,
                      tile: int = -1) -> torch.Tensor:

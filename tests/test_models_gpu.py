@@ -122,3 +122,35 @@ def test_yolov8n_fused_stem_parity(yolo):
         cos = torch.nn.functional.cosine_similarity(g.float().cpu().flatten(), c.float().flatten(),
                                                     dim=0)
         assert cos > 0.999, float(cos)
+
+
+@pytest.mark.parametrize("hw", [(224, 224), (64, 96), (36, 20)])
+def test_stem_pool_frames_kernel(resnet, hw):
+    """Frames-in ResNet stem + pool (preprocess fused into the fetch) vs the CPU reference
+    preprocess -> s2d stem -> pool; borders (padding must be 0, not -mean/std) included."""
+    _, kv, kv_cpu = resnet
+    fr = torch.randint(0, 256, (5, hw[0], hw[1], 3), dtype=torch.uint8,
+                       generator=torch.Generator().manual_seed(11))
+    s = kv_cpu.stem
+    ref = ops.stem_pool_frames(fr, s.spec, s.w, s.b).float()
+    got = ops.stem_pool_frames(fr.cuda(), kv.stem.spec, kv.stem.w, kv.stem.b)
+    two = ops.stem_pool(ops.preprocess(fr.cuda(), s2d=True), kv.stem.spec, kv.stem.w, kv.stem.b)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape
+    err = (got.cpu().float() - ref).abs().max().item()
+    assert err <= 0.02 * ref.abs().max().item() + 0.02, err
+    err2 = (got.float() - two.float()).abs().max().item()
+    assert err2 <= 0.01 * ref.abs().max().item() + 0.01, err2
+
+
+def test_resnet50_frames_in_parity(resnet):
+    """The default GPU forward (frames straight into the stem kernel) equals the
+    explicit preprocess path."""
+    _, kv, _ = resnet
+    fr = _frames(4, 3).cuda()
+    with torch.no_grad():
+        p_fused, t_fused = kv(fr)
+        lg_two = kv.logits(kv.preprocess(fr))
+        p_two, _ = ops.softmax_rows(lg_two)
+    torch.cuda.synchronize()
+    assert torch.allclose(p_fused.float(), p_two.float(), atol=2e-3)

@@ -21,18 +21,22 @@ def main():
     m = KvResNet50.build(seed=0, device="cuda", calibrate=False)
     fr = torch.randint(0, 256, (a.batch, 224, 224, 3), dtype=torch.uint8, device="cuda")
     x = m.preprocess(fr)
-    out = m.stem_and_pool(x)
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(a.reps):
-        m.stem_and_pool(x)
-    e.record()
-    torch.cuda.synchronize()
-    us = s.elapsed_time(e) / a.reps * 1e3
     flops = 2 * a.batch * 112 * 112 * 64 * 147
-    print(f"stem_pool threads={os.environ.get('KVEDGE_STEM_THREADS', 'default')} batch={a.batch}: "
-          f"{us:.1f} us  ({flops / us / 1e6:.0f} TF/s model-FLOP)  checksum={float(out.float().sum()):.6g}")
+    for name, fn in (("preprocess+stem_pool", lambda: m.stem_and_pool(m.preprocess(fr))),
+                     ("stem_pool", lambda: m.stem_and_pool(x)),
+                     ("stem_pool_frames", lambda: m.stem_and_pool(fr, frames_in=True))):
+        out = fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) / a.reps * 1e3
+        print(f"{name} threads={os.environ.get('KVEDGE_STEM_THREADS', 'default')} "
+              f"batch={a.batch}: {us:.1f} us  ({flops / us / 1e6:.0f} TF/s model-FLOP)  "
+              f"checksum={float(out.float().sum()):.6g}")
 
 
 if __name__ == "__main__":
