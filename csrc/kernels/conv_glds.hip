@@ -53,14 +53,27 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N < 63 ? N : 63) : "memory");
 }
 
-template <int BM, int BN, int WM, int WN, int MODE, int D>
+// BKT = K elements per ring stage.  64: 128-B rows, 8 rows per DMA instruction.  32: 64-B
+// rows, 16 rows per instruction -- half the bytes per stage, so twice the stages fit the
+// same LDS (a 128x128 tile can keep 4 K steps in flight at 2 workgroups per CU, D = 5).
+template <int BM, int BN, int WM, int WN, int MODE, int D, int BKT = 64>
 __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p) {
+  constexpr int BK = BKT;         // shadows the file-scope 64
+  constexpr int CH = BK / 8;      // 16-B chunks per LDS row
+  constexpr int RPI = 64 / CH;    // rows per DMA instruction (64 lanes x 16 B)
+  constexpr int KS = BK / 16;     // MFMA K steps per stage
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
-  constexpr int A_INS = BM / 32;  // DMA instructions per wave per stage (8 rows each)
-  constexpr int B_INS = BN / 32;
+  constexpr int A_INS = BM / (4 * RPI);  // DMA instructions per wave per stage
+  constexpr int B_INS = BN / (4 * RPI);
   constexpr int STAGE = (BM + BN) * BK;
-  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1 && D >= 2 && D <= 4, "tile");
+  static_assert(BK == 64 || BK == 32, "BK");
+  static_assert(A_INS >= 1 && B_INS >= 1, "tile too small for BK");
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1 && D >= 2 && D <= 6, "tile");
+  // chunk swizzle of row r: ds_read_b128 of 16 rows x one logical chunk is conflict-free
+  auto sw = [](int r) __attribute__((always_inline)) {
+    return BK == 64 ? ((r >> 1) & 7) : ((r >> 2) & 3);
+  };
   __shared__ __attribute__((aligned(16))) bf16 smem[D * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -93,7 +106,7 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
   }
 
   // ---- per-lane source descriptors (constant over the K loop) -------------
-  const int lrow = lane >> 3, pch = lane & 7;
+  const int lrow = lane / CH, pch = lane % CH;
   int a_off[A_INS];   // MODE 0: pixel-row base offset (elements); MODE 1/4: full byte offset
   int a_off2[A_INS];  // MODE 4: byte offset of the strided second source
   unsigned a_msk[A_INS];
@@ -102,8 +115,8 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
   const int HoWo = p.Ho * p.Wo;
 #pragma unroll
   for (int i = 0; i < A_INS; ++i) {
-    const int row = (wv * A_INS + i) * 8 + lrow;
-    const int lc = pch ^ ((row >> 1) & 7);
+    const int row = (wv * A_INS + i) * RPI + lrow;
+    const int lc = pch ^ sw(row);
     a_lc[i] = lc;
     const int m = m0 + row;
     a_msk[i] = 0u;
@@ -142,8 +155,8 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
   int b_off[B_INS];
 #pragma unroll
   for (int i = 0; i < B_INS; ++i) {
-    const int row = (wv * B_INS + i) * 8 + lrow;
-    const int lc = pch ^ ((row >> 1) & 7);
+    const int row = (wv * B_INS + i) * RPI + lrow;
+    const int lc = pch ^ sw(row);
     const int n = n0 + row;
     b_off[i] = n < p.Cout ? (n * p.Kpad + lc * 8) * 2 : kOOB;
   }
@@ -232,18 +245,18 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
         const int row = wm * WTM + tm * 32 + fr;
-        af[buf][tm] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((q ^ ((row >> 1) & 7)) << 3));
+        af[buf][tm] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((q ^ sw(row)) << 3));
       }
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
         const int row = wn * WTN + tn * 32 + fr;
-        bfg[buf][tn] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((q ^ ((row >> 1) & 7)) << 3));
+        bfg[buf][tn] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((q ^ sw(row)) << 3));
       }
     };
     load(0, 0);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      if (ks < 3) load((ks + 1) & 1, ks + 1);
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks < KS - 1) load((ks + 1) & 1, ks + 1);
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
@@ -255,8 +268,8 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
     // reads(0) | reads(1) MFMAs(0) | reads(2) MFMAs(1) | reads(3) MFMAs(2) | MFMAs(3)
     __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      if (ks < 3) __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks < KS - 1) __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
     }
   };
@@ -340,13 +353,13 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
 
 typedef void (*ConvKernelFn)(const KvConvParams);
 
-template <int BM, int BN, int WM, int WN, int D = 2>
+template <int BM, int BN, int WM, int WN, int D = 2, int BKT = 64>
 ConvKernelFn glds_get(int mode) {
   switch (mode) {
-    case 0: return conv_glds_kernel<BM, BN, WM, WN, 0, D>;
-    case 1: return conv_glds_kernel<BM, BN, WM, WN, 1, D>;
-    case 4: return conv_glds_kernel<BM, BN, WM, WN, 4, D>;
-    default: return conv_glds_kernel<BM, BN, WM, WN, 3, D>;
+    case 0: return conv_glds_kernel<BM, BN, WM, WN, 0, D, BKT>;
+    case 1: return conv_glds_kernel<BM, BN, WM, WN, 1, D, BKT>;
+    case 4: return conv_glds_kernel<BM, BN, WM, WN, 4, D, BKT>;
+    default: return conv_glds_kernel<BM, BN, WM, WN, 3, D, BKT>;
   }
 }
 
@@ -376,6 +389,10 @@ static const GldsTile kGldsTiles[] = {
     // narrow N (YOLO's 16/32-channel layers at 160^2 / 320^2): BN = 32, 4 waves along M
     {128, 32, &glds_get<128, 32, 4, 1>},
     {256, 32, &glds_get<256, 32, 4, 1>},
+    // (BK = 32 rings -- glds_get<128, 128, 2, 2, 5, 32> etc., 4-5 K steps in flight at 2
+    // workgroups per CU -- measured 10-40 % SLOWER than {128, 128} D = 2 on every 3x3 and
+    // 1x1 layer of ResNet-50 at batch 640 (profiles/r1_v10_tile_probe_bk32.md): the 3x3
+    // layers are not L2-latency-bound, so they are not instantiated)
 };
 
 int glds_num_tiles() { return (int)(sizeof(kGldsTiles) / sizeof(kGldsTiles[0])); }
