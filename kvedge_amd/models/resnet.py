@@ -146,15 +146,18 @@ class DeployedBottleneck:
                 self.c3.spec.act == ACT_RELU and (self.dual is not None or self.down is None) and
                 (self.dual is None or c1.cout == 64) and k <= 128)
 
-    def call_tail(self, x, nxt: "DeployedBottleneck", t1=None):
-        """-> (this block's output y, the next block's conv1 output z) in one fused pass."""
+    def call_tail(self, x, nxt: "DeployedBottleneck", t1=None, out=None, z=None):
+        """-> (this block's output y, the next block's conv1 output z) in one fused pass.
+        ``out``/``z``: preallocated destinations (micro-batch slices of full-batch tensors)."""
         y = self.c1(x) if t1 is None else t1
         y = self.c2(y)
         c1 = nxt.c1
         if self.dual is not None:
             d = self.dual
-            return ops.conv_tail(y, d.w, d.b, d.act, c1.w, c1.b, x2=x, stride2=d.stride2)
-        return ops.conv_tail(y, self.c3.w, self.c3.b, self.c3.spec.act, c1.w, c1.b, res=x)
+            return ops.conv_tail(y, d.w, d.b, d.act, c1.w, c1.b, x2=x, stride2=d.stride2,
+                                 out=out, z=z)
+        return ops.conv_tail(y, self.c3.w, self.c3.b, self.c3.spec.act, c1.w, c1.b, res=x,
+                             out=out, z=z)
 
     def out_shape(self, x_shape):
         N, H, W, _ = x_shape
@@ -229,23 +232,35 @@ class KvResNet50:
         B = x.shape[0]
         mb = self.microbatch
         nb = self.microbatch_blocks
-        if mb and B > mb and B % mb == 0 and nb > 0:
-            full = None
+        t1 = None
+        if mb and B > mb and B % mb == 0 and 0 < nb < len(self.blocks):
+            full = full_t1 = None
             for i in range(0, B, mb):
                 y = self.stem_and_pool(x[i:i + mb], frames_in)
-                for b in self.blocks[:nb - 1]:
-                    y = b(y)
-                last = self.blocks[nb - 1]
-                if full is None:
-                    shp = last.out_shape(y.shape)
-                    full = ops.empty((B,) + shp[1:], dtype=y.dtype, device=y.device)
-                last(y, out=full[i:i + mb])  # write straight into the full-batch tensor
-            x = full
+                z = None
+                for j in range(nb):
+                    b, nxt = self.blocks[j], self.blocks[j + 1]
+                    last = j == nb - 1
+                    fuse = self.fuse_tail and y.is_cuda and b.can_tail(nxt)
+                    if last and full is None:
+                        shp = b.out_shape(y.shape)
+                        full = ops.empty((B,) + shp[1:], dtype=y.dtype, device=y.device)
+                        if fuse:
+                            full_t1 = ops.empty((B,) + shp[1:3] + (nxt.c1.spec.cout,),
+                                                dtype=y.dtype, device=y.device)
+                    # the last micro-batched block writes straight into the full-batch
+                    # tensors (and, fused, the next block's conv1 output too)
+                    o = full[i:i + mb] if last else None
+                    if fuse:
+                        y, z = b.call_tail(y, nxt, t1=z, out=o,
+                                           z=full_t1[i:i + mb] if last else None)
+                    else:
+                        y, z = b(y, t1=z, out=o), None
+            x, t1 = full, full_t1
             rest = self.blocks[nb:]
         else:
             x = self.stem_and_pool(x, frames_in)
             rest = self.blocks
-        t1 = None
         for i, b in enumerate(rest):
             nxt = rest[i + 1] if i + 1 < len(rest) else None
             if self.fuse_tail and x.is_cuda and nxt is not None and b.can_tail(nxt):

@@ -154,3 +154,20 @@ def test_resnet50_frames_in_parity(resnet):
         p_two, _ = ops.softmax_rows(lg_two)
     torch.cuda.synchronize()
     assert torch.allclose(p_fused.float(), p_two.float(), atol=2e-3)
+
+
+@pytest.mark.parametrize("mb,nb", [(2, 3), (4, 2), (2, 5)])
+def test_resnet50_microbatch_fused_tail(resnet, mb, nb):
+    """Micro-batched early stages (fused tails inside the micro-batch, the last one
+    writing y and the next conv1 output into full-batch slices) == the whole-batch path."""
+    _, kv, _ = resnet
+    fr = _frames(8, 5).cuda()
+    with torch.no_grad():
+        lg_full = kv.logits(fr, frames_in=True).float()
+        kv.microbatch, kv.microbatch_blocks = mb, nb
+        try:
+            lg_mb = kv.logits(fr, frames_in=True).float()
+        finally:
+            kv.microbatch, kv.microbatch_blocks = 0, 3
+    torch.cuda.synchronize()
+    assert torch.allclose(lg_full, lg_mb, atol=1e-2, rtol=1e-2), (lg_full - lg_mb).abs().max()
