@@ -33,6 +33,25 @@ def _time(fn: Callable[[int], object], tile: int, iters: int) -> float:
     return ts[len(ts) // 2]
 
 
+def _fleet_mean(rows):
+    """Mean over data-parallel ranks of a [keys][tiles] timing matrix (identity when not
+    distributed).  +inf (tile invalid for the layer) is the same on every rank."""
+    from .. import parallel
+
+    if not rows or not parallel.is_dist():
+        return rows
+    flat = [x for r in rows for x in r]
+    fin = [x if x != float("inf") else 0.0 for x in flat]
+    tot = parallel.allreduce_scalars(fin, op="sum")
+    world = parallel.info().world_size
+    out, i = [], 0
+    for r in rows:
+        out.append([tot[i + j] / world if r[j] != float("inf") else float("inf")
+                    for j in range(len(r))])
+        i += len(r)
+    return out
+
+
 def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
              cache_path: str = None, verbose: bool = False) -> Dict:
     """Tune every conv of ``model`` for ``example_input``'s shape. Returns {key: (tile, us)}."""
@@ -47,24 +66,36 @@ def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
     torch.cuda.synchronize()
     ntiles = int(torch.ops.kvedge.conv_num_tiles())
     results: Dict = {}
+    # phase 1: time every (distinct key, tile) on this GPU; invalid tiles stay +inf
+    todo = {}  # key string -> (key, fn, [us per tile])
     for layer, key, fn in rec:
         ks = repr(key)
-        if ks in results or ks in cache:
-            layer.tile = (results.get(ks) or cache[ks])[0]
-            results.setdefault(ks, cache.get(ks))
+        if ks in cache or ks in todo:
             continue
-        best, best_t = -1, float("inf")
+        ts = [float("inf")] * ntiles
         for t in range(ntiles):
             try:
-                dt = _time(fn, t, iters)
+                ts[t] = _time(fn, t, iters) * 1e3
             except RuntimeError:  # tile not valid for this layer kind
                 continue
-            if dt < best_t:
-                best, best_t = t, dt
-        layer.tile = best
-        results[ks] = (best, round(best_t * 1e3, 2))
+        todo[ks] = (key, ts)
+    # phase 2 (data-parallel replicas): every rank times the same keys in the same order
+    # (same model, same batch), so ONE all-reduce of the timing matrix gives each rank the
+    # fleet-mean time per tile and every replica pins the same, less noisy choice -- the
+    # job's images/sec is set by the slowest rank, so per-rank tuning noise costs throughput
+    fleet = _fleet_mean([v[1] for v in todo.values()])
+    for (ks, (key, _)), ts in zip(todo.items(), fleet):
+        best = min(range(ntiles), key=lambda t: ts[t]) if ntiles else -1
+        if ntiles and ts[best] == float("inf"):
+            best = -1
+        results[ks] = (best, round(ts[best], 2) if best >= 0 else None)
         if verbose:
-            print(f"autotune {key} -> tile {best} {best_t * 1e3:.1f} us", flush=True)
+            print(f"autotune {key} -> tile {best} {results[ks][1]} us", flush=True)
+    for layer, key, fn in rec:
+        ks = repr(key)
+        layer.tile = (results.get(ks) or cache[ks])[0]
+        if ks not in results:
+            results[ks] = cache[ks]
     if cache_path:
         os.makedirs(os.path.dirname(cache_path) or ".", exist_ok=True)
         cache.update(results)

@@ -33,8 +33,13 @@ def _worker(rank, world, port, q):
         s = parallel.allreduce_scalars([1.0, rank], op="sum")
         m = parallel.allreduce_scalars([rank * 1.5], op="max")
         g = parallel.all_gather_scalar(float(rank))
+        # fleet autotune: per-tile timings averaged over ranks, invalid tiles stay inf
+        from kvedge_amd.engine.autotune import _fleet_mean
+
+        inf = float("inf")
+        fm = _fleet_mean([[1.0 + rank, inf, 3.0], [inf, 2.0 * (rank + 1), 0.5]])
         parallel.barrier()
-        q.put((rank, ok_b, s, m, g))
+        q.put((rank, ok_b, s, m, g, fm))
     finally:
         parallel.shutdown()
 
@@ -51,8 +56,10 @@ def test_dp_collectives_gloo(world):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, ok_b, s, m, g in res:
+    for rank, ok_b, s, m, g, fm in res:
         assert ok_b
+        mean_r = sum(range(world)) / world
+        assert fm == [[1.0 + mean_r, float("inf"), 3.0], [float("inf"), 2.0 * (mean_r + 1), 0.5]]
         assert s == [float(world), float(sum(range(world)))]
         assert m == [1.5 * (world - 1)]
         assert g == [float(r) for r in range(world)]
