@@ -49,7 +49,8 @@ struct DirectCfg {
   static constexpr int CPP = CIN / 8;             // 16-B chunks per pixel
   static constexpr int KPT = CIN / 16;            // 16-wide k-steps per tap
   static constexpr int KS = KK * KK * KPT;        // k-steps per output block
-  static constexpr int PRE = CIN >= 64 ? 7 : 10;  // prefetch uint4 per thread (VGPR budget)
+  // prefetch uint4 per thread (VGPR budget: CIN 80 holds 180 weight VGPRs)
+  static constexpr int PRE = CIN >= 80 ? 6 : CIN >= 64 ? 7 : 10;
   static constexpr int MAX_PATCH = PRE * kNT * 16;
 };
 
@@ -69,8 +70,10 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
   static_assert(!U8 || (CIN == 16 && KK == 2 && S == 1), "frames-in form: the 2x2 s2d stem");
   using C = DirectCfg<CIN, KK>;
   constexpr int NCB = (COUT + 31) / 32;  // 32-channel blocks
-  static_assert(8 % NCB == 0, "waves split evenly over channel blocks");
-  constexpr int NPH = 8 / NCB;           // pixel-block phases
+  static_assert(NCB >= 1 && NCB <= 4, "channel blocks");
+  // pixel-block phases; with NCB = 3 (YOLO's 80-channel Detect cls branch) waves 6 and 7
+  // sit out the MFMA phase and only help with the patch fetch and the store pass
+  constexpr int NPH = 8 / NCB;
   constexpr int OS = COUT + 8;           // output tile pixel stride (elements)
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   unsigned char* patch = lds;
@@ -170,7 +173,7 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
     const int oy0 = band * kR;
     fetch(item + gridDim.x);  // next band: in flight during this band's MFMAs
 
-    for (int b = ph; b < nblk; b += NPH) {
+    for (int b = ph < NPH ? ph : nblk; b < nblk; b += NPH) {
       const int j = min(b * 32 + fr, npix - 1);  // clamp: pixels past npix are discarded
       const int yl = j / Wo, xc = j - yl * Wo;
       const unsigned char* pa0 = patch + (yl * S * PW + xc * S) * C::PB + fh * 16;
@@ -278,6 +281,7 @@ static const DirectEntry kDirect[] = {
     KV_DIRECT(64, 64, 2, kActSilu, false),   // h16
     KV_DIRECT(64, 128, 1, kActSilu, false),  // Detect P3 merged branch stem 64 -> 144 =
     KV_DIRECT(64, 16, 1, kActSilu, false),   //   128 + 16 (Cout split, direct_launch)
+    KV_DIRECT(80, 80, 1, kActSilu, false),   // Detect cls branch 3x3 (c3 = 80), NCB = 3
     // YOLO b0 stem in space-to-depth form: 2x2 over [N,320,320,16]
     {16, 16, 1, 2, kActSilu, false, conv3x3_direct_kernel<16, 16, 1, 2, kActSilu, false>},
     // ... and its frames-in form (preprocess fused)
@@ -287,7 +291,7 @@ static const DirectEntry kDirect[] = {
 #undef KV_DIRECT
 
 int direct_pb(int cin) { return cin * 2 + 16; }
-int direct_max_patch(int cin) { return (cin >= 64 ? 7 : 10) * kNT * 16; }
+int direct_max_patch(int cin) { return (cin >= 80 ? 6 : cin >= 64 ? 7 : 10) * kNT * 16; }
 
 }  // namespace
 

@@ -329,6 +329,9 @@ def test_conv_poisoned_canary(tile, k):
     (2, 10, 10, 64, 64, 2, ops.ACT_SILU, False, 0, 0, 0, 0),     # h16
     (1, 160, 160, 16, 16, 1, ops.ACT_SILU, False, 0, 0, 0, 0),   # full YOLO row width
     (2, 20, 20, 64, 144, 1, ops.ACT_SILU, False, 0, 0, 16, 8),   # Detect stem: 128 + 16 split
+    (2, 80, 80, 80, 80, 1, ops.ACT_SILU, False, 64, 64, 0, 0),   # Detect P3 cls 3x3 (NCB = 3)
+    (3, 13, 11, 80, 80, 1, ops.ACT_SILU, False, 0, 0, 8, 8),     # pixel-block tails, y slice
+    (2, 40, 40, 80, 80, 1, ops.ACT_SILU, False, 64, 64, 0, 0),   # Detect P4 cls
 ])
 def test_conv_direct3x3(case):
     """v4 persistent direct 3x3 conv (csrc/kernels/conv_direct.hip) vs the fp32 reference:
