@@ -389,6 +389,10 @@ static const GldsTile kGldsTiles[] = {
     // narrow N (YOLO's 16/32-channel layers at 160^2 / 320^2): BN = 32, 4 waves along M
     {128, 32, &glds_get<128, 32, 4, 1>},
     {256, 32, &glds_get<256, 32, 4, 1>},
+    // BN = 96 (3 x 32-wide MFMA blocks per wave, 4 waves along M): YOLO's 80-channel Detect
+    // cls convs waste 17 % of the MFMA columns here instead of 37.5 % on a BN = 128 tile
+    {128, 96, &glds_get<128, 96, 4, 1>},
+    {256, 96, &glds_get<256, 96, 4, 1>},
     // (BK = 32 rings -- glds_get<128, 128, 2, 2, 5, 32> etc., 4-5 K steps in flight at 2
     // workgroups per CU -- measured 10-40 % SLOWER than {128, 128} D = 2 on every 3x3 and
     // 1x1 layer of ResNet-50 at batch 640 (profiles/r1_v10_tile_probe_bk32.md): the 3x3
