@@ -62,9 +62,20 @@ struct DirectCfg {
 #ifndef KV_DIRECT_PD
 #define KV_DIRECT_PD 2
 #endif
-constexpr int KPD = KV_DIRECT_PD;  // LDS fragment reads in flight ahead of the MFMA
+constexpr int KPD = KV_DIRECT_PD;
 
-template <int CIN, int COUT, int S, int KK, int ACT, bool RES, bool U8 = false>
+// bytes of one patch buffer: the DMA form rounds up to whole 1-KB DMA instructions (the
+// last one may run past the patch) and keeps two buffers
+__host__ __device__ constexpr int direct_patch_alloc(int patch_bytes, bool dma) {
+  return dma ? (patch_bytes + 1023) / 1024 * 1024 : (patch_bytes + 15) / 16 * 16;
+}  // LDS fragment reads in flight ahead of the MFMA
+
+// DMA: the next band's patch goes global -> LDS with buffer_load ... lds into a second
+// patch buffer (no VGPR staging, so no PRE cap on the band height: the CIN = 80 form holds
+// 180 weight VGPRs and had room for a single 80-pixel output row per band otherwise).
+// Lane-linear DMA slots of 16 B; slot q = (pixel q / SL, chunk q % SL) with SL = PB / 16,
+// the pitch-padding chunk (q % SL == CPP) gets an out-of-range offset (zero fill).
+template <int CIN, int COUT, int S, int KK, int ACT, bool RES, bool U8 = false, bool DMA = false>
 __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvParams p, int kR,
                                                                 int PW, int patch_rows) {
   static_assert(!U8 || (CIN == 16 && KK == 2 && S == 1), "frames-in form: the 2x2 s2d stem");
@@ -76,8 +87,10 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
   constexpr int NPH = 8 / NCB;
   constexpr int OS = COUT + 8;           // output tile pixel stride (elements)
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  static_assert(!(DMA && U8), "DMA patch fetch: bf16 NHWC inputs only");
+  const int psz = direct_patch_alloc(patch_rows * PW * C::PB, DMA);
   unsigned char* patch = lds;
-  bf16* otile = reinterpret_cast<bf16*>(lds + ((patch_rows * PW * C::PB + 15) & ~15));
+  bf16* otile = reinterpret_cast<bf16*>(lds + (DMA ? 2 * psz : psz));
 
   const int H = p.H, W = p.W, Ho = p.Ho, Wo = p.Wo;
   const int nbands = (Ho + kR - 1) / kR;
@@ -98,7 +111,7 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
   }
   // bias staged once in LDS (not 16 live VGPRs: the CIN = 64 forms sit at the 256 cap)
   float* lbias = reinterpret_cast<float*>(
-      lds + ((patch_rows * PW * C::PB + 15) & ~15) + ((kR * p.Wo * OS * 2 + 15) & ~15));
+      reinterpret_cast<unsigned char*>(otile) + ((kR * p.Wo * OS * 2 + 15) & ~15));
   if (tid < NCB * 32) lbias[tid] = (p.bias && tid < COUT) ? p.bias[tid] : 0.f;
 
   // ---- band patch prefetch: 16-B chunk q -> patch pixel q / CPP (row-major, pitch PW)
@@ -159,24 +172,53 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
     }
   };
 
+  constexpr int SL = C::PB / 16;  // 16-B slots per patch pixel (CPP data + 1 padding)
+  const int nslots = patch_rows * PW * SL;
+  auto dma_fetch = [&](int item, unsigned char* dst) __attribute__((always_inline)) {
+    const int n = item / nbands, band = item - n * nbands;
+    const int iy0 = band * kR * S - 1;
+    const bool live = item < total;
+    for (int j = wv; j * 64 < nslots; j += kNT / 64) {  // one 1-KB DMA per wave per j
+      const int q = j * 64 + lane;
+      const int pp = q / SL, c = q - pp * SL;
+      const int pr = pp / PW, pc = pp - pr * PW;
+      const int iy = iy0 + pr, ix = pc - 1;
+      const bool ok = live && q < nslots && c < C::CPP && (unsigned)iy < (unsigned)H &&
+                      (unsigned)ix < (unsigned)W;
+      const int off = ok ? (((n * H + iy) * W + ix) * p.ldx + p.x_coff + c * 8) * 2 : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rx, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16, off, 0, 0, 0);
+    }
+  };
+
   bf16* __restrict__ Y = reinterpret_cast<bf16*>(p.y);
   const bf16* __restrict__ R = reinterpret_cast<const bf16*>(p.res);
   const int npix = kR * Wo;
   const int nblk = (npix + 31) / 32;
   const int rowb = PW * C::PB;
   int item = xcd_remap(blockIdx.x, gridDim.x);  // neighbour bands share an XCD
-  fetch(item);
-  commit();
+  int cur = 0;
+  if constexpr (DMA) {
+    dma_fetch(item, patch);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    fetch(item);
+    commit();
+  }
   __syncthreads();
   for (; item < total; item += gridDim.x) {
     const int n = item / nbands, band = item - n * nbands;
     const int oy0 = band * kR;
-    fetch(item + gridDim.x);  // next band: in flight during this band's MFMAs
+    // next band: in flight during this band's MFMAs (DMA: into the other patch buffer,
+    // last read in the previous band, before the barrier that ended it)
+    if constexpr (DMA) dma_fetch(item + gridDim.x, patch + (cur ^ 1) * psz);
+    else fetch(item + gridDim.x);
+    const unsigned char* pbase = patch + cur * psz;
 
     for (int b = ph < NPH ? ph : nblk; b < nblk; b += NPH) {
       const int j = min(b * 32 + fr, npix - 1);  // clamp: pixels past npix are discarded
       const int yl = j / Wo, xc = j - yl * Wo;
-      const unsigned char* pa0 = patch + (yl * S * PW + xc * S) * C::PB + fh * 16;
+      const unsigned char* pa0 = pbase + (yl * S * PW + xc * S) * C::PB + fh * 16;
       const unsigned char* pa[KK];
 #pragma unroll
       for (int r = 0; r < KK; ++r) pa[r] = pa0 + r * rowb;
@@ -230,7 +272,7 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
     __syncthreads();  // output tile complete; patch no longer read
     // next band's patch BEFORE this band's stores: on gfx9 vmcnt counts stores too, so a
     // commit after the store pass made its vmcnt(0) wait for this band's stores to land
-    commit();
+    if constexpr (!DMA) commit();
 
     // ---- store the band (+ residual after the activation): 16-B channel chunks
     constexpr int OCH = COUT / 8;
@@ -250,6 +292,10 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
       }
       *reinterpret_cast<uint4*>(Y + m * p.ldy + p.y_coff + c * 8) = v;
     }
+    if constexpr (DMA) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs landed
+      cur ^= 1;
+    }
     __syncthreads();  // patch ready, output tile free
   }
 }
@@ -261,33 +307,42 @@ struct DirectEntry {
   bool res;
   DirectFn fn;
   bool u8 = false;
+  bool dma = false;
 };
 
 #define KV_DIRECT(CI, CO, S, A, R) {CI, CO, S, 3, A, R, conv3x3_direct_kernel<CI, CO, S, 3, A, R>}
+// the same shape with the DMA patch fetch (direct tile 1; the autotuner picks per layer)
+#define KV_DIRECT_DMA(CI, CO, S, A, R) \
+  {CI, CO, S, 3, A, R, conv3x3_direct_kernel<CI, CO, S, 3, A, R, false, true>, false, true}
+#define KV_DIRECT2(CI, CO, S, A, R) KV_DIRECT(CI, CO, S, A, R), KV_DIRECT_DMA(CI, CO, S, A, R)
 // the 3x3 shapes of ResNet-50 stage 1 and YOLOv8n's narrow layers (backbone, C2f
 // bottlenecks, PAN downsamplers, Detect 64-channel branches)
 static const DirectEntry kDirect[] = {
-    KV_DIRECT(64, 64, 1, kActRelu, false),   // ResNet-50 layer1 conv2 x3
-    KV_DIRECT(64, 64, 1, kActNone, false),
-    KV_DIRECT(16, 32, 2, kActSilu, false),   // YOLO b1
-    KV_DIRECT(16, 16, 1, kActSilu, false),   // b2 bottleneck cv1
-    KV_DIRECT(16, 16, 1, kActSilu, true),    // b2 bottleneck cv2 (+x)
-    KV_DIRECT(32, 64, 2, kActSilu, false),   // b3
-    KV_DIRECT(32, 32, 1, kActSilu, false),   // b4 / h15 bottlenecks
-    KV_DIRECT(32, 32, 1, kActSilu, true),
-    KV_DIRECT(64, 128, 2, kActSilu, false),  // b5
-    KV_DIRECT(64, 64, 1, kActSilu, false),   // b6 / h12 / h18 bottlenecks, Detect a1
-    KV_DIRECT(64, 64, 1, kActSilu, true),
-    KV_DIRECT(64, 64, 2, kActSilu, false),   // h16
-    KV_DIRECT(64, 128, 1, kActSilu, false),  // Detect P3 merged branch stem 64 -> 144 =
-    KV_DIRECT(64, 16, 1, kActSilu, false),   //   128 + 16 (Cout split, direct_launch)
-    KV_DIRECT(80, 80, 1, kActSilu, false),   // Detect cls branch 3x3 (c3 = 80), NCB = 3
+    KV_DIRECT2(64, 64, 1, kActRelu, false),   // ResNet-50 layer1 conv2 x3
+    KV_DIRECT2(64, 64, 1, kActNone, false),
+    KV_DIRECT2(16, 32, 2, kActSilu, false),   // YOLO b1
+    KV_DIRECT2(16, 16, 1, kActSilu, false),   // b2 bottleneck cv1
+    KV_DIRECT2(16, 16, 1, kActSilu, true),    // b2 bottleneck cv2 (+x)
+    KV_DIRECT2(32, 64, 2, kActSilu, false),   // b3
+    KV_DIRECT2(32, 32, 1, kActSilu, false),   // b4 / h15 bottlenecks
+    KV_DIRECT2(32, 32, 1, kActSilu, true),
+    KV_DIRECT2(64, 128, 2, kActSilu, false),  // b5
+    KV_DIRECT2(64, 64, 1, kActSilu, false),   // b6 / h12 / h18 bottlenecks, Detect a1
+    KV_DIRECT2(64, 64, 1, kActSilu, true),
+    KV_DIRECT2(64, 64, 2, kActSilu, false),   // h16
+    KV_DIRECT2(64, 128, 1, kActSilu, false),  // Detect P3 merged branch stem 64 -> 144 =
+    KV_DIRECT2(64, 16, 1, kActSilu, false),   //   128 + 16 (Cout split, direct_launch)
+    // Detect cls branch 3x3 (c3 = 80), NCB = 3: DMA form only (the VGPR-prefetch form
+    // spills with 180 weight VGPRs and fits one output row per band)
+    KV_DIRECT_DMA(80, 80, 1, kActSilu, false),
     // YOLO b0 stem in space-to-depth form: 2x2 over [N,320,320,16]
     {16, 16, 1, 2, kActSilu, false, conv3x3_direct_kernel<16, 16, 1, 2, kActSilu, false>},
     // ... and its frames-in form (preprocess fused)
     {16, 16, 1, 2, kActSilu, false, conv3x3_direct_kernel<16, 16, 1, 2, kActSilu, false, true>,
      true},
 };
+#undef KV_DIRECT2
+#undef KV_DIRECT_DMA
 #undef KV_DIRECT
 
 int direct_pb(int cin) { return cin * 2 + 16; }
@@ -295,10 +350,11 @@ int direct_max_patch(int cin) { return (cin >= 80 ? 6 : cin >= 64 ? 7 : 10) * kN
 
 }  // namespace
 
-int direct_num_tiles() { return 1; }
+// tile 0: the VGPR-prefetch form where one exists; tile 1: the DMA form where one exists
+int direct_num_tiles() { return 2; }
 
 // Returns the instantiation index for p (or < 0), and the band geometry it would use.
-static int direct_plan(const KvConvParams* p, int* kR, int* PW, int* rows, int* lds) {
+static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* rows, int* lds) {
   const int kk = p->KH;
   if (p->mode != 0 || p->KW != kk || (kk != 2 && kk != 3) || p->pad != 1) return -8;
   if (p->stride != 1 && p->stride != 2) return -8;
@@ -307,12 +363,15 @@ static int direct_plan(const KvConvParams* p, int* kR, int* PW, int* rows, int* 
   const bool res = p->res != nullptr;
   if (res && !(p->act & 4) && act != kActNone) return -8;  // only x + act(conv)
   int idx = -1;
-  for (int i = 0; i < (int)(sizeof(kDirect) / sizeof(kDirect[0])); ++i) {
-    const DirectEntry& e = kDirect[i];
-    if (e.cin == p->Cin && e.cout == p->Cout && e.stride == p->stride && e.kk == kk &&
-        e.act == act && e.res == res && e.u8 == (p->in_u8 != 0)) {
-      idx = i;
-      break;
+  for (int pass = 0; pass < 2 && idx < 0; ++pass) {  // the tile's form first, then any
+    for (int i = 0; i < (int)(sizeof(kDirect) / sizeof(kDirect[0])); ++i) {
+      const DirectEntry& e = kDirect[i];
+      if (e.cin == p->Cin && e.cout == p->Cout && e.stride == p->stride && e.kk == kk &&
+          e.act == act && e.res == res && e.u8 == (p->in_u8 != 0) &&
+          (pass == 1 || e.dma == (tile == 1))) {
+        idx = i;
+        break;
+      }
     }
   }
   if (idx < 0) return -8;
@@ -326,26 +385,33 @@ static int direct_plan(const KvConvParams* p, int* kR, int* PW, int* rows, int* 
   const int pb = direct_pb(p->Cin);
   const int os = p->Cout + 8;
   // rows per band: as many as fit (<= 8) in the prefetch budget and LDS
+  // (DMA form: two patch buffers in LDS, no VGPR prefetch budget)
+  const bool dma = kDirect[idx].dma;
+  auto lds_of = [&](int prows, int r) {
+    const int np = dma ? 2 : 1;
+    return np * direct_patch_alloc(prows * *PW * pb, dma) + ((r * p->Wo * os * 2 + 15) & ~15) +
+           kBiasBytes;
+  };
+  // band height: the tallest that fits (<= 8).  (A "fewest pixel-block rounds" rule was
+  // measured slower on YOLO's 32-channel layers at 160^2: the extra halo rows and per-band
+  // overhead of shorter bands outweigh the better MFMA-phase balance.)
   int r = 8;
   for (; r >= 1; --r) {
     const int prows = (r - 1) * S + kk;
     const int patch = prows * *PW * pb;
-    const int ob = r * p->Wo * os * 2;
-    if (patch <= direct_max_patch(p->Cin) &&
-        ((patch + 15) & ~15) + ((ob + 15) & ~15) + kBiasBytes <= kLds)
-      break;
+    if ((dma || patch <= direct_max_patch(p->Cin)) && lds_of(prows, r) <= kLds) break;
   }
   if (r < 1) return -11;
   if (r > p->Ho) r = p->Ho;
   *kR = r;
   *rows = (r - 1) * S + kk;
-  *lds = ((*rows * *PW * pb + 15) & ~15) + ((r * p->Wo * os * 2 + 15) & ~15) + kBiasBytes;
+  *lds = lds_of(*rows, r);
   return idx;
 }
 
-static int direct_launch_one(const KvConvParams* p, hipStream_t stream) {
+static int direct_launch_one(const KvConvParams* p, int tile, hipStream_t stream) {
   int kR, PW, rows, lds;
-  const int idx = direct_plan(p, &kR, &PW, &rows, &lds);
+  const int idx = direct_plan(p, tile, &kR, &PW, &rows, &lds);
   if (idx < 0) return idx;
   const long long items = (long long)p->N * ((p->Ho + kR - 1) / kR);
   if (items <= 0) return 0;
@@ -367,7 +433,7 @@ static int direct_launch_one(const KvConvParams* p, hipStream_t stream) {
 int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   if (tile < 0 || tile >= direct_num_tiles()) return -6;
   int kR, PW, rows, lds;
-  if (direct_plan(p, &kR, &PW, &rows, &lds) >= 0) return direct_launch_one(p, stream);
+  if (direct_plan(p, tile, &kR, &PW, &rows, &lds) >= 0) return direct_launch_one(p, tile, stream);
   if (p->res || p->Cout % 16) return -8;
   // validate the whole split before launching anything
   int cuts[8], ncut = 0, done = 0;
@@ -376,7 +442,7 @@ int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
     for (const DirectEntry& e : kDirect) {
       KvConvParams q = *p;
       q.Cout = e.cout;
-      if (e.cout <= p->Cout - done && e.cout > best && direct_plan(&q, &kR, &PW, &rows, &lds) >= 0)
+      if (e.cout <= p->Cout - done && e.cout > best && direct_plan(&q, tile, &kR, &PW, &rows, &lds) >= 0)
         best = e.cout;
     }
     if (best == 0) return -8;
@@ -391,7 +457,7 @@ int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
     q.w = static_cast<const bf16*>(p->w) + (size_t)off * p->Kpad;
     q.bias = p->bias ? p->bias + off : nullptr;
     q.y_coff = p->y_coff + off;
-    const int rc = direct_launch_one(&q, stream);
+    const int rc = direct_launch_one(&q, tile, stream);
     if (rc != 0) return rc;
     off += cuts[i];
   }

@@ -82,7 +82,7 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale + 0.02
 
 
-N_TILES = 42  # v1 register-staged (0-5) + v2 LDS-DMA (6-23) + v3 streaming (24-40) + v4 direct (41)
+N_TILES = 43  # v1 register-staged (0-5) + v2 LDS-DMA (6-23) + v3 streaming (24-40) + v4 direct (41-42)
 STREAM0 = 24  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
 DIRECT0 = 41  # v4 direct 3x3 (conv_direct.hip): its instantiation table only
 # v3 (bm, bn, ring depth, weight slice resident in LDS) -- conv_stream.hip kStreamTiles
@@ -279,7 +279,8 @@ def test_conv_dual_rejects_v1_tiles():
         ops.conv_dual(x1, x2, w, None, ops.ACT_NONE, 1, tile=0)
 
 
-@pytest.mark.parametrize("tile", [-1, 1, 6, 7, 12, 13, STREAM0, STREAM0 + 1, STREAM0 + 5, DIRECT0])
+@pytest.mark.parametrize("tile", [-1, 1, 6, 7, 12, 13, STREAM0, STREAM0 + 1, STREAM0 + 5, DIRECT0,
+                                  DIRECT0 + 1])
 @pytest.mark.parametrize("k", [1, 3])
 def test_conv_poisoned_canary(tile, k):
     """SURVEY §5.2 poisoned-buffer check: the output buffer is NaN-filled, with a NaN
@@ -288,10 +289,10 @@ def test_conv_poisoned_canary(tile, k):
     (a kernel that writes past M/N tails or outside [y_coff, y_coff+cout) fails here)."""
     if STREAM0 <= tile < DIRECT0 and k != 1:
         pytest.skip("v3 tiles take 1x1 GEMMs only")
-    if tile == DIRECT0 and k != 3:
+    if tile >= DIRECT0 and k != 3:
         pytest.skip("v4 takes 3x3 only")
     N, H, W, cin, cout, ldy, y_coff = 3, 13, 11, 64, 72, 104, 16
-    if tile == DIRECT0:
+    if tile >= DIRECT0:
         cout = 64  # an instantiated direct shape (64 -> 64 ReLU)
     spec = ConvSpec.auto(cin, cout, k, 1, k // 2, ops.ACT_RELU)
     g = torch.Generator().manual_seed(3)
@@ -333,13 +334,15 @@ def test_conv_poisoned_canary(tile, k):
     (3, 13, 11, 80, 80, 1, ops.ACT_SILU, False, 0, 0, 8, 8),     # pixel-block tails, y slice
     (2, 40, 40, 80, 80, 1, ops.ACT_SILU, False, 64, 64, 0, 0),   # Detect P4 cls
 ])
-def test_conv_direct3x3(case):
+@pytest.mark.parametrize("dtile", [0, 1])
+def test_conv_direct3x3(case, dtile):
     """v4 persistent direct 3x3 conv (csrc/kernels/conv_direct.hip) vs the fp32 reference:
-    both strides, odd sizes, channel slices in/out, residual after the activation."""
+    both strides, odd sizes, channel slices in/out, residual after the activation.
+    dtile 0: VGPR-prefetched band patch; 1: the DMA (buffer_load ... lds) double buffer."""
     N, H, W, cin, cout, s, act, res, lx, xc, ly, yc = case
     a = act | (ops.RES_AFTER_ACT if res and act != ops.ACT_NONE else 0)
     err, scale = _conv_case(N, H, W, cin, cout, 3, s, 1, a, res=res, ldx_extra=lx, x_coff=xc,
-                            ldy_extra=ly, y_coff=yc, tile=DIRECT0)
+                            ldy_extra=ly, y_coff=yc, tile=DIRECT0 + dtile)
     assert err <= 0.02 * scale + 0.02, (case, err, scale)
 
 
