@@ -200,24 +200,29 @@ __global__ __launch_bounds__(kBlock) void softmax_kernel(const bf16* __restrict_
 }
 
 // ---- K8 nearest 2x upsample into a channel slice ---------------------------
+// One thread per SOURCE 16-B vector: one load, four stores (the 2x2 block it
+// feeds).  32-bit index math (host checks N*H*W*C/8 < 2^31); the grid is sized to
+// the work, so each thread runs its body at most a few times.
 __global__ __launch_bounds__(kBlock) void upsample2x_kernel(const bf16* __restrict__ x,
                                                             bf16* __restrict__ y, int N, int H,
                                                             int W, int C, int ldx, int x_coff,
                                                             int ldy, int y_coff) {
-  const int C8 = C / 8;
-  const int Ho = 2 * H, Wo = 2 * W;
-  const long long total = (long long)N * Ho * Wo * C8;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c8 = (int)(i % C8);
-    long long pix = i / C8;
-    const int wo = (int)(pix % Wo);
-    pix /= Wo;
-    const int ho = (int)(pix % Ho);
-    const int n = (int)(pix / Ho);
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(
-        x + ((long long)(n * H + (ho >> 1)) * W + (wo >> 1)) * ldx + x_coff + c8 * 8);
-    *reinterpret_cast<bf16x8*>(y + ((long long)(n * Ho + ho) * Wo + wo) * ldy + y_coff + c8 * 8) = v;
+  const int C8 = C >> 3;
+  const int total = N * H * W * C8;
+  const int Wo = 2 * W;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c8 = i % C8;
+    const int pix = i / C8;              // (n*H + h)*W + w
+    const int w = pix % W;
+    const int nh = pix / W;              // n*H + h
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (long long)pix * ldx + x_coff + c8 * 8);
+    // output row n*Ho + 2h = 2*nh, columns 2w and 2w+1
+    bf16* r0 = y + ((long long)(2 * nh) * Wo + 2 * w) * ldy + y_coff + c8 * 8;
+    bf16* r1 = r0 + (long long)Wo * ldy;
+    *reinterpret_cast<bf16x8*>(r0) = v;
+    *reinterpret_cast<bf16x8*>(r0 + ldy) = v;
+    *reinterpret_cast<bf16x8*>(r1) = v;
+    *reinterpret_cast<bf16x8*>(r1 + ldy) = v;
   }
 }
 
@@ -382,8 +387,11 @@ extern "C" int kv_softmax_rows(const void* x, float* y, int64_t* argmax, int row
 extern "C" int kv_upsample2x(const void* x, void* y, int N, int H, int W, int C, int ldx,
                              int x_coff, int ldy, int y_coff, hipStream_t s) {
   if (C % 8 || ldx % 8 || x_coff % 8 || ldy % 8 || y_coff % 8) return -1;
-  const long long work = (long long)N * 4 * H * W * (C / 8);
-  hipLaunchKernelGGL(upsample2x_kernel, dim3(grid_for(work)), dim3(kBlock), 0, s,
+  const long long work = (long long)N * H * W * (C / 8);
+  if (work >= (1ll << 31)) return -1;
+  long long g = (work + kBlock - 1) / kBlock;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(upsample2x_kernel, dim3((unsigned)(g < 1 ? 1 : g)), dim3(kBlock), 0, s,
                      (const bf16*)x, (bf16*)y, N, H, W, C, ldx, x_coff, ldy, y_coff);
   KV_CHECK_LAUNCH();
 }

@@ -94,9 +94,22 @@ __global__ __launch_bounds__(256) void yolo_decode_kernel(
   const bf16* cr = row + 4 * kRegMax + p * cq;
   float best = -INFINITY;
   int bc = p * cq;
-  for (int c = 0; c < cq; ++c) {
-    const float v = (float)cr[c];
-    if (v > best) { best = v; bc = p * cq + c; }
+  if ((cq & 3) == 0) {
+    // 8-B LDS reads (cq*2 bytes per lane quarter is 8-B aligned; rows are 16-B aligned):
+    // 4x fewer ds_read issues than the u16 loop, same first-max tie rule
+    for (int c = 0; c < cq; c += 4) {
+      const bf16x4 v4 = *reinterpret_cast<const bf16x4*>(cr + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = (float)v4[j];
+        if (v > best) { best = v; bc = p * cq + c + j; }
+      }
+    }
+  } else {
+    for (int c = 0; c < cq; ++c) {
+      const float v = (float)cr[c];
+      if (v > best) { best = v; bc = p * cq + c; }
+    }
   }
 #pragma unroll
   for (int o = 1; o <= 2; o <<= 1) {

@@ -200,6 +200,21 @@ def test_sppf_and_upsample():
     assert torch.equal(out.cpu(), out_ref)
 
 
+@pytest.mark.parametrize("N,H,W,C", [(3, 7, 5, 8), (2, 20, 20, 256), (1, 13, 40, 128)])
+def test_upsample_slices_and_canary(N, H, W, C):
+    """Non-square / odd sizes, channel slices on both sides; untouched channels of the
+    destination (the concat partner's slice) must keep their NaN canary."""
+    ldx, ldy = C + 16, C + 24
+    x = _rand((N, H, W, ldx), 11)
+    out_ref = torch.full((N, 2 * H, 2 * W, ldy), float("nan"), dtype=torch.bfloat16)
+    out = out_ref.clone().cuda()
+    ops.upsample2x(x, out_ref, C=C, x_coff=8, y_coff=16)
+    ops.upsample2x(x.cuda(), out, C=C, x_coff=8, y_coff=16)
+    got = out.cpu()
+    assert torch.equal(got[..., 16:16 + C], out_ref[..., 16:16 + C])
+    assert torch.isnan(got[..., :16]).all() and torch.isnan(got[..., 16 + C:]).all()
+
+
 def test_synth_preprocess_bn():
     fr = torch.empty(2, 16, 16, 3, dtype=torch.uint8)
     ops.synth_frames(fr, 7, 3)
