@@ -172,6 +172,11 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
     }
   }
 
+  // MODE 0 K-step position (tap row r, tap col s, channel base c0), advanced once per
+  // issue(): the issue order is kt = 0, 1, 2, ... on both pipelines, so the per-step
+  // k0 / Cin and tap / KW divisions (a ~20-instruction VALU expansion each: there is no
+  // scalar divide) become a compare-and-bump on wave-uniform values
+  int k_c0 = 0, k_r = 0, k_s = 0;
   auto issue = [&](int stage, int kt) {
     bf16* As = smem + stage * STAGE;
     bf16* Bs = As + BM * BK;
@@ -194,11 +199,14 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
           glds16(rx2, As + (wv * A_INS + i) * 512, a_off2[i], (kbase - p.K1) * 2);
       }
     } else if (MODE == 0) {
-      const int k0 = kt * BK;
-      const int tap = k0 / p.Cin;           // wave-uniform
-      const int c0 = k0 - tap * p.Cin;
-      const int r = tap / p.KW, s = tap - (tap / p.KW) * p.KW;
+      const int c0 = k_c0, r = k_r, s = k_s;  // wave-uniform
+      const int tap = r * p.KW + s;
       const int toff = (r * p.W + s) * p.ldx + c0;  // elements, wave-uniform
+      k_c0 += BK;  // Cin % 64 == 0 in MODE 0: a K step never straddles two taps
+      if (k_c0 >= p.Cin) {
+        k_c0 = 0;
+        if (++k_s == p.KW) { k_s = 0; ++k_r; }
+      }
 #pragma unroll
       for (int i = 0; i < A_INS; ++i) {
         // a_off may be negative (top/left padding rows); only valid taps form an address

@@ -96,7 +96,7 @@ def test_yolov8n_pipeline_graph(yolo):
     assert (o_g.cpu() - o_c).abs().max() < 1e-3
 
 
-@pytest.mark.parametrize("hw", [(64, 96), (22, 10)])
+@pytest.mark.parametrize("hw", [(64, 96), (22, 10), (30, 44), (18, 132)])
 def test_stem_from_frames_kernel(hw):
     """Frames-in v4 kernel (preprocess + s2d + 2x2 stem in one pass) vs the CPU reference."""
     from kvedge_amd.models.yolov8 import KvYoloV8n, init_yolov8n
