@@ -52,11 +52,28 @@ def _fleet_mean(rows):
     return out
 
 
+def _near_ties(rows, tol: float):
+    """[(row, tile)] of every tile within ``tol`` of its row's best, for rows with more
+    than one such tile (the re-timing list of the refine phase; deterministic order)."""
+    out = []
+    for i, ts in enumerate(rows):
+        best = min(ts) if ts else float("inf")
+        if best == float("inf"):
+            continue
+        near = [t for t in range(len(ts)) if ts[t] <= best * (1.0 + tol)]
+        if len(near) > 1:
+            out += [(i, t) for t in near]
+    return out
+
+
 def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
-             cache_path: str = None, verbose: bool = False) -> Dict:
+             cache_path: str = None, verbose: bool = False, refine_iters: int = None,
+             refine_tol: float = 0.05) -> Dict:
     """Tune every conv of ``model`` for ``example_input``'s shape. Returns {key: (tile, us)}."""
     if not example_input.is_cuda:
         return {}
+    if refine_iters is None:
+        refine_iters = int(os.environ.get("KVEDGE_AUTOTUNE_REFINE_ITERS", "20"))
     cache = {}
     if cache_path and os.path.exists(cache_path):
         with open(cache_path) as f:
@@ -78,13 +95,26 @@ def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
                 ts[t] = _time(fn, t, iters) * 1e3
             except RuntimeError:  # tile not valid for this layer kind
                 continue
-        todo[ks] = (key, ts)
+        todo[ks] = (key, fn, ts)
     # phase 2 (data-parallel replicas): every rank times the same keys in the same order
     # (same model, same batch), so ONE all-reduce of the timing matrix gives each rank the
     # fleet-mean time per tile and every replica pins the same, less noisy choice -- the
     # job's images/sec is set by the slowest rank, so per-rank tuning noise costs throughput
-    fleet = _fleet_mean([v[1] for v in todo.values()])
-    for (ks, (key, _)), ts in zip(todo.items(), fleet):
+    fleet = _fleet_mean([v[2] for v in todo.values()])
+    # phase 3: near-ties (within ``refine_tol`` of the best, by the fleet mean -- so every
+    # rank re-times the same (key, tile) list in the same order) are re-timed with
+    # ``refine_iters`` launches; a 5-launch median alone flipped picks between runs
+    if refine_iters > iters:
+        fns = [(ks, fn) for ks, (_, fn, _) in todo.items()]
+        cand = [(fns[i][0], fns[i][1], t) for i, t in _near_ties(fleet, refine_tol)]
+        if cand:
+            re = _fleet_mean([[_time(fn, t, refine_iters) * 1e3 for ks, fn, t in cand]])[0]
+            idx = {ks: i for i, ks in enumerate(todo)}
+            for (ks, _, t), us in zip(cand, re):
+                row = fleet[idx[ks]]
+                row[t] = us
+            # tiles not re-timed keep their (slower by > tol) phase-1 times
+    for (ks, (key, _, _)), ts in zip(todo.items(), fleet):
         best = min(range(ntiles), key=lambda t: ts[t]) if ntiles else -1
         if ntiles and ts[best] == float("inf"):
             best = -1

@@ -74,3 +74,13 @@ def test_single_process_noop():
     assert parallel.broadcast_tensors([torch.ones(3)]) == 0
     assert parallel.allreduce_scalars([2.0]) == [2.0]
     assert parallel.all_gather_scalar(3.0) == [3.0]
+
+
+def test_autotune_near_ties():
+    from kvedge_amd.engine.autotune import _near_ties
+
+    inf = float("inf")
+    rows = [[10.0, 10.4, 12.0, inf], [5.0, 9.0, inf, inf], [inf, inf, inf, inf], [],
+            [20.0, 20.0, 20.9, 21.5]]
+    assert _near_ties(rows, 0.05) == [(0, 0), (0, 1), (4, 0), (4, 1), (4, 2)]
+    assert _near_ties(rows, 0.0) == [(4, 0), (4, 1)]
