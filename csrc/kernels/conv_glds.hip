@@ -182,10 +182,15 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
     bf16* Bs = As + BM * BK;
     if (MODE == 1) {
       const int kbase = kt * BK;
+      if (kbase + BK <= p.Cin) {  // wave-uniform: no K tail in this step, no per-lane select
 #pragma unroll
-      for (int i = 0; i < A_INS; ++i) {
-        const int v = (kbase + a_lc[i] * 8 < p.Cin) ? a_off[i] : kOOB;
-        glds16(rx, As + (wv * A_INS + i) * 512, v, kbase * 2);
+        for (int i = 0; i < A_INS; ++i) glds16(rx, As + (wv * A_INS + i) * 512, a_off[i], kbase * 2);
+      } else {
+#pragma unroll
+        for (int i = 0; i < A_INS; ++i) {
+          const int v = (kbase + a_lc[i] * 8 < p.Cin) ? a_off[i] : kOOB;
+          glds16(rx, As + (wv * A_INS + i) * 512, v, kbase * 2);
+        }
       }
     } else if (MODE == 4) {
       const int kbase = kt * BK;  // K1 and K - K1 are multiples of 64: no tails
