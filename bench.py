@@ -33,8 +33,8 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("KVEDGE_BENCH_BATCH", 0)),
-                    help="per-GPU batch (0 = model default: ResNet-50 640, YOLOv8n 256 -- the "
-                         "throughput knees of the batch sweep, profiles/r1_batch_sweep.jsonl)")
+                    help="per-GPU batch (0 = model default: ResNet-50 640, YOLOv8n 384 -- the "
+                         "throughput knees of the batch sweep, profiles/r1_v13_batch_sweep.jsonl)")
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "yolov8n"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-autotune", action="store_true")
@@ -72,7 +72,7 @@ def main(argv=None):
             torch.cuda.synchronize()
 
     if a.batch <= 0:
-        a.batch = (640 if a.model == "resnet50" else 256) if on_gpu else 1
+        a.batch = (640 if a.model == "resnet50" else 384) if on_gpu else 1
     t_build = time.perf_counter()
     if a.model == "resnet50":
         from kvedge_amd.models.resnet import KvResNet50
