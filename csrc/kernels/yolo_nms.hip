@@ -30,10 +30,15 @@ constexpr int kMaxCand = 16384;
 
 constexpr int kDecAnch = 64;  // anchors per workgroup (256 threads = 4 lanes per anchor)
 
+// NC > 0: the class count is a compile-time constant (COCO's 80), so the staging loop's
+// row / chunk split is a multiply-shift instead of a runtime divide (a ~20-instruction VALU
+// expansion per 16-B chunk on gfx9).  NC = 0: any nc % 8 == 0 at run time.
+template <int NC>
 __global__ __launch_bounds__(256) void yolo_decode_kernel(
     const bf16* __restrict__ f0, const bf16* __restrict__ f1, const bf16* __restrict__ f2,
-    int h0, int w0, int h1, int w1, int h2, int w2, int s0, int s1, int s2, int N, int nc,
+    int h0, int w0, int h1, int w1, int h2, int w2, int s0, int s1, int s2, int N, int nc_rt,
     float* __restrict__ boxes, float* __restrict__ scores, int* __restrict__ cls) {
+  const int nc = NC > 0 ? NC : nc_rt;
   extern __shared__ __attribute__((aligned(16))) bf16 tile[];  // [64][ch + 8]
   const int A0 = h0 * w0, A1 = h1 * w1, A2 = h2 * w2;
   const int A = A0 + A1 + A2;
@@ -84,7 +89,10 @@ __global__ __launch_bounds__(256) void yolo_decode_kernel(
   }
   const float dist = sw / se;
   const int al = a0 + a;
-  const float ax = (float)(al % w) + 0.5f, ay = (float)(al / w) + 0.5f;
+  // al / w via a float reciprocal: al < 2^16, and (al + 0.5) / w sits >= 0.5 / w away from
+  // an integer, far beyond the float rounding error, so the floor is exact
+  const int iy = (int)(((float)al + 0.5f) * __frcp_rn((float)w));
+  const float ax = (float)(al - iy * w) + 0.5f, ay = (float)iy + 0.5f;
   // p: 0 -> x1 = ax - l, 1 -> y1 = ay - t, 2 -> x2 = ax + r, 3 -> y2 = ay + b
   const float base = (p & 1) ? ay : ax;
   const long long i = (long long)n * A + abase + al;
@@ -292,7 +300,9 @@ extern "C" int kv_yolo_decode(const void* f0, const void* f1, const void* f2, in
   auto nb = [](int a) { return (a + kDecAnch - 1) / kDecAnch; };
   const long long g = (long long)N * (nb(h0 * w0) + nb(h1 * w1) + nb(h2 * w2));
   if (g <= 0) return 0;
-  hipLaunchKernelGGL(yolo_decode_kernel, dim3((unsigned)g), dim3(256), lds, s, (const bf16*)f0,
+  if (h0 * w0 >= 65536 || h1 * w1 >= 65536 || h2 * w2 >= 65536) return -3;
+  hipLaunchKernelGGL(nc == 80 ? yolo_decode_kernel<80> : yolo_decode_kernel<0>, dim3((unsigned)g),
+                     dim3(256), lds, s, (const bf16*)f0,
                      (const bf16*)f1, (const bf16*)f2, h0, w0, h1, w1, h2, w2, s0, s1, s2, N, nc,
                      boxes, scores, cls);
   return hipGetLastError() == hipSuccess ? 0 : -100;

@@ -235,10 +235,14 @@ def test_synth_preprocess_bn():
     assert (y.float() - y_ref.float()).abs().max() <= 0.05
 
 
-@pytest.mark.parametrize("hs", [(16, 8, 4), (10, 5, 3)])
-def test_yolo_decode_and_nms(hs):
-    nc = 80
-    feats = [_rand((2, h, h, 64 + nc), 10 + i, 2.0) for i, h in enumerate(hs)]
+@pytest.mark.parametrize("hs,nc", [((16, 8, 4), 80), ((10, 5, 3), 80), ((12, 6, 3), 16),
+                                   (((24, 40), (12, 20), (6, 10)), 80),
+                                   (((9, 13), (5, 7), (3, 4)), 8)])
+def test_yolo_decode_and_nms(hs, nc):
+    """nc = 80 runs the compile-time class-count instantiation, others the generic one;
+    non-square levels exercise the float-reciprocal anchor row/col split."""
+    hw = [h if isinstance(h, tuple) else (h, h) for h in hs]
+    feats = [_rand((2, h, w, 64 + nc), 10 + i, 2.0) for i, (h, w) in enumerate(hw)]
     b_ref, s_ref, c_ref = ops.yolo_decode(feats, (8, 16, 32), nc)
     b, s, c = ops.yolo_decode([f.cuda() for f in feats], (8, 16, 32), nc)
     assert (b.cpu() - b_ref).abs().max() < 2e-2
