@@ -66,79 +66,72 @@ __global__ __launch_bounds__(kBlock) void maxpool_kernel(const bf16* __restrict_
 }
 
 // ---- K5b SPPF: y1 = mp5(x), y2 = mp5(y1) = mp9(x), y3 = mp13(x) ------------
-// Composition of stride-1 max filters with -inf padding is the max over the
-// summed window, so one pass over x produces all three slices exactly.
-// Separable, LDS-resident: one workgroup per (image, 16-channel group) holds the
-// H x W x 16 input slice, the three row-max images (radius 2/4/6) and writes the
-// column maxes of each -- O(13+13) reads per output instead of the 13x13 window scan
-// (the first version read 169 x 16 B per output from global: 155 us at 64x20x20x128).
+// (Composition of stride-1 max filters with -inf padding is the max over the summed
+// window, so chaining gives exactly mp5 / mp9 / mp13 of x.)
+// Separable, LDS-resident, chained: one workgroup per (image, 16-channel group) runs the
+// three 5x5 pools as they are defined (y_k = mp5(y_{k-1})), each as a radius-2 row max
+// into LDS image t and a radius-2 column max back into image a, which then holds y_k and
+// is also written to its global slice.  Two LDS images (not four: x plus the three
+// radius-2/4/6 row-max images of the previous version) -> 2.5x the workgroups per CU, and
+// 5 + 5 reads per output per stage instead of 13 + (5 + 9 + 13) for the whole pass.
 constexpr int kSppfCg = 16;  // channels per workgroup
 __global__ __launch_bounds__(kBlock) void sppf_kernel(bf16* __restrict__ buf, int N, int H,
                                                       int W, int C) {
-  extern __shared__ __attribute__((aligned(16))) bf16 sp[];  // 4 x [H*W][16]
+  extern __shared__ __attribute__((aligned(16))) bf16 sp[];  // 2 x [H*W][16]
   const int HW = H * W;
   const int ncg = C / kSppfCg;
   const int n = blockIdx.x / ncg, cg = blockIdx.x - n * ncg;
   const int ld = 4 * C;
-  bf16* in = sp;
-  bf16* hr[3] = {sp + HW * kSppfCg, sp + 2 * HW * kSppfCg, sp + 3 * HW * kSppfCg};
+  bf16* a = sp;
+  bf16* t = sp + HW * kSppfCg;
   bf16* base = buf + (long long)n * HW * ld + cg * kSppfCg;
   for (int q = threadIdx.x; q < HW * 2; q += kBlock) {  // 2 x 16 B per pixel
     const int pix = q >> 1, hf = q & 1;
-    *reinterpret_cast<bf16x8*>(in + pix * kSppfCg + hf * 8) =
+    *reinterpret_cast<bf16x8*>(a + pix * kSppfCg + hf * 8) =
         *reinterpret_cast<const bf16x8*>(base + (long long)pix * ld + hf * 8);
   }
-  __syncthreads();
-  for (int q = threadIdx.x; q < HW * 2; q += kBlock) {  // row maxes, radius 2 / 4 / 6
-    const int pix = q >> 1, hf = q & 1;
-    const int y = pix / W, x = pix - y * W;
-    float m[3][8];
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) m[k][j] = -INFINITY;
-    for (int dx = -6; dx <= 6; ++dx) {
-      const int xi = x + dx;
-      if ((unsigned)xi >= (unsigned)W) continue;
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(in + (y * W + xi) * kSppfCg + hf * 8);
-      const int ad = dx < 0 ? -dx : dx;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float f = (float)v[j];
-        m[2][j] = fmaxf(m[2][j], f);
-        if (ad <= 4) m[1][j] = fmaxf(m[1][j], f);
-        if (ad <= 2) m[0][j] = fmaxf(m[0][j], f);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      bf16x8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(m[k][j]);
-      *reinterpret_cast<bf16x8*>(hr[k] + pix * kSppfCg + hf * 8) = o;
-    }
-  }
-  __syncthreads();
-  for (int q = threadIdx.x; q < HW * 2; q += kBlock) {  // column maxes -> slices 1..3
-    const int pix = q >> 1, hf = q & 1;
-    const int y = pix / W, x = pix - y * W;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int rad = 2 * (k + 1);
+  // max of bf16 values is exact in bf16: no float round trip needed beyond the compare
+  for (int k = 1; k <= 3; ++k) {
+    __syncthreads();  // a complete (x or y_{k-1})
+    for (int q = threadIdx.x; q < HW * 2; q += kBlock) {  // t = row max, radius 2
+      const int pix = q >> 1, hf = q & 1;
+      const int y = pix / W, x = pix - y * W;
       float m[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
-      for (int dy = -rad; dy <= rad; ++dy) {
-        const int yi = y + dy;
-        if ((unsigned)yi >= (unsigned)H) continue;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(hr[k] + (yi * W + x) * kSppfCg + hf * 8);
+#pragma unroll
+      for (int dx = -2; dx <= 2; ++dx) {
+        const int xi = x + dx;
+        if ((unsigned)xi >= (unsigned)W) continue;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(a + (y * W + xi) * kSppfCg + hf * 8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], (float)v[j]);
       }
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = f2bf(m[j]);
-      *reinterpret_cast<bf16x8*>(base + (long long)pix * ld + (k + 1) * C + hf * 8) = o;
+      *reinterpret_cast<bf16x8*>(t + pix * kSppfCg + hf * 8) = o;
+    }
+    __syncthreads();  // t complete; a no longer read
+    for (int q = threadIdx.x; q < HW * 2; q += kBlock) {  // a = y_k = column max of t
+      const int pix = q >> 1, hf = q & 1;
+      const int y = pix / W, x = pix - y * W;
+      float m[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+#pragma unroll
+      for (int dy = -2; dy <= 2; ++dy) {
+        const int yi = y + dy;
+        if ((unsigned)yi >= (unsigned)H) continue;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(t + (yi * W + x) * kSppfCg + hf * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], (float)v[j]);
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(m[j]);
+      if (k < 3) *reinterpret_cast<bf16x8*>(a + pix * kSppfCg + hf * 8) = o;
+      *reinterpret_cast<bf16x8*>(base + (long long)pix * ld + k * C + hf * 8) = o;
     }
   }
 }
@@ -358,8 +351,8 @@ extern "C" int kv_maxpool2d(const void* x, void* y, int N, int H, int W, int C, 
 
 extern "C" int kv_sppf_pool(void* buf, int N, int H, int W, int C, hipStream_t s) {
   if (C % kSppfCg) return -1;
-  const long long lds = 4LL * H * W * kSppfCg * 2;
-  if (lds > 160 * 1024) return -2;  // 4 LDS images of the 16-channel slice must fit
+  const long long lds = 2LL * H * W * kSppfCg * 2;
+  if (lds > 160 * 1024) return -2;  // 2 LDS images of the 16-channel slice must fit
   const long long g = (long long)N * (C / kSppfCg);
   if (g <= 0) return 0;
   hipLaunchKernelGGL(sppf_kernel, dim3((unsigned)g), dim3(kBlock), (unsigned)lds, s, (bf16*)buf, N,
