@@ -12,6 +12,13 @@ WHOLE-JOB images/sec = world * batch * steps / max_rank_elapsed.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
   torchrun --nproc-per-node N bench.py --gpus N ...
+
+Without a launcher (no WORLD_SIZE in the env) ``--gpus N>1`` makes this process a
+launcher: it counts devices (no HIP initialisation), spawns N fresh ranks of itself
+with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, and exits with the first failing rank's
+code.  After the timed loop every rank replays one batch of frames from a SHARED seed
+and the ranks compare digests of the pre-softmax logits (C4): a replica whose
+weights or kernels drifted fails the run instead of silently skewing it.
 """
 from __future__ import annotations
 
@@ -53,11 +60,27 @@ def main(argv=None):
     ap.add_argument("--native-loop", action="store_true",
                     help="time the K steps with the native C++ serve loop (csrc/runtime) "
                          "instead of Python graph.replay() calls")
-    a = ap.parse_args(argv)
+    ap.add_argument("--perturb-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    raw = list(sys.argv[1:] if argv is None else argv)
+    a = ap.parse_args(raw)
 
     import torch
     from kvedge_amd import ops, parallel
     from kvedge_amd.engine import InferenceEngine
+
+    if a.gpus < 1:
+        print("--gpus must be >= 1", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        if not a.cpu:
+            ndev = torch.cuda.device_count()  # counts only; HIP stays uninitialised here
+            if a.gpus > ndev:
+                print(f"--gpus {a.gpus} but only {ndev} GPU(s) visible", file=sys.stderr)
+                return 2
+        return parallel.launch_local(a.gpus, [os.path.abspath(__file__)] + raw)
+    if int(os.environ.get("WORLD_SIZE", "1")) != a.gpus:
+        print(f"# note: --gpus {a.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')}; "
+              "reporting the launched world size", file=sys.stderr)
 
     di = parallel.init_from_env(prefer_gpu=not a.cpu)
     on_gpu = di.device.type == "cuda"
@@ -87,6 +110,9 @@ def main(argv=None):
         hw = KvYoloV8n.image_size
     # C1: every replica serves rank 0's weights
     parallel.broadcast_tensors(parallel.model_tensors(model), src=0)
+    if a.perturb_rank == di.rank:  # test hook: a drifted replica must fail C4
+        with torch.no_grad():
+            parallel.model_tensors(model)[-1].add_(0.05)
     eng = InferenceEngine(model, a.batch, hw, device=di.device, seed=a.seed + di.rank,
                           use_graph=not a.no_graph)
     eng.prepare(warmup=2, autotune=not a.no_autotune)
@@ -112,13 +138,19 @@ def main(argv=None):
     parallel.barrier()
     sync()
 
-    # C3: job time = slowest rank; C4: replica checksums (sanity, not timed)
+    # C3: job time = slowest rank
     (max_elapsed,) = parallel.allreduce_scalars([elapsed], op="max")
-    out0 = eng.outputs[0]
-    checksum = float(out0.double().sum().item())
-    sums = parallel.all_gather_scalar(checksum)
+    # C4 (untimed): every rank runs the same frames (shared seed, not seed+rank) through
+    # its own weights/kernels; digests of the pre-softmax outputs must agree
+    with torch.no_grad():
+        ops.synth_frames(eng.frames, a.seed, 0)
+        raw_out = model.raw_outputs(eng.frames)
+        local = parallel.digest(raw_out)
+    sync()
+    rc = parallel.check_replicas(local)
+    del raw_out
 
-    world = di.world_size
+    world = parallel.info().world_size
     imgs = world * a.batch * a.steps
     value = imgs / max_elapsed
     ms_per_step = max_elapsed / a.steps * 1e3
@@ -144,6 +176,7 @@ def main(argv=None):
             "seq_len": None,
             "image_size": hw,
             "parallelism": f"dp{world}",
+            "backend": di.backend,
             "hip_graph": eng.graph is not None,
             "microbatch": getattr(model, "microbatch", 0),
             "mb_blocks": getattr(model, "microbatch_blocks", 0),
@@ -151,7 +184,8 @@ def main(argv=None):
         "extra": {
             "tflops_per_gpu": round(value / world * flops / 1e12, 2) if flops else None,
             "build_s": round(build_s, 2),
-            "replica_checksums": sums,
+            "replica_check": {"ok": rc.ok, "max_rel_dev": rc.max_rel_dev,
+                              "digests": rc.digests},
             "backend": di.backend,
             "timed_loop": "native" if lat_hist is not None else "python",
         },
@@ -173,6 +207,10 @@ def main(argv=None):
         print(f"# eager-step profile -> {a.profile}: total {prof['total_ms']:.2f} ms; "
               + ", ".join(f"{k} {v:.2f}" for k, v in top), file=sys.stderr)
     parallel.shutdown()
+    if not rc.ok:
+        print(f"replica check FAILED: max relative deviation {rc.max_rel_dev:.3e} "
+              f"(digests {rc.digests})", file=sys.stderr)
+        return 3
     return 0
 
 

@@ -275,10 +275,14 @@ class KvResNet50:
         pooled = ops.global_avgpool(f).view(B, 1, 1, 2048)
         return self.fc(pooled).view(B, self.num_classes)
 
-    def __call__(self, frames_u8: torch.Tensor, out: Optional[dict] = None):
+    def raw_outputs(self, frames_u8: torch.Tensor) -> torch.Tensor:
+        """uint8 frames -> pre-softmax logits [B, C] (same kernel path as __call__); the
+        cross-replica determinism check (C4) hashes these, not the probabilities."""
         if self.fuse_preprocess and self.fuse_stem_pool and frames_u8.is_cuda:
-            lg = self.logits(frames_u8, frames_in=True)
-        else:
-            lg = self.logits(self.preprocess(frames_u8))
+            return self.logits(frames_u8, frames_in=True)
+        return self.logits(self.preprocess(frames_u8))
+
+    def __call__(self, frames_u8: torch.Tensor, out: Optional[dict] = None):
+        lg = self.raw_outputs(frames_u8)
         probs, top1 = ops.softmax_rows(lg)
         return probs, top1

@@ -344,6 +344,13 @@ class KvYoloV8n:
         p5 = self.h21(cat20)                                       # [N,20,20,256]
         return [lv(p) for lv, p in zip(self.levels, (p3, p4, p5))]
 
+    def raw_outputs(self, frames_u8: torch.Tensor) -> torch.Tensor:
+        """uint8 frames -> the three Detect head maps flattened and concatenated
+        [N, 8400*144] (pre-decode, pre-NMS): what the C4 replica check hashes."""
+        feats = self.heads(self.stem(frames_u8), stem_done=True)
+        N = frames_u8.shape[0]
+        return torch.cat([f.reshape(N, -1) for f in feats], dim=1)
+
     def __call__(self, frames_u8: torch.Tensor):
         feats = self.heads(self.stem(frames_u8), stem_done=True)
         boxes, scores, cls = ops.yolo_decode(feats, STRIDES, self.nc)

@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import os
 from dataclasses import dataclass
-from typing import Iterable, List, Sequence
+from typing import Iterable, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
@@ -40,6 +40,59 @@ _INFO = DistInfo()
 
 def info() -> DistInfo:
     return _INFO
+
+
+def launch_local(nproc: int, argv: Sequence[str], env: Optional[dict] = None,
+                 timeout_s: Optional[float] = None) -> int:
+    """Single-node launcher (the torchrun role, without its agent): start ``nproc``
+    fresh child processes ``python <argv>`` with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set,
+    one per GPU, wait for all, return the first non-zero exit code (0 if all passed).
+
+    The parent must not have touched the GPU (a process that initialised HIP must not
+    be replaced or fork GPU children); it only counts devices.  If one rank fails, the
+    others would block in their next collective, so the survivors are terminated.
+    """
+    import socket
+    import subprocess
+    import sys
+    import time
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    base = dict(os.environ if env is None else env)
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host
+    procs = []
+    for r in range(nproc):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc),
+                 LOCAL_WORLD_SIZE=str(nproc), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=e))
+    rc = 0
+    t_end = None if timeout_s is None else time.monotonic() + timeout_s
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:  # peers would hang in their next collective
+                    q.terminate()
+        if t_end is not None and time.monotonic() > t_end:
+            for q in pending:
+                q.kill()
+            rc = rc or 124
+            break
+        time.sleep(0.05)
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    return rc if rc >= 0 else 128 - rc
 
 
 def init_from_env(prefer_gpu: bool = True) -> DistInfo:
@@ -140,6 +193,48 @@ def all_gather_scalar(x: float) -> List[float]:
     out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
     return [float(o.item()) for o in out]
+
+
+def all_gather_vector(vals: Sequence[float]) -> List[List[float]]:
+    """C4: gather a small fp64 vector per rank -> [world][len(vals)]."""
+    t = torch.tensor(list(vals), dtype=torch.float64, device=_INFO.device)
+    if not is_dist():
+        return [t.cpu().tolist()]
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [o.cpu().tolist() for o in out]
+
+
+def digest(t: torch.Tensor) -> List[float]:
+    """Order-sensitive fp64 digest of a tensor: [sum, sum of squares, position-weighted
+    sum].  The weights (1 + i mod 97) make a permutation or a sign flip visible, which a
+    plain sum (e.g. of softmax probabilities, always == batch) cannot see."""
+    x = t.detach().reshape(-1).double()
+    w = (torch.arange(x.numel(), device=x.device, dtype=torch.float64) % 97) + 1.0
+    return [float(x.sum()), float((x * x).sum()), float((x * w).sum())]
+
+
+@dataclass
+class ReplicaCheck:
+    ok: bool
+    max_rel_dev: float
+    digests: List[List[float]]
+
+
+def check_replicas(local: Sequence[float], rtol: float = 1e-4) -> ReplicaCheck:
+    """C4 cross-replica determinism: every rank computed ``local`` (a :func:`digest`) on
+    the SAME input with its own copy of the weights and kernels; all ranks must agree
+    with rank 0 within ``rtol`` (relative to rank 0's magnitude per component).  Same
+    kernels and the same (fleet-autotuned) tiles on identical hardware are bitwise
+    deterministic, so a deviation means a replica drifted (weights, tile, fault)."""
+    rows = all_gather_vector(local)
+    ref = rows[0]
+    dev = 0.0
+    for r in rows[1:]:
+        for a, b in zip(r, ref):
+            dev = max(dev, abs(a - b) / max(abs(b), 1e-30))
+    finite = all(x == x and abs(x) != float("inf") for r in rows for x in r)
+    return ReplicaCheck(finite and dev <= rtol, dev, rows)
 
 
 def model_tensors(model) -> List[torch.Tensor]:

@@ -42,4 +42,48 @@ def test_bench_dp_contract_gloo(world):
     assert res["config"]["global_batch"] == world * res["config"]["per_gpu_batch"]
     assert res["value"] > 0 and "NOT a measurement" in res["data"]
     assert res["extra"]["backend"] == "gloo"
-    assert len(res["extra"]["replica_checksums"]) == world
+    rc = res["extra"]["replica_check"]
+    assert rc["ok"] and len(rc["digests"]) == world and rc["max_rel_dev"] == 0.0
+
+
+def _run_bench(args, timeout=900):
+    env = dict(os.environ, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    env.pop("WORLD_SIZE", None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args,
+                          capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+
+
+def test_bench_self_launch_gpus4():
+    """No torchrun: ``--gpus 4`` spawns four ranks itself."""
+    r = _run_bench(["--cpu", "--gpus", "4", "--steps", "1", "--warmup", "0"])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 4 and res["extra"]["backend"] == "gloo"
+    assert res["config"]["parallelism"] == "dp4" and res["config"]["backend"] == "gloo"
+    rc = res["extra"]["replica_check"]
+    assert rc["ok"] and len(rc["digests"]) == 4
+    # all four replicas hashed the same shared-seed frames through identical weights
+    assert all(d == rc["digests"][0] for d in rc["digests"])
+
+
+def test_bench_replica_check_catches_drift():
+    """C4 is not vacuous: one rank with perturbed weights fails the run (exit 3)."""
+    r = _run_bench(["--cpu", "--gpus", "2", "--steps", "1", "--warmup", "0",
+                    "--perturb-rank", "1"])
+    assert r.returncode == 3, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "replica check FAILED" in r.stderr
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert res["extra"]["replica_check"]["ok"] is False
+    assert res["extra"]["replica_check"]["max_rel_dev"] > 1e-3
+
+
+def test_bench_rejects_bad_gpus():
+    r = _run_bench(["--cpu", "--gpus", "0"], timeout=300)
+    assert r.returncode == 2 and "--gpus must be" in r.stderr
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    r = _run_bench(["--gpus", "2"], timeout=300)  # no --cpu; this host sees 0 GPUs
+    assert r.returncode == 2 and "GPU(s) visible" in r.stderr
