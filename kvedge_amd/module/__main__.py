@@ -35,25 +35,26 @@ def main(argv=None):
     ap.add_argument("--steps-per-poll", type=int, default=d.steps_per_poll)
     ap.add_argument("--steps", type=int, default=None, help="stop after N steps")
     ap.add_argument("--duration-s", type=float, default=None)
+    ap.add_argument("--sync-every", type=int, default=d.sync_every,
+                    help="module steps between lockstep control boundaries (0 = auto)")
     ap.add_argument("--state", default=os.environ.get("KVEDGE_STATE", "/var/lib/kvedge/module-state.json"))
+    ap.add_argument("--stamps", default=os.environ.get("KVEDGE_STAMPS", "/var/lib/kvedge/boot-timing"),
+                    help="guest boot-timing stamp file (module_first_inference is appended)")
     a = ap.parse_args(argv)
     di = parallel.init_from_env(prefer_gpu=True)
     cfg = ModuleConfig(model=a.model, batch=a.batch, dtype=a.dtype, seed=a.seed,
                        report_interval_s=a.report_interval_s, image_size=a.image_size,
                        fps=a.fps, use_graph=not a.no_graph, world_size=di.world_size,
                        source=a.source, native_loop=not a.no_native_loop,
-                       steps_per_poll=a.steps_per_poll).validate()
-    app = ModuleApp(make_transport(a.transport), cfg, state_path=a.state)
-    stop = {"flag": False}
-    signal.signal(signal.SIGTERM, lambda *_: stop.update(flag=True))
+                       steps_per_poll=a.steps_per_poll, sync_every=a.sync_every).validate()
+    app = ModuleApp(make_transport(a.transport), cfg, state_path=a.state,
+                    stamp_path=a.stamps or None)
+    # SIGTERM (edgeAgent stop, VM shutdown) only votes to stop: the replicas leave the
+    # loop together at the next control boundary, so the final report's collectives match
+    signal.signal(signal.SIGTERM, lambda *_: app.request_stop())
     app.start()
     try:
-        n = 0
-        while not stop["flag"] and (a.steps is None or n < a.steps):
-            app.run(max_steps=1)
-            n += 1
-            if a.duration_s is not None and n and app.clock() - app._win_t0 > a.duration_s:
-                break
+        app.run(max_steps=a.steps, duration_s=a.duration_s)
         if app.engine is not None:
             app.report()
     finally:

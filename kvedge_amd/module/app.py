@@ -12,25 +12,37 @@ but the workload is ResNet-50 / YOLOv8n on the passed-through MI355X:
              With world_size > 1 the throughput counters are all-reduced over RCCL (C2)
              and rank 0 reports the job total.
   twin patch: validated; engine rebuilt only if a REBUILD key changed; reported props
-             updated; invalid patches are rejected and reported, never crash the loop.
+             updated; invalid patches are rejected and reported, never crash the loop;
+             a rebuild that fails (e.g. out of HBM) rolls back to the previous config
+             and reports ``lastError``.
   direct methods: benchmark {steps, warmup}, getStatus, reconfigure {...}, ping.
+
+Multi-replica lockstep (world_size > 1, one rank per GPU/VM).  Every collective a rank
+issues must be issued by every other rank in the same order, but twin patches, method
+calls, report timers and SIGTERM are per-rank events.  So handlers only QUEUE events;
+every ``sync_every`` module steps all ranks meet at a control boundary, all-gather their
+queues and stop flags (one small object collective) and then apply the union in rank
+order -- rebuilds (weight broadcast), ``benchmark`` (throughput all-reduce), the
+telemetry report (rank 0's clock decides) and shutdown happen on every rank together.
+Methods that need no collective (ping, getStatus) are answered immediately; the others
+reply (``transport.Deferred``) once the boundary has run them.
   model "simulated-temperature": the reference demo's CPU-only plumbing workload
              (BASELINE config 1) -- machine/ambient temperature/pressure/humidity.
 """
 from __future__ import annotations
 
 import json
-import math
 import os
 import random
 import time
-from typing import Any, Dict, Optional, Tuple
+from dataclasses import replace
+from typing import Any, Dict, List, Optional, Tuple
 
 import torch
 
 from .. import ops, parallel
 from .config import ModuleConfig
-from .transport import Transport, now_iso
+from .transport import Deferred, Transport, now_iso
 
 
 class _SimTempModel:
@@ -90,11 +102,14 @@ class _CameraSource:
 class ModuleApp:
     def __init__(self, transport: Transport, config: Optional[ModuleConfig] = None,
                  device: Optional[str] = None, state_path: Optional[str] = None,
-                 clock=time.perf_counter):
+                 clock=time.perf_counter, stamp_path: Optional[str] = None):
         self.tr = transport
         self.cfg = (config or ModuleConfig()).validate()
         self.device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
         self.state_path = state_path
+        # guest boot-timing stamp file (chart cloud-init writes the same file); the module
+        # adds ``module_first_inference`` -- one leg of the boot-to-ready headline
+        self.stamp_path = stamp_path
         self.clock = clock
         self.engine = None
         self.model = None
@@ -102,7 +117,7 @@ class ModuleApp:
         self.camera: Optional[_CameraSource] = None
         self.sim: Optional[_SimTempModel] = None
         self.state = {"total_images": 0, "total_steps": 0, "restarts": 0, "rebuilds": 0,
-                      "rejected_patches": 0, "messages": 0}
+                      "rejected_patches": 0, "failed_rebuilds": 0, "messages": 0}
         self._win_imgs = 0
         self._win_t0 = 0.0
         self._lat_ms = []
@@ -116,8 +131,17 @@ class ModuleApp:
             self._hist = LatencyHistogram()
         self._last_report = 0.0
         self.last_telemetry: Optional[Dict[str, Any]] = None
+        self.last_error: Optional[str] = None
         self.rank = parallel.info().rank
         self.world = parallel.info().world_size
+        # lockstep control plane
+        self._events: List[Tuple[str, Any]] = []      # queued since the last boundary
+        self._replies: List[Optional[Deferred]] = []  # parallel to _events (own rank)
+        self._tick = 0
+        self._stop_req = False
+        self.sync_every = 1
+        self.boundaries = 0
+        self._first_inference_stamped = False
 
     # ---------------------------------------------------------------- lifecycle
     def start(self):
@@ -130,11 +154,24 @@ class ModuleApp:
         except (ValueError, TypeError) as e:
             self.state["rejected_patches"] += 1
             self.tr.patch_reported({"lastError": f"invalid desired properties: {e}"})
+        if self.world > 1:
+            # one model config fleet-wide (the weights are rank 0's): adopt rank 0's
+            cfgs = parallel.all_gather_object(self.cfg.to_dict())
+            if cfgs[0] != self.cfg.to_dict():
+                self.cfg = ModuleConfig(**cfgs[0]).validate()
+        self.sync_every = self.cfg.sync_every or (1 if self.world == 1 else 16)
         self._load_state()
-        self._build()
+        err = self._build_fleet()
+        if err is not None:
+            self.tr.patch_reported({"status": "failed", "lastError": err})
+            raise RuntimeError(f"module build failed: {err}")
         self._report_config()
         self._win_t0 = self._last_report = self.clock()
         return self
+
+    def request_stop(self):
+        """Signal-safe: the fleet stops together at the next control boundary."""
+        self._stop_req = True
 
     def stop(self):
         self._stop_camera()
@@ -167,12 +204,25 @@ class ModuleApp:
             json.dump(dict(self.state, config=self.cfg.to_dict(), ts=now_iso()), f)
         os.replace(tmp, self.state_path)  # atomic on the persistent disk
 
-    def _build(self):
+    def _stamp(self, name: str):
+        if not self.stamp_path:
+            return
+        try:
+            os.makedirs(os.path.dirname(self.stamp_path) or ".", exist_ok=True)
+            with open(self.stamp_path, "a") as f:
+                f.write(f"{name} {time.time():.6f}\n")
+        except OSError:
+            pass  # read-only / missing mount: timing is best-effort, never fatal
+
+    def _build_local(self):
+        """Build model + engine for self.cfg on this rank (no collectives)."""
         cfg = self.cfg
         self._stop_camera()
         self.engine = None
         self.model = None
         self.sim = None
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
         if cfg.model == "simulated-temperature":
             self.sim = _SimTempModel(cfg.seed)
             return
@@ -189,8 +239,6 @@ class ModuleApp:
 
             self.model = KvYoloV8n(init_yolov8n(cfg.seed, calibrate=dev.type == "cuda"), dev,
                                    conf=cfg.conf, iou=cfg.iou, max_det=cfg.max_det)
-        if self.world > 1:
-            parallel.broadcast_tensors(parallel.model_tensors(self.model), src=0)
         camera = cfg.source == "camera"
         self.engine = InferenceEngine(self.model, cfg.batch, cfg.resolved_image_size(), device=dev,
                                       seed=cfg.seed + self.rank, use_graph=cfg.use_graph,
@@ -203,17 +251,56 @@ class ModuleApp:
             self.camera = _CameraSource(self.ring, cfg.batch, cfg.resolved_image_size(), cfg.fps,
                                         cfg.seed + self.rank)
 
+    def _build_fleet(self, previous: Optional[ModuleConfig] = None) -> Optional[str]:
+        """Build on every rank; if ANY rank failed (HBM exhausted, bad shape), every rank
+        rolls back to ``previous`` so the replicas stay identical.  Collective-safe:
+        called by all ranks at the same boundary.  Returns the error (None = ok)."""
+        err = None
+        try:
+            self._build_local()
+        except Exception as e:  # noqa: BLE001 -- any build failure must be survivable
+            err = f"rank {self.rank}: {type(e).__name__}: {e}"
+        errs = parallel.all_gather_object(err) if self.world > 1 else [err]
+        err = next((e for e in errs if e), None)
+        if err is not None:
+            self.engine = self.model = None
+            self.sim = None
+            self._stop_camera()
+            if previous is None:
+                return err
+            self.state["failed_rebuilds"] += 1
+            self.cfg = previous
+            back = self._build_fleet(None)  # the previous config built before
+            if back is not None:
+                return f"{err}; rollback failed: {back}"
+            self.last_error = f"rebuild failed, rolled back: {err}"
+            self.tr.patch_reported({"lastError": self.last_error})
+            return None
+        if self.world > 1 and self.model is not None:
+            parallel.broadcast_tensors(parallel.model_tensors(self.model), src=0)  # C1
+        return None
+
     def _report_config(self):
         self.tr.patch_reported({"config": self.cfg.to_dict(), "status": "running",
                                 "device": str(self.device), "rank": self.rank,
-                                "world_size": self.world, "restarts": self.state["restarts"]})
+                                "world_size": self.world, "restarts": self.state["restarts"],
+                                "sync_every": self.sync_every})
 
     # ---------------------------------------------------------------- main loop
-    def step(self) -> None:
+    def step(self, want_stop: bool = False) -> bool:
+        """One module step.  Returns True when the fleet decided (at a control
+        boundary) to stop; ``want_stop`` is this rank's vote."""
         self.tr.poll()
         if self.sim is not None:
             self._sim_step()
-            return
+        elif self.engine is not None:
+            self._infer_step()
+        self._tick += 1
+        if self._tick % self.sync_every == 0:
+            return self._boundary(want_stop or self._stop_req)
+        return False
+
+    def _infer_step(self):
         native = (self.cfg.native_loop and self.engine.graph is not None and
                   self._hist is not None)
         t0 = self.clock()
@@ -242,12 +329,13 @@ class ModuleApp:
         self._win_imgs += self.cfg.batch * nsteps
         self.state["total_images"] += self.cfg.batch * nsteps
         self.state["total_steps"] += nsteps
+        if not self._first_inference_stamped and nsteps > 0:
+            self._first_inference_stamped = True
+            self._stamp("module_first_inference")
         if self.cfg.fps > 0 and self.ring is None:
             budget = self.cfg.batch / self.cfg.fps
             if dt < budget:
                 time.sleep(budget - dt)
-        if self.clock() - self._last_report >= self.cfg.report_interval_s:
-            self.report()
 
     def _sim_step(self):
         now = self.clock()
@@ -257,14 +345,45 @@ class ModuleApp:
                 self.state["messages"] += 1
                 self._last_report = now
                 self._save_state()
+                if not self._first_inference_stamped:
+                    self._first_inference_stamped = True
+                    self._stamp("module_first_message")
 
-    def run(self, max_steps: Optional[int] = None, duration_s: Optional[float] = None):
+    def _boundary(self, want_stop: bool) -> bool:
+        """Lockstep control boundary (all ranks, same tick)."""
+        self.boundaries += 1
+        report_due = (self.engine is not None and
+                      self.clock() - self._last_report >= self.cfg.report_interval_s)
+        mine = {"events": self._events, "stop": bool(want_stop), "report": report_due}
+        replies, self._events, self._replies = self._replies, [], []
+        fleet = parallel.all_gather_object(mine)
+        for r, part in enumerate(fleet):
+            for k, (kind, data) in enumerate(part["events"]):
+                res = self._apply(kind, data)
+                if r == self.rank and replies[k] is not None:
+                    replies[k].resolve(*res)
+        if fleet[0]["report"] and self.engine is not None:
+            self.report()  # rank 0's clock decides, every rank all-reduces together
+        return any(p["stop"] for p in fleet)
+
+    def _apply(self, kind: str, data: Any) -> Tuple[int, Dict[str, Any]]:
+        if kind == "twin":
+            return self._apply_patch(data)
+        if kind == "benchmark":
+            return self._benchmark(data)
+        return 404, {"error": f"unknown event {kind}"}
+
+    def run(self, max_steps: Optional[int] = None, duration_s: Optional[float] = None) -> int:
+        """Step until this rank wants to stop (max_steps / duration / request_stop) AND
+        the fleet agrees at a control boundary.  World 1: a boundary every step."""
         t_end = None if duration_s is None else self.clock() + duration_s
         n = 0
-        while (max_steps is None or n < max_steps) and (t_end is None or self.clock() < t_end):
-            self.step()
+        while True:
             n += 1
-        return n
+            want = (self._stop_req or (max_steps is not None and n >= max_steps) or
+                    (t_end is not None and self.clock() >= t_end))
+            if self.step(want_stop=want):
+                return n
 
     def _summary(self) -> Dict[str, Any]:
         now = self.clock()
@@ -280,6 +399,8 @@ class ModuleApp:
                 "steps": len(lat)}
 
     def report(self) -> Dict[str, Any]:
+        """Telemetry.  Collective at world > 1: call it only from a control boundary or
+        after run() returned (every rank returns from the same boundary)."""
         s = self._summary()
         ips_total, lat_max = s["images_per_s"], s["p99_ms"]
         if self.world > 1:  # C2 + C3 off the hot path, once per report interval
@@ -324,45 +445,67 @@ class ModuleApp:
         return {"detections": {"total": int(cnt.sum()), "max_per_image": int(cnt.max())}}
 
     # ---------------------------------------------------------------- handlers
+    # Handlers run on the module thread from transport.poll(); they only queue work
+    # that may involve collectives, to be applied at the next control boundary.
     def on_twin_patch(self, patch: Dict[str, Any]):
+        self._events.append(("twin", dict(patch or {})))
+        self._replies.append(None)
+
+    def _apply_patch(self, patch: Dict[str, Any]) -> Tuple[int, Dict[str, Any]]:
         try:
             new = self.cfg.apply_patch(patch)
         except (ValueError, TypeError) as e:
             self.state["rejected_patches"] += 1
             self.tr.patch_reported({"lastError": f"rejected patch: {e}"})
-            return
-        rebuild = new.needs_rebuild(self.cfg)
-        self.cfg = new
-        if rebuild:
+            return 400, {"error": f"rejected patch: {e}"}
+        old = self.cfg
+        self.cfg = replace(new, world_size=old.world_size, sync_every=old.sync_every)
+        if self.cfg.needs_rebuild(old):
             self.state["rebuilds"] += 1
-            self._build()
+            err = self._build_fleet(previous=old)
+            if err is not None:  # even the rollback failed: nothing left to serve
+                self.tr.patch_reported({"status": "failed", "lastError": err})
+                return 500, {"error": err}
+            if self.cfg is old:  # rolled back
+                self._report_config()
+                return 409, {"error": self.last_error, "config": self.cfg.to_dict()}
         self._report_config()
+        return 200, {"config": self.cfg.to_dict()}
 
-    def on_method(self, name: str, payload: Dict[str, Any]) -> Tuple[int, Dict[str, Any]]:
+    def _benchmark(self, payload: Dict[str, Any]) -> Tuple[int, Dict[str, Any]]:
+        if self.engine is None:
+            return 400, {"error": "no inference engine for model " + self.cfg.model}
+        try:
+            steps = max(1, int(payload.get("steps", 20)))
+            warm = max(0, int(payload.get("warmup", 3)))
+        except (TypeError, ValueError) as e:
+            return 400, {"error": f"bad payload: {e}"}
+        for _ in range(warm):
+            self.engine.run()
+        dt = self.engine.run_timed(steps)
+        lat = self.engine.measure_latency(min(steps, 20))
+        ips = steps * self.cfg.batch / dt
+        if self.world > 1:  # every rank is here (same boundary): lockstep all-reduce
+            ips = parallel.allreduce_scalars([ips], op="sum")[0]
+        return 200, {"images_per_s": round(ips, 2), "steps": steps, "world_size": self.world,
+                     "batch": self.cfg.batch, "p50_ms": round(lat.percentile(50), 3),
+                     "p99_ms": round(lat.percentile(99), 3)}
+
+    def on_method(self, name: str, payload: Dict[str, Any]):
         try:
             if name == "ping":
-                return 200, {"pong": now_iso()}
+                return 200, {"pong": now_iso(), "rank": self.rank}
             if name == "getStatus":
                 return 200, {"config": self.cfg.to_dict(), "state": dict(self.state),
-                             "last_telemetry": self.last_telemetry}
-            if name == "reconfigure":
-                self.on_twin_patch(payload)
-                return 200, {"config": self.cfg.to_dict()}
-            if name == "benchmark":
-                if self.engine is None:
-                    return 400, {"error": "no inference engine for model " + self.cfg.model}
-                steps = int(payload.get("steps", 20))
-                warm = int(payload.get("warmup", 3))
-                for _ in range(warm):
-                    self.engine.run()
-                dt = self.engine.run_timed(steps)
-                lat = self.engine.measure_latency(min(steps, 20))
-                ips = steps * self.cfg.batch / dt
-                if self.world > 1:
-                    ips = parallel.allreduce_scalars([ips], op="sum")[0]
-                return 200, {"images_per_s": round(ips, 2), "steps": steps,
-                             "batch": self.cfg.batch, "p50_ms": round(lat.percentile(50), 3),
-                             "p99_ms": round(lat.percentile(99), 3)}
+                             "last_telemetry": self.last_telemetry,
+                             "last_error": self.last_error, "rank": self.rank,
+                             "world_size": self.world}
+            if name in ("reconfigure", "benchmark"):
+                d = Deferred()
+                self._events.append(("twin" if name == "reconfigure" else "benchmark",
+                                     dict(payload or {})))
+                self._replies.append(d)
+                return d
             return 404, {"error": f"unknown method {name}"}
         except Exception as e:  # a bad method call must not kill the module
             return 500, {"error": repr(e)}

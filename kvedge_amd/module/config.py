@@ -35,6 +35,11 @@ class ModuleConfig:
     source: str = "synthetic"
     native_loop: bool = True     # GPU: replay the graph from the C++ serve loop
     steps_per_poll: int = 1      # graph replays per module step (native loop)
+    # multi-replica lockstep: module steps between control boundaries (0 = auto: every
+    # step at world 1, 16 otherwise).  Twin patches, collective direct methods, report
+    # decisions and stop requests are exchanged ONLY at these boundaries, so every rank
+    # issues the same collectives in the same order.  Rank 0's value wins fleet-wide.
+    sync_every: int = 0
     # SimulatedTemperatureSensor compatibility (BASELINE config 1, CPU-only plumbing)
     send_interval_s: float = 5.0
     max_messages: int = 500
@@ -64,6 +69,8 @@ class ModuleConfig:
             raise ValueError(f"source must be one of {SOURCES}, got {self.source!r}")
         if not 1 <= self.steps_per_poll <= 1000:
             raise ValueError("steps_per_poll must be 1..1000")
+        if not 0 <= self.sync_every <= 10000:
+            raise ValueError("sync_every must be 0..10000")
         return self
 
     def apply_patch(self, patch: Dict[str, Any]) -> "ModuleConfig":

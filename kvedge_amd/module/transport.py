@@ -19,7 +19,43 @@ import time
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
 TwinHandler = Callable[[Dict[str, Any]], None]
-MethodHandler = Callable[[str, Dict[str, Any]], Tuple[int, Dict[str, Any]]]
+
+
+class Deferred:
+    """A direct-method reply that is produced later.  A multi-replica module answers a
+    method that needs collectives (e.g. ``benchmark``) only at the next lockstep
+    boundary, when every rank runs it together; IoT Hub keeps the caller waiting until
+    the response arrives (up to the method's responseTimeoutInSeconds)."""
+
+    def __init__(self):
+        self._result: Optional[Tuple[int, Dict[str, Any]]] = None
+        self._sink: Optional[Callable[[int, Dict[str, Any]], None]] = None
+
+    def bind(self, sink: Callable[[int, Dict[str, Any]], None]) -> None:
+        self._sink = sink
+        if self._result is not None:
+            sink(*self._result)
+
+    def resolve(self, status: int, res: Dict[str, Any]) -> None:
+        if self._result is not None:
+            return
+        self._result = (status, res)
+        if self._sink is not None:
+            self._sink(status, res)
+
+    @property
+    def done(self) -> bool:
+        return self._result is not None
+
+
+MethodHandler = Callable[[str, Dict[str, Any]], "Tuple[int, Dict[str, Any]] | Deferred"]
+
+
+def _deliver(result, sink: Callable[[int, Dict[str, Any]], None]) -> None:
+    if isinstance(result, Deferred):
+        result.bind(sink)
+    else:
+        sink(*result)
 
 
 class Transport:
@@ -101,8 +137,9 @@ class FakeTransport(Transport):
             if kind == "twin" and self._twin_cb:
                 self._twin_cb(data)
             elif kind == "method" and self._method_cb:
-                status, res = self._method_cb(*data)
-                self.method_results.append((data[0], status, res))
+                name = data[0]
+                _deliver(self._method_cb(*data),
+                         lambda st, res, n=name: self.method_results.append((n, st, res)))
 
     def outputs(self, name: str) -> List[Dict[str, Any]]:
         with self._lock:
@@ -173,9 +210,9 @@ class AzureIoTTransport(Transport):
             if kind == "twin" and self._twin_cb:
                 self._twin_cb(data)
             elif kind == "method" and self._method_cb:
-                status, res = self._method_cb(data.name, data.payload or {})
-                self.client.send_method_response(
-                    self._MethodResponse.create_from_method_request(data, status, res))
+                _deliver(self._method_cb(data.name, data.payload or {}),
+                         lambda st, res, req=data: self.client.send_method_response(
+                             self._MethodResponse.create_from_method_request(req, st, res)))
 
 
 def make_transport(kind: str, desired: Optional[Dict[str, Any]] = None) -> Transport:

@@ -205,6 +205,16 @@ def all_gather_vector(vals: Sequence[float]) -> List[List[float]]:
     return [o.cpu().tolist() for o in out]
 
 
+def all_gather_object(obj) -> list:
+    """Gather one small picklable control object per rank (module lockstep boundary:
+    queued twin patches / method calls, stop flags).  Identity at world size 1."""
+    if not is_dist():
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def digest(t: torch.Tensor) -> List[float]:
     """Order-sensitive fp64 digest of a tensor: [sum, sum of squares, position-weighted
     sum].  The weights (1 + i mod 97) make a permutation or a sign flip visible, which a

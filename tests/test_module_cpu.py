@@ -114,3 +114,38 @@ def test_camera_source_ring_feeds_engine(tmp_path):
     app.run(max_steps=1)
     assert app.ring is None and app.camera is None and app.engine.synthetic
     app.stop()
+
+
+def test_failed_rebuild_rolls_back_and_stamps(tmp_path):
+    """A rebuild that raises (e.g. batch 4096 exhausts HBM) must not kill the module:
+    previous config restored, engine serving, lastError reported.  The first inference
+    appends ``module_first_inference`` to the guest boot-timing stamp file."""
+    stamps = tmp_path / "boot-timing"
+    tr = FakeTransport({"model": "resnet50", "batch": 2, "report_interval_s": 1.0,
+                        "image_size": 64})
+    app = ModuleApp(tr, device="cpu", clock=Clock(), stamp_path=str(stamps)).start()
+    orig = app._build_local
+
+    def build():
+        if app.cfg.batch == 4096:
+            raise RuntimeError("HIP out of memory (injected)")
+        orig()
+
+    app._build_local = build
+    app.run(max_steps=2)
+    assert stamps.read_text().startswith("module_first_inference ")
+    eng = app.engine
+    tr.push_twin_patch({"batch": 4096})
+    app.run(max_steps=1)
+    assert app.cfg.batch == 2 and app.engine is not None and app.engine is not eng
+    assert "rolled back" in tr.reported["lastError"] and app.state["failed_rebuilds"] == 1
+    assert tr.reported["config"]["batch"] == 2 and tr.reported["status"] == "running"
+    tr.invoke_method("reconfigure", {"batch": 4096})
+    app.run(max_steps=2)
+    res = {n: (s, r) for n, s, r in tr.method_results}
+    assert res["reconfigure"][0] == 409 and app.cfg.batch == 2
+    n0 = app.state["total_images"]
+    app.run(max_steps=2)
+    assert app.state["total_images"] == n0 + 4  # still serving
+    assert stamps.read_text().count("module_first_inference") == 1
+    app.stop()

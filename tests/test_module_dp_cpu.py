@@ -1,0 +1,123 @@
+"""T-module x T-dist: the edge module with 4 replicas (gloo, one process per rank) stays
+in lockstep when events hit only SOME ranks (VERDICT r1 weak #5 / ADVICE high):
+
+  * a ``benchmark`` direct method and a rebuilding ``batch`` twin patch arrive on rank 2
+    only, mid-run;
+  * a patch that fails to build on rank 3 only (injected) must roll EVERY rank back;
+  * the per-rank report clocks disagree (rank r's clock runs r+1 times faster);
+  * one rank asks to stop earlier than the others.
+
+Before the control-boundary design any of these hung the job in a collective.  The test
+passes if every rank exits, agrees on the final config and rank 2 got its reply.
+"""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+WORLD = 4
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q, tmp):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+
+    torch.set_num_threads(1)
+    from kvedge_amd import parallel
+    from kvedge_amd.module.app import ModuleApp
+    from kvedge_amd.module.config import ModuleConfig
+    from kvedge_amd.module.transport import FakeTransport
+
+    class Scripted(FakeTransport):
+        """Pushes scripted events into this rank's queue on given poll() calls."""
+
+        def __init__(self, desired, script):
+            super().__init__(desired)
+            self.script, self.polls = script, 0
+
+        def poll(self):
+            self.polls += 1
+            for ev in self.script.get(self.polls, []):
+                if ev[0] == "twin":
+                    self.push_twin_patch(ev[1])
+                else:
+                    self.invoke_method(ev[1], ev[2])
+            super().poll()
+
+    class Clock:  # per-rank clock speeds: report timers disagree across ranks
+        def __init__(self):
+            self.t = 0.0
+
+        def __call__(self):
+            self.t += 0.1 * (rank + 1)
+            return self.t
+
+    script = {}
+    if rank == 2:
+        script = {3: [("method", "benchmark", {"steps": 1, "warmup": 0}),
+                      ("twin", {"batch": 2})],
+                  7: [("method", "reconfigure", {"batch": 3})]}
+    tr = Scripted({"model": "resnet50", "batch": 1, "image_size": 64,
+                   "report_interval_s": 0.5}, script)
+    cfg = ModuleConfig(world_size=world, sync_every=2, use_graph=False)
+    di = parallel.init_from_env(prefer_gpu=False)
+    app = ModuleApp(tr, cfg, device="cpu", state_path=os.path.join(tmp, f"s{rank}.json"),
+                    clock=Clock())
+    if rank == 3:  # batch 3 cannot be built on rank 3 (e.g. its HBM is exhausted)
+        orig = app._build_local
+
+        def failing():
+            if app.cfg.batch == 3:
+                raise RuntimeError("injected: out of memory")
+            orig()
+
+        app._build_local = failing
+    try:
+        app.start()
+        n = app.run(max_steps=10 if rank == 1 else 40)
+        app.report()  # final collective report: every rank left run() at one boundary
+        res = {n_: (s, r) for n_, s, r in tr.method_results}
+        q.put((rank, n, app.cfg.batch, app.boundaries, app.state["rebuilds"],
+               app.state["failed_rebuilds"], res, tr.reported.get("lastError", ""),
+               len(tr.outputs("telemetry")), di.world_size))
+    finally:
+        parallel.shutdown()
+
+
+@pytest.mark.timeout(600)
+def test_module_lockstep_4_ranks(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, str(tmp_path)))
+             for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=500) for _ in range(WORLD))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    steps = {r[1] for r in res}
+    assert len(steps) == 1, f"ranks left the loop at different steps: {res}"
+    n = steps.pop()
+    assert n == 10  # rank 1 voted to stop at step 10: everyone left at that boundary
+    # every rank applied rank 2's batch patch, and rolled back the failing batch=3 together
+    assert [r[2] for r in res] == [2] * WORLD
+    assert all(r[4] == 2 and r[5] == 1 for r in res)
+    assert all(r[3] == n // 2 for r in res)
+    r2 = res[2][6]
+    assert r2["benchmark"][0] == 200 and r2["benchmark"][1]["world_size"] == WORLD
+    assert r2["reconfigure"][0] == 409 and "injected" in r2["reconfigure"][1]["error"]
+    assert all("rolled back" in r[7] for r in res)
+    # only rank 0 emits telemetry (job totals)
+    assert res[0][8] >= 1 and all(r[8] == 0 for r in res[1:])
