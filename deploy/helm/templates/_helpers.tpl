@@ -45,6 +45,14 @@ app.kubernetes.io/part-of: kvedge
      the truncated name instead of the invalid "-vm-cloudconfig" when it is empty. */}}
 {{- define "kvedge.ciSecret" -}}{{ default (include "kvedge.name" .root) .root.Values.nameOverride }}-vm-cloudconfig{{ include "kvedge.sfx" . }}{{- end -}}
 
+{{/* Multi-VM data parallelism active: dp.enabled and more than one VM. */}}
+{{- define "kvedge.dpActive" -}}
+{{- if and .Values.dp.enabled (gt (int .Values.replicas) 1) }}true{{ end -}}
+{{- end -}}
+{{- define "kvedge.rdzvName" -}}{{ include "kvedge.name" . }}-dp-rendezvous{{- end -}}
+{{/* ranks per VM (one per passed-through GPU, at least 1) */}}
+{{- define "kvedge.ranksPerVm" -}}{{ max 1 (int .Values.gpu.count) }}{{- end -}}
+
 {{- define "kvedge.replicaConfig" -}}
 {{- $cfgs := .root.Values.replicaConfigs | default list -}}
 {{- if lt (int .i) (len $cfgs) }}{{ index $cfgs (int .i) }}{{ else }}{{ .root.Values.azIotEdgeConfig }}{{ end -}}
@@ -69,8 +77,10 @@ cloud-init user-data (GPU-aware).  Context: (dict "root" $ "i" $i)
 {{- $v := .root.Values -}}
 #cloud-config
 hostname: {{ $v.guest.hostname }}{{ include "kvedge.sfx" . }}
+{{- if $v.publicSshKey }}
 ssh_authorized_keys:
   - {{ $v.publicSshKey }}
+{{- end }}
 {{- if not $v.image.prebaked }}
 apt:
   sources:
@@ -92,17 +102,32 @@ write_files:
     permissions: "0755"
     content: |
       #!/bin/sh
-      # Install /mnt/app-secret/userdata as /etc/aziot/config.toml when it changed,
-      # then `iotedge config apply`.  Safe to run on every boot.
+      # Apply /mnt/app-secret/userdata as the IoT Edge config.  Safe on every boot.
+      # The new file is staged and only moved to /etc/aziot/config.toml AFTER
+      # `iotedge config apply` accepted it; the applied content's hash is recorded, so
+      # a failed apply (iotedge not ready yet) is retried on the next run instead of
+      # being skipped because the destination already matches.
       set -eu
       src=/mnt/app-secret/userdata
       dst=/etc/aziot/config.toml
+      mark=/var/lib/kvedge/config.applied
       [ -s "$src" ] || { echo "kvedge: no config on secret disk"; exit 0; }
-      mkdir -p /etc/aziot
-      if [ ! -f "$dst" ] || ! cmp -s "$src" "$dst"; then
-        install -m 0600 "$src" "$dst"
-        if command -v iotedge >/dev/null 2>&1; then iotedge config apply -c "$dst"; fi
+      mkdir -p /etc/aziot /var/lib/kvedge
+      want=$(sha256sum "$src" | cut -d' ' -f1)
+      if [ -f "$mark" ] && [ "$(cat "$mark")" = "$want" ] && [ -f "$dst" ]; then
+        /usr/local/sbin/kvedge-stamp config_applied
+        exit 0
       fi
+      command -v iotedge >/dev/null 2>&1 || { echo "kvedge: iotedge not installed yet"; exit 1; }
+      tmp="$dst.kvedge-new"
+      install -m 0600 "$src" "$tmp"
+      if ! iotedge config apply -c "$tmp"; then
+        rm -f "$tmp"
+        echo "kvedge: iotedge config apply failed; will retry"
+        exit 1
+      fi
+      mv -f "$tmp" "$dst"
+      echo "$want" > "$mark"
       /usr/local/sbin/kvedge-stamp config_applied
   - path: /usr/local/sbin/kvedge-gpu-check
     permissions: "0755"
@@ -121,6 +146,29 @@ write_files:
       done
       echo "{\"kfd\": false, \"render_nodes\": $n, \"wanted\": $want, \"waited_s\": $t, \"error\": \"timeout\"}" > /var/lib/kvedge/gpu.json
       exit 1
+  - path: /usr/local/sbin/kvedge-ready
+    permissions: "0755"
+    content: |
+      #!/bin/sh
+      # Boot-to-ready producer: poll `iotedge list` until edgeAgent runs and
+      # `iotedge check` until it passes (exit 0 = no failed check; warnings allowed),
+      # bounded; stamp both into /var/lib/kvedge/boot-timing and keep the last check
+      # report as JSON for the collector (python -m kvedge_amd.utils.boottime collect).
+      wait_s=${1:-900}; poll_s=${2:-2}; t0=$(date +%s); agent=0
+      mkdir -p /var/lib/kvedge
+      while [ $(( $(date +%s) - t0 )) -lt "$wait_s" ]; do
+        if [ "$agent" -eq 0 ] && iotedge list 2>/dev/null | awk '$1=="edgeAgent" && $2=="running"{f=1} END{exit !f}'; then
+          /usr/local/sbin/kvedge-stamp edge_agent_running; agent=1
+        fi
+        if iotedge check --output json > /var/lib/kvedge/iotedge-check.json 2>/dev/null; then
+          [ "$agent" -eq 1 ] || /usr/local/sbin/kvedge-stamp edge_agent_running
+          /usr/local/sbin/kvedge-stamp iotedge_check_pass
+          exit 0
+        fi
+        sleep "$poll_s"
+      done
+      /usr/local/sbin/kvedge-stamp iotedge_check_timeout
+      exit 1
   - path: /etc/systemd/system/kvedge-config.service
     content: |
       [Unit]
@@ -131,6 +179,20 @@ write_files:
       Type=oneshot
       ExecStart=/usr/local/sbin/kvedge-apply-config
       RemainAfterExit=yes
+      Restart=on-failure
+      RestartSec=5
+      [Install]
+      WantedBy=multi-user.target
+  - path: /etc/systemd/system/kvedge-ready.service
+    content: |
+      [Unit]
+      Description=kvedge: wait for iotedge check to pass (boot-to-ready stamp)
+      After=kvedge-config.service aziot-edged.service
+      Wants=kvedge-config.service
+      [Service]
+      Type=oneshot
+      ExecStart=/usr/local/sbin/kvedge-ready {{ $v.guest.readyWaitSeconds }} {{ $v.guest.readyPollSeconds }}
+      RemainAfterExit=yes
       [Install]
       WantedBy=multi-user.target
 runcmd:
@@ -140,6 +202,7 @@ runcmd:
   - [sh, -c, "getent group render >/dev/null && getent passwd iotedge >/dev/null && usermod -aG video,render iotedge || true"]
   - [systemctl, daemon-reload]
   - [systemctl, enable, --now, kvedge-config.service]
+  - [systemctl, enable, --now, --no-block, kvedge-ready.service]
   - [/usr/local/sbin/kvedge-gpu-check, "{{ $v.gpu.count }}", "{{ $v.guest.gpuWaitSeconds }}"]
   - [/usr/local/sbin/kvedge-stamp, runcmd_done]
 final_message: "kvedge guest {{ $v.guest.hostname }}{{ include "kvedge.sfx" . }} up after $UPTIME s"

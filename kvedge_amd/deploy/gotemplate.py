@@ -488,6 +488,10 @@ class Renderer:
         def ternary(a, b, c):
             return a if truthy(c) else b
 
+        def _set(d, k, v):  # Sprig: mutates and returns the dict
+            d[k] = v
+            return d
+
         def coalesce(*vs):
             for v in vs:
                 if truthy(v):
@@ -528,6 +532,9 @@ class Renderer:
             "mul": lambda *a: __import__("math").prod(_num(x) for x in a),
             "div": lambda a, b: int(_num(a) // _num(b)),
             "mod": lambda a, b: _num(a) % _num(b),
+            "max": lambda *a: int(max(_num(x) for x in a)),
+            "min": lambda *a: int(min(_num(x) for x in a)),
+            "set": _set,
             "until": lambda n: list(range(int(n))),
             "untilStep": lambda a, b, c: list(range(int(a), int(b), int(c))),
             "list": lambda *a: list(a),

@@ -17,7 +17,38 @@ from .config import ModuleConfig
 from .transport import make_transport
 
 
+def _topology_from_env() -> int:
+    """Map the chart's per-VM env (KVEDGE_NODE_RANK / KVEDGE_NNODES /
+    KVEDGE_RANKS_PER_NODE, deploy/helm/templates/kvedge-module-deployment.yaml) to
+    torch.distributed's.  Returns the number of local ranks this process must launch
+    (0 = run in-process)."""
+    if "WORLD_SIZE" in os.environ:  # already a launched rank (torchrun / our launcher)
+        return 0
+    nnodes = int(os.environ.get("KVEDGE_NNODES", "1"))
+    rpn = int(os.environ.get("KVEDGE_RANKS_PER_NODE", "1"))
+    node = int(os.environ.get("KVEDGE_NODE_RANK", "0"))
+    if rpn > 1:
+        return rpn
+    if nnodes > 1:  # one GPU per VM: this process IS the rank
+        os.environ.update(RANK=str(node), LOCAL_RANK="0", WORLD_SIZE=str(nnodes))
+    return 0
+
+
 def main(argv=None):
+    local = _topology_from_env()
+    if local:
+        # topology (a): one VM owns several GPUs -> one child rank per GPU (the parent
+        # never touches the GPU); topology (a)+(b) mixes work the same way per VM
+        pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env = dict(os.environ, PYTHONPATH=os.pathsep.join(
+            p for p in (pkg_root, os.environ.get("PYTHONPATH", "")) if p))
+        return parallel.launch_local(
+            local, ["-m", "kvedge_amd.module", *(sys.argv[1:] if argv is None else argv)],
+            env=env,
+            node_rank=int(os.environ.get("KVEDGE_NODE_RANK", "0")),
+            nnodes=int(os.environ.get("KVEDGE_NNODES", "1")),
+            master_addr=os.environ.get("MASTER_ADDR"),
+            master_port=int(os.environ["MASTER_PORT"]) if "MASTER_PORT" in os.environ else None)
     d = ModuleConfig()
     ap = argparse.ArgumentParser(prog="kvedge-module")
     ap.add_argument("--transport", default=os.environ.get("KVEDGE_TRANSPORT", "stdout"),
@@ -47,7 +78,9 @@ def main(argv=None):
                        fps=a.fps, use_graph=not a.no_graph, world_size=di.world_size,
                        source=a.source, native_loop=not a.no_native_loop,
                        steps_per_poll=a.steps_per_poll, sync_every=a.sync_every).validate()
-    app = ModuleApp(make_transport(a.transport), cfg, state_path=a.state,
+    # one IoT Edge identity per VM: only local rank 0 talks to edgeHub
+    kind = a.transport if di.local_rank == 0 or a.transport != "azure" else "null"
+    app = ModuleApp(make_transport(kind), cfg, state_path=a.state,
                     stamp_path=a.stamps or None)
     # SIGTERM (edgeAgent stop, VM shutdown) only votes to stop: the replicas leave the
     # loop together at the next control boundary, so the final report's collectives match

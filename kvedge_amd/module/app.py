@@ -134,6 +134,12 @@ class ModuleApp:
         self.last_error: Optional[str] = None
         self.rank = parallel.info().rank
         self.world = parallel.info().world_size
+        if state_path and self.world > 1:
+            # several ranks may share one VM's disk (topology a): one state file each
+            root, ext = os.path.splitext(state_path)
+            self.state_path = f"{root}.rank{self.rank}{ext}"
+        if parallel.info().local_rank != 0:
+            self.stamp_path = None  # one boot-timing stamp per VM
         # lockstep control plane
         self._events: List[Tuple[str, Any]] = []      # queued since the last boundary
         self._replies: List[Optional[Deferred]] = []  # parallel to _events (own rank)

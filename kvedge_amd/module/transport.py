@@ -146,6 +146,24 @@ class FakeTransport(Transport):
             return [p for o, p in self.messages if o == name]
 
 
+class NullTransport(Transport):
+    """For the non-leader ranks of a multi-GPU VM (topology a): the VM is ONE IoT Edge
+    device, so only local rank 0 holds the edgeHub connection; the other ranks take
+    part through the lockstep boundaries and have nothing to send."""
+
+    def __init__(self, desired: Optional[Dict[str, Any]] = None):
+        self.desired = dict(desired or {})
+
+    def get_desired(self):
+        return dict(self.desired)
+
+    def patch_reported(self, props):
+        pass
+
+    def send_message(self, output, payload):
+        pass
+
+
 class StdoutTransport(Transport):
     def __init__(self, desired: Optional[Dict[str, Any]] = None, stream=None):
         self.desired = dict(desired or {})
@@ -222,6 +240,8 @@ def make_transport(kind: str, desired: Optional[Dict[str, Any]] = None) -> Trans
         return StdoutTransport(desired)
     if kind == "azure":
         return AzureIoTTransport()
+    if kind == "null":
+        return NullTransport(desired)
     raise ValueError(f"unknown transport {kind!r}")
 
 

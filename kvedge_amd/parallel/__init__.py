@@ -43,10 +43,13 @@ def info() -> DistInfo:
 
 
 def launch_local(nproc: int, argv: Sequence[str], env: Optional[dict] = None,
-                 timeout_s: Optional[float] = None) -> int:
-    """Single-node launcher (the torchrun role, without its agent): start ``nproc``
+                 timeout_s: Optional[float] = None, node_rank: int = 0, nnodes: int = 1,
+                 master_addr: Optional[str] = None, master_port: Optional[int] = None) -> int:
+    """Per-node launcher (the torchrun role, without its agent): start ``nproc``
     fresh child processes ``python <argv>`` with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set,
     one per GPU, wait for all, return the first non-zero exit code (0 if all passed).
+    Multi-node (e.g. several 8-GPU VMs): global rank = node_rank * nproc + local rank,
+    and every node must be given the same master_addr/port (rank 0's node).
 
     The parent must not have touched the GPU (a process that initialised HIP must not
     be replaced or fork GPU children); it only counts devices.  If one rank fails, the
@@ -57,16 +60,21 @@ def launch_local(nproc: int, argv: Sequence[str], env: Optional[dict] = None,
     import sys
     import time
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    if master_port is None:
+        if nnodes > 1:
+            raise ValueError("multi-node launch needs an explicit master_port")
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        master_port = s.getsockname()[1]
+        s.close()
+    addr = master_addr or "127.0.0.1"
     base = dict(os.environ if env is None else env)
     base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host
     procs = []
     for r in range(nproc):
-        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc),
-                 LOCAL_WORLD_SIZE=str(nproc), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        e = dict(base, RANK=str(node_rank * nproc + r), LOCAL_RANK=str(r),
+                 WORLD_SIZE=str(nnodes * nproc), LOCAL_WORLD_SIZE=str(nproc),
+                 MASTER_ADDR=addr, MASTER_PORT=str(master_port))
         procs.append(subprocess.Popen([sys.executable] + list(argv), env=e))
     rc = 0
     t_end = None if timeout_s is None else time.monotonic() + timeout_s

@@ -25,7 +25,12 @@ RWO, RWX = "ReadWriteOnce", "ReadWriteMany"
 
 @dataclass
 class Timings:
-    """Seconds per phase of a cold migration (defaults: pre-baked ROCm guest)."""
+    """Seconds per phase of a cold migration, fed to the FakeCluster's clock.
+
+    The defaults are ASSUMED INPUTS, not measurements (no cluster has been run): any
+    "cold-migration time" computed from them is a model output and is labelled
+    ``source="assumed"``.  :meth:`from_boot_summary` replaces the guest-side phases with
+    the ones the boot-timing collector measured (kvedge_amd.utils.boottime collect)."""
     graceful_stop: float = 20.0
     node_failure_detect: float = 40.0
     schedule: float = 2.0
@@ -33,6 +38,28 @@ class Timings:
     gpu_attach: float = 3.0
     guest_boot: float = 45.0
     module_ready: float = 15.0
+    source: str = "assumed"
+
+    @classmethod
+    def from_boot_summary(cls, summary: Dict[str, float],
+                          base: Optional["Timings"] = None) -> "Timings":
+        """Derive the boot phases from one replica's collector summary (seconds after
+        helm install): guest_boot = VMI Running -> cloud-init runcmd done (includes the
+        GPU wait); module_ready = runcmd done -> ready (iotedge check pass, else the
+        module's first inference).  Phases the summary lacks keep ``base``'s values."""
+        b = base or cls()
+        kw = dict(b.__dict__)
+        run, done = summary.get("vmi_running_s"), summary.get("guest_runcmd_done_s")
+        ready = summary.get("iotedge_check_pass_s", summary.get("module_first_inference_s"))
+        measured = []
+        if run is not None and done is not None and done >= run:
+            kw["guest_boot"] = done - run
+            measured.append("guest_boot")
+        if done is not None and ready is not None and ready >= done:
+            kw["module_ready"] = ready - done
+            measured.append("module_ready")
+        kw["source"] = ("boot-timing:" + ",".join(measured)) if measured else b.source
+        return cls(**kw)
 
 
 @dataclass
@@ -257,7 +284,9 @@ class ResilienceController:
 
 class KubectlAdapter:
     """The same operations against a real cluster (kubectl + virtctl).  dry_run=True
-    returns the command lines without executing them."""
+    returns the command lines without executing them.  VM names come from
+    :class:`kvedge_amd.deploy.names.ChartNames` (checked against a chart render in
+    tests/test_resilience.py)."""
 
     def __init__(self, namespace: str = "default", dry_run: bool = True):
         self.ns = namespace
@@ -292,3 +321,18 @@ class KubectlAdapter:
 
     def uncordon(self, node: str):
         self._run("kubectl", "uncordon", node)
+
+    def wait_deleted(self, vm: str, timeout_s: int = 300):
+        self._run("kubectl", "wait", f"vmi/{vm}", "-n", self.ns, "--for=delete",
+                  f"--timeout={timeout_s}s")
+
+    def cold_migrate(self, vm: str, from_node: str, timeout_s: int = 600):
+        """Drain one node's GPU VM the only way VFIO allows: cordon, stop (releases the
+        MI355X), wait until the VMI is gone, start (scheduler picks a node with a free
+        GPU; RWX storage lets it leave the node), wait Running; uncordon is left to the
+        operator after maintenance."""
+        self._run("kubectl", "cordon", from_node)
+        self.stop_vm(vm)
+        self.wait_deleted(vm)
+        self.start_vm(vm)
+        self.wait_running(vm, timeout_s)

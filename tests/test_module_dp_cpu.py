@@ -121,3 +121,53 @@ def test_module_lockstep_4_ranks(tmp_path):
     assert all("rolled back" in r[7] for r in res)
     # only rank 0 emits telemetry (job totals)
     assert res[0][8] >= 1 and all(r[8] == 0 for r in res[1:])
+
+
+def _module_cmd(tmp, tag):
+    import sys
+
+    return [sys.executable, "-m", "kvedge_amd.module", "--transport", "stdout",
+            "--model", "resnet50", "--batch", "1", "--image-size", "64", "--no-graph",
+            "--steps", "4", "--sync-every", "2", "--report-interval-s", "1000",
+            "--state", os.path.join(tmp, f"state-{tag}.json"),
+            "--stamps", os.path.join(tmp, f"stamps-{tag}")]
+
+
+def _telemetry(out):
+    import json
+
+    msgs = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+    return [m["payload"] for m in msgs if m.get("output") == "telemetry"]
+
+
+@pytest.mark.timeout(600)
+def test_module_cli_topologies(tmp_path):
+    """The chart's per-VM env (kvedge-module-deployment.yaml) drives the module CLI:
+    (a) one VM with 2 GPUs -> the module launches 2 local ranks;
+    (b) two one-GPU VMs -> two independent processes, KVEDGE_NODE_RANK 0/1."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    base = dict(os.environ, PYTHONPATH=root, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1")
+    base.pop("WORLD_SIZE", None)
+    # (a)
+    env = dict(base, KVEDGE_NNODES="1", KVEDGE_RANKS_PER_NODE="2", KVEDGE_NODE_RANK="0",
+               MASTER_PORT=str(_free_port()))
+    r = subprocess.run(_module_cmd(str(tmp_path), "a"), env=env, capture_output=True,
+                       text=True, timeout=500, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    tel = _telemetry(r.stdout)
+    assert tel and tel[-1]["world_size"] == 2 and {t["rank"] for t in tel} == {0}
+    # (b)
+    port = str(_free_port())
+    procs = [subprocess.Popen(_module_cmd(str(tmp_path), f"b{i}"), cwd=str(tmp_path),
+                              env=dict(base, KVEDGE_NNODES="2", KVEDGE_RANKS_PER_NODE="1",
+                                       KVEDGE_NODE_RANK=str(i), MASTER_PORT=port),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for i in range(2)]
+    outs = [p.communicate(timeout=500) for p in procs]
+    assert [p.returncode for p in procs] == [0, 0], outs[1][1][-3000:]
+    tel0, tel1 = _telemetry(outs[0][0]), _telemetry(outs[1][0])
+    assert tel0 and tel0[-1]["world_size"] == 2 and not tel1
+    assert open(os.path.join(str(tmp_path), "stamps-b1")).read().startswith(
+        "module_first_inference ")

@@ -87,3 +87,93 @@ def test_kubectl_adapter_dry_run():
     assert cmds[1].startswith("kubectl drain n1")
     assert cmds[2] == "virtctl restart aziot-edge-kubevirt-linux -n edge"
     assert "--for=jsonpath={.status.phase}=Running" in cmds[3]
+
+
+def test_timings_are_labelled_and_driven_by_boot_collector():
+    """default phase times are assumed inputs; a boot-timing
+    collector summary replaces the guest-side phases."""
+    assert Timings().source == "assumed"
+    summary = {"vmi_running_s": 38.0, "guest_runcmd_done_s": 63.0,
+               "iotedge_check_pass_s": 90.0, "module_first_inference_s": 80.0}
+    t = Timings.from_boot_summary(summary)
+    assert t.guest_boot == 25.0 and t.module_ready == 27.0
+    assert t.source == "boot-timing:guest_boot,module_ready"
+    assert t.schedule == Timings().schedule  # not measured by the collector: kept
+    t2 = Timings.from_boot_summary({"vmi_running_s": 10.0})
+    assert t2.source == "assumed" and t2.guest_boot == Timings().guest_boot
+    c = FakeCluster(t)
+    c.add_node("n1", 8)
+    c.add_vm("vm0", access_mode=RWX)
+    rec = ResilienceController(c).reconcile()
+    assert rec[0].seconds == t.schedule + t.pvc_attach + t.gpu_attach + 25.0 + 27.0
+
+
+def test_kubectl_adapter_uses_rendered_chart_names():
+    """The adapter's targets are exactly the VirtualMachines the chart renders."""
+    from kvedge_amd.deploy.helm import Chart, manifests
+    from kvedge_amd.deploy.names import ChartNames
+    import os
+
+    chart = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                         "deploy", "helm")
+    objs = manifests(Chart(chart).render("rel", sets=["replicas=3"]))
+    vms = [o["metadata"]["name"] for o in objs if o["kind"] == "VirtualMachine"]
+    names = ChartNames("aziot-edge-kubevirt", 3)
+    assert names.all_vms() == vms
+    k = KubectlAdapter("edge", dry_run=True)
+    k.cold_migrate(names.vm(2), "n1")
+    cmds = [" ".join(c) for c in k.log]
+    assert cmds == ["kubectl cordon n1",
+                    f"virtctl stop {vms[2]} -n edge",
+                    f"kubectl wait vmi/{vms[2]} -n edge --for=delete --timeout=300s",
+                    f"virtctl start {vms[2]} -n edge",
+                    f"kubectl wait vmi/{vms[2]} -n edge --for=jsonpath={{.status.phase}}=Running "
+                    "--timeout=600s"]
+    dvs = {o["metadata"]["name"] for o in objs if o["kind"] == "DataVolume"}
+    assert {names.dv(i) for i in range(3)} == dvs
+    svcs = {o["metadata"]["name"] for o in objs if o["kind"] == "Service"}
+    assert {names.ssh_service(i) for i in range(3)} | {names.rendezvous()} == svcs
+    secrets = {o["metadata"]["name"] for o in objs if o["kind"] == "Secret"}
+    assert {names.config_secret(i) for i in range(3)} | \
+        {names.cloudinit_secret(i) for i in range(3)} == secrets
+
+
+def test_gpu_reattach_restart_resumes_module_from_state_file(tmp_path):
+    """Cold migration end to end on CPU: the fake cluster moves vm0 (GPU re-attached on
+    the other node); the module process restarts on the persistent disk's state file:
+    restarts + 1, counters continue, telemetry resumes."""
+    from kvedge_amd.module.app import ModuleApp
+    from kvedge_amd.module.transport import FakeTransport
+
+    class Clock:
+        def __init__(self):
+            self.t = 0.0
+
+        def __call__(self):
+            self.t += 0.25
+            return self.t
+
+    state = str(tmp_path / "module-state.json")  # lives on the VM's DataVolume
+    desired = {"model": "resnet50", "batch": 1, "image_size": 64, "report_interval_s": 0.5}
+    tr = FakeTransport(desired)
+    app = ModuleApp(tr, device="cpu", state_path=state, clock=Clock()).start()
+    app.run(max_steps=4)
+    before = app.state["total_images"]
+    n_tel = len(tr.outputs("telemetry"))
+    assert before == 4 and n_tel >= 1
+    c, ctl = _cluster(access=RWX)
+    ctl.reconcile()
+    src = c.vmis["vm0"].node
+    app.request_stop()  # SIGTERM from the graceful VM stop
+    app.run()
+    app.stop()          # state flushed to the persistent disk
+    rec = {r.vm: r for r in ctl.drain(src)}["vm0"]
+    assert rec.ok and rec.to_node != src and rec.gpu_ids
+    tr2 = FakeTransport(desired)
+    app2 = ModuleApp(tr2, device="cpu", state_path=state, clock=Clock()).start()
+    assert app2.state["restarts"] == 1 and app2.state["total_images"] >= before
+    assert tr2.reported["restarts"] == 1
+    app2.run(max_steps=4)
+    tel = tr2.outputs("telemetry")
+    assert tel and tel[-1]["total_images"] > before
+    app2.stop()
