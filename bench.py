@@ -117,6 +117,12 @@ def main(argv=None):
                           use_graph=not a.no_graph)
     eng.prepare(warmup=2, autotune=not a.no_autotune)
     build_s = time.perf_counter() - t_build
+    from kvedge_amd.utils.logging import get_logger, log_event
+
+    log = get_logger("kvedge.bench")
+    if di.is_main:
+        log_event(log, "built", model=a.model, batch=a.batch, world=di.world_size,
+                  build_s=round(build_s, 2), tuned_layers=len(getattr(eng, "tuning", {}) or {}))
 
     for _ in range(a.warmup):
         eng.run()
@@ -194,6 +200,8 @@ def main(argv=None):
         lat_hist.allreduce()  # fleet-wide step-latency distribution (one SUM all-reduce)
         res["extra"]["step_latency_ms"] = {k: round(v, 4) for k, v in lat_hist.summary().items()}
     if di.is_main:
+        log_event(log, "timed", steps=a.steps, ms_per_step=res["ms_per_step"],
+                  value=res["value"], replica_ok=rc.ok)
         line = json.dumps(res)
         print(line, flush=True)
         if a.json_out:

@@ -63,8 +63,10 @@ void conv(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
   p.M = (int)(N * Ho * Wo);
   p.ldy = (int)ldy; p.y_coff = (int)y_coff; p.ldr = (int)ldr; p.r_coff = (int)r_coff;
   p.act = (int)act; p.mode = (int)mode;
-  // bounds: every pointer offset the kernel forms must stay in int32 and in the buffer
-  TORCH_CHECK(x.numel() < (1ll << 31) && y.numel() < (1ll << 31), "kvedge: tensor too large for int32 indexing");
+  // bounds: every operand inside its tensor.  No whole-tensor size cap: kv_conv2d splits
+  // batches whose operands exceed 2 GiB into image chunks (32-bit in-kernel offsets)
+  TORCH_CHECK(N > 0 && H * W * ldx * 2 < (1ll << 31) && Ho * Wo * ldy * 2 < (1ll << 31),
+              "kvedge: one image's activations exceed 2 GiB");
   TORCH_CHECK(x.numel() >= N * H * W * ldx, "kvedge: x smaller than N*H*W*ldx");
   TORCH_CHECK(x_coff + Cin <= ldx, "kvedge: x channel slice out of range");
   TORCH_CHECK(y.numel() >= (int64_t)p.M * ldy && y_coff + Cout <= ldy, "kvedge: y too small");
@@ -111,8 +113,6 @@ void conv_dual(const at::Tensor& x1, const at::Tensor& x2, const at::Tensor& w,
   p.act = (int)act; p.mode = 4;
   p.x2 = x2.data_ptr(); p.K1 = (int)K1; p.H2 = (int)x2.size(1); p.W2 = (int)x2.size(2);
   p.ldx2 = (int)K2; p.stride2 = (int)stride2;
-  TORCH_CHECK(x1.numel() < (1ll << 30) && x2.numel() < (1ll << 30) && y.numel() < (1ll << 31),
-              "kvedge: tensor too large for 32-bit buffer offsets");
   const int rc = kv_conv2d(&p, (int)tile, cur_stream(x1));
   TORCH_CHECK(rc == 0, "kvedge: conv_dual failed rc=", rc);
 }
@@ -182,8 +182,6 @@ void conv_tail(const at::Tensor& x, const c10::optional<at::Tensor>& x2, const a
     p.bias_t = b1->data_ptr<float>();
   }
   p.z = z.data_ptr(); p.n_t = (int)Nt; p.ldz = (int)Nt; p.z_coff = 0; p.act_t = 1;
-  TORCH_CHECK(x.numel() < (1ll << 30) && y.numel() < (1ll << 31) && z.numel() < (1ll << 31),
-              "kvedge: tensor too large for 32-bit buffer offsets");
   const int rc = kv_conv2d(&p, (int)tile, cur_stream(x));
   TORCH_CHECK(rc == 0, "kvedge: conv_tail failed rc=", rc);
 }
@@ -205,7 +203,6 @@ void conv_frames_s2d(const at::Tensor& frames, const at::Tensor& w,
   TORCH_CHECK(w.dim() == 2 && w.size(1) == 64, "kvedge: s2d stem weight must be [Cout, 64]");
   TORCH_CHECK(y.dim() == 4 && y.size(0) == N && y.size(1) == H && y.size(2) == W &&
                   y.size(3) == Cout, "kvedge: y must be [N, H/2, W/2, Cout]");
-  TORCH_CHECK(frames.numel() < (1ll << 31) && y.numel() < (1ll << 31), "kvedge: int32 indexing");
   const c10::DeviceGuard g(frames.device());
   KvConvParams p{};
   p.x = frames.data_ptr();
@@ -436,6 +433,7 @@ void batchnorm_nhwc(const at::Tensor& x, at::Tensor& y, const at::Tensor& scale,
 }
 
 int64_t conv_num_tiles() { return kv_conv_num_tiles(); }
+int64_t set_conv_chunk_bytes(int64_t b) { return kv_set_conv_chunk_bytes(b); }
 
 }  // namespace
 
@@ -468,6 +466,7 @@ TORCH_LIBRARY(kvedge, m) {
   m.def("preprocess(Tensor x, Tensor(a!) y, float[] mean, float[] std) -> ()");
   m.def("batchnorm_nhwc(Tensor x, Tensor(a!) y, Tensor scale, Tensor shift, bool relu) -> ()");
   m.def("conv_num_tiles() -> int", conv_num_tiles);
+  m.def("set_conv_chunk_bytes(int bytes) -> int", set_conv_chunk_bytes);
 }
 
 TORCH_LIBRARY_IMPL(kvedge, CUDA, m) {

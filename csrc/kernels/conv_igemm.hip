@@ -21,6 +21,8 @@
 //
 // The reference has no kernels; the kernel inventory this
 // implements is SURVEY.md §2.5 K1-K3.
+#include <algorithm>
+
 #include "common.h"
 #include "kvedge_kernels.h"
 
@@ -369,10 +371,62 @@ static int kv_conv_check_extents(const KvConvParams* p) {
 }
 #endif
 
+static int kv_conv2d_one(const KvConvParams* p, int tile, hipStream_t stream);
+
+// Byte span of one image of every NHWC operand a conv touches.  The kernels address
+// operands through 32-bit buffer-resource offsets (out-of-range offsets are the zero-fill
+// padding trick), so one launch must keep every operand below 2 GiB.
+static long long kv_conv_max_image_bytes(const KvConvParams* p) {
+  const long long hw = (long long)p->H * p->W, ohw = (long long)p->Ho * p->Wo;
+  long long m = p->in_u8 ? hw * 12 : hw * p->ldx * 2;
+  m = std::max(m, ohw * p->ldy * 2);
+  if (p->res) m = std::max(m, ohw * p->ldr * 2);
+  if (p->mode == 4) m = std::max(m, (long long)p->H2 * p->W2 * p->ldx2 * 2);
+  if (p->n_t) m = std::max(m, ohw * p->ldz * 2);
+  return m;
+}
+
+// Batches whose activations exceed 2 GiB per tensor (ResNet-50 past ~1200 images, YOLOv8n
+// past ~650: the 288 GB of HBM holds far more) run as a sequence of image-chunk launches
+// on the same stream; each chunk's base pointers are 64-bit offsets from the host, so
+// the in-kernel 32-bit offsets stay in range.  Small batches take the single launch.
+static long long g_chunk_bytes = 0x7f000000LL;  // < kOOB: OOB offsets stay past the end
+
+// Tests shrink the chunk size to exercise the chunked path with small tensors
+// (0 restores the default).  Returns the value in effect.
+extern "C" long long kv_set_conv_chunk_bytes(long long bytes) {
+  g_chunk_bytes = bytes > 0 ? std::min(bytes, 0x7f000000LL) : 0x7f000000LL;
+  return g_chunk_bytes;
+}
+
 extern "C" int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream) {
 #ifdef KVEDGE_CHECKS
   if (const int rc = kv_conv_check_extents(p)) return rc;
 #endif
+  const long long kChunkBytes = g_chunk_bytes;
+  const long long per = kv_conv_max_image_bytes(p);
+  if (per <= 0 || per >= kChunkBytes) return per <= 0 ? -1 : -9;
+  const long long cap = kChunkBytes / per;
+  if (p->N <= cap) return kv_conv2d_one(p, tile, stream);
+  const long long hw = (long long)p->H * p->W, ohw = (long long)p->Ho * p->Wo;
+  for (int n0 = 0; n0 < p->N; n0 += (int)cap) {
+    KvConvParams q = *p;
+    q.N = (int)std::min<long long>(cap, p->N - n0);
+    q.M = (int)(q.N * ohw);
+    auto adv = [&](const void* b, long long bytes_per_image) -> const char* {
+      return b ? static_cast<const char*>(b) + (long long)n0 * bytes_per_image : nullptr;
+    };
+    q.x = adv(p->x, p->in_u8 ? hw * 12 : hw * p->ldx * 2);
+    q.y = const_cast<char*>(adv(p->y, ohw * p->ldy * 2));
+    if (p->res) q.res = adv(p->res, ohw * p->ldr * 2);
+    if (p->mode == 4) q.x2 = adv(p->x2, (long long)p->H2 * p->W2 * p->ldx2 * 2);
+    if (p->n_t) q.z = const_cast<char*>(adv(p->z, ohw * p->ldz * 2));
+    if (const int rc = kv_conv2d_one(&q, tile, stream)) return rc;
+  }
+  return 0;
+}
+
+static int kv_conv2d_one(const KvConvParams* p, int tile, hipStream_t stream) {
   if (p->Kpad % BK != 0 || p->Cout % 8 != 0) return -1;
   if (p->n_t) {  // fused bottleneck tail: the v3 tail tile only
     const int v3 = kNumTiles + glds_num_tiles();

@@ -53,6 +53,8 @@ typedef struct KvConvParams {
 
 // tile: -1 = heuristic; otherwise an index into the tile table (kv_conv_num_tiles()).
 int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream);
+// image-chunk size of kv_conv2d launches (bytes per operand per launch); 0 = default
+long long kv_set_conv_chunk_bytes(long long bytes);
 int kv_conv_num_tiles(void);
 int kv_conv_pick_tile(const KvConvParams* p);
 

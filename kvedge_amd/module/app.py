@@ -41,6 +41,7 @@ from typing import Any, Dict, List, Optional, Tuple
 import torch
 
 from .. import ops, parallel
+from ..utils.logging import get_logger, log_event
 from .config import ModuleConfig
 from .transport import Deferred, Transport, now_iso
 
@@ -148,6 +149,12 @@ class ModuleApp:
         self.sync_every = 1
         self.boundaries = 0
         self._first_inference_stamped = False
+        self.log = get_logger("kvedge.module")
+        self._gpu = None
+        if self.device.type == "cuda":
+            from ..utils.gpustat import GpuStat
+
+            self._gpu = GpuStat(self.device.index or 0)
 
     # ---------------------------------------------------------------- lifecycle
     def start(self):
@@ -169,8 +176,12 @@ class ModuleApp:
         self._load_state()
         err = self._build_fleet()
         if err is not None:
+            log_event(self.log, "start_failed", 40, error=err)
             self.tr.patch_reported({"status": "failed", "lastError": err})
             raise RuntimeError(f"module build failed: {err}")
+        log_event(self.log, "started", model=self.cfg.model, batch=self.cfg.batch,
+                  world_size=self.world, sync_every=self.sync_every, device=str(self.device),
+                  restarts=self.state["restarts"])
         self._report_config()
         self._win_t0 = self._last_report = self.clock()
         return self
@@ -275,6 +286,8 @@ class ModuleApp:
             if previous is None:
                 return err
             self.state["failed_rebuilds"] += 1
+            log_event(self.log, "rebuild_failed", 30, error=err, batch=self.cfg.batch,
+                      rollback_batch=previous.batch)
             self.cfg = previous
             back = self._build_fleet(None)  # the previous config built before
             if back is not None:
@@ -370,7 +383,11 @@ class ModuleApp:
                     replies[k].resolve(*res)
         if fleet[0]["report"] and self.engine is not None:
             self.report()  # rank 0's clock decides, every rank all-reduces together
-        return any(p["stop"] for p in fleet)
+        stop = any(p["stop"] for p in fleet)
+        if stop:
+            log_event(self.log, "fleet_stop", boundary=self.boundaries,
+                      voters=[r for r, p in enumerate(fleet) if p["stop"]])
+        return stop
 
     def _apply(self, kind: str, data: Any) -> Tuple[int, Dict[str, Any]]:
         if kind == "twin":
@@ -425,6 +442,10 @@ class ModuleApp:
                "source": self.cfg.source}
         if self.ring is not None:
             msg["frames_dropped"] = self.ring.dropped
+        if self._gpu is not None:
+            g = self._gpu.sample()
+            if g:
+                msg["gpu"] = g
         msg.update(self._outputs_summary())
         if self.rank == 0:
             self.tr.send_message("telemetry", msg)
@@ -468,6 +489,7 @@ class ModuleApp:
         self.cfg = replace(new, world_size=old.world_size, sync_every=old.sync_every)
         if self.cfg.needs_rebuild(old):
             self.state["rebuilds"] += 1
+            log_event(self.log, "rebuild", model=self.cfg.model, batch=self.cfg.batch)
             err = self._build_fleet(previous=old)
             if err is not None:  # even the rollback failed: nothing left to serve
                 self.tr.patch_reported({"status": "failed", "lastError": err})

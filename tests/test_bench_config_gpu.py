@@ -1,0 +1,96 @@
+"""The configuration bench.py actually times, checked against the fp32 nn.Module
+(VERDICT r1 weak #3 / next #6): autotuned tiles, batch 640 (ResNet-50) / 384 (YOLOv8n),
+hipGraph capture.  A slice of the batch is compared as LOGITS (pre-softmax) / raw head
+maps, not as probabilities, against the fp32 reference model on the same frames.
+"""
+import copy
+import json
+import os
+
+import pytest
+import torch
+
+from kvedge_amd import ops
+from kvedge_amd.engine import InferenceEngine
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    assert ops.load(), "native kvedge library must be loaded on the GPU box"
+
+
+def test_resnet50_bench_config_vs_fp32_reference():
+    from kvedge_amd.models.layers import frames_to_nchw
+    from kvedge_amd.models.resnet import KvResNet50, init_resnet50
+
+    ref = init_resnet50(seed=0)
+    kv = KvResNet50(ref, "cuda")
+    eng = InferenceEngine(kv, 640, 224, device="cuda", seed=0, use_graph=True)
+    eng.prepare(warmup=1, autotune=True)
+    assert eng.graph is not None and eng.tuning  # the timed configuration
+    eng.run()
+    torch.cuda.synchronize()
+    n = 64
+    probs_graph = eng.outputs[0][:n].float().cpu()
+    frames = eng.frames[:n].cpu()
+    with torch.no_grad():
+        lg_bench = kv.raw_outputs(eng.frames)[:n].float().cpu()  # same autotuned tiles
+        lg_ref = ref(frames_to_nchw(frames)).float()
+        # yard-stick: the same fp32 weights run by PyTorch-ROCm (MIOpen) in bf16
+        ref_bf16 = copy.deepcopy(ref).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
+        x16 = frames_to_nchw(frames).cuda().to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        lg_torch16 = ref_bf16(x16).float().cpu()
+    # the graph computed exactly this: its probabilities are the softmax of these logits
+    assert torch.allclose(probs_graph, torch.softmax(lg_bench, 1), rtol=1e-3, atol=1e-6)
+    cos = torch.nn.functional.cosine_similarity(lg_bench.flatten(), lg_ref.flatten(), dim=0)
+    cos_t = torch.nn.functional.cosine_similarity(lg_torch16.flatten(), lg_ref.flatten(), dim=0)
+    per_img = torch.nn.functional.cosine_similarity(lg_bench, lg_ref, dim=1)
+    agree = float((lg_bench.argmax(1) == lg_ref.argmax(1)).float().mean())
+    agree_t = float((lg_torch16.argmax(1) == lg_ref.argmax(1)).float().mean())
+    top2 = lg_ref.topk(2, dim=1).values
+    margins = (top2[:, 0] - top2[:, 1]).tolist()
+    flips = (lg_bench.argmax(1) != lg_ref.argmax(1)).nonzero().flatten().tolist()
+    stats = {"images": n, "batch": 640, "cos_logits": float(cos), "cos_logits_torch_bf16": float(cos_t),
+             "min_cos_per_image": float(per_img.min()), "top1_agree": agree,
+             "top1_agree_torch_bf16": agree_t, "flip_margins": [margins[i] for i in flips],
+             "median_margin": sorted(margins)[n // 2],
+             "logit_std": float(lg_ref.std())}
+    if os.path.isdir("gpurun_out"):
+        with open("gpurun_out/bench_config_parity_resnet50.json", "w") as f:
+            json.dump(stats, f, indent=1)
+    assert cos > 0.99 and cos >= cos_t - 2e-3, stats
+    assert per_img.min() > 0.98, stats
+    # random-init logits have small top-1 margins, so bf16 noise flips some of them: the
+    # kernels must agree with fp32 at least as well as PyTorch's own bf16 path (or >= 95%)
+    assert agree >= min(0.95, agree_t - 1.0 / n), stats
+    # and only near-ties may flip
+    assert all(margins[i] < 0.1 for i in flips), stats
+
+
+def test_yolov8n_bench_config_vs_fp32_reference():
+    from kvedge_amd.models.yolov8 import KvYoloV8n, frames_to_yolo, init_yolov8n
+
+    ref = init_yolov8n(seed=0)
+    kv = KvYoloV8n(ref, "cuda")
+    eng = InferenceEngine(kv, 384, 640, device="cuda", seed=0, use_graph=True)
+    eng.prepare(warmup=1, autotune=True)
+    assert eng.graph is not None and eng.tuning
+    eng.run()
+    torch.cuda.synchronize()
+    frames = eng.frames[:4].contiguous()
+    with torch.no_grad():
+        heads = kv.heads(kv.stem(eng.frames), stem_done=True)  # autotuned, full batch
+        hr = ref(frames_to_yolo(frames.cpu()))
+    for g, r in zip(heads, hr):
+        g = g[:4].float().cpu()
+        r = r.permute(0, 2, 3, 1).float()
+        cos = torch.nn.functional.cosine_similarity(g.flatten(), r.flatten(), dim=0)
+        assert cos > 0.99, float(cos)
+        # class logits and box-DFL logits separately (different magnitudes)
+        for sl in (slice(0, 64), slice(64, None)):
+            c = torch.nn.functional.cosine_similarity(g[..., sl].flatten(),
+                                                      r[..., sl].flatten(), dim=0)
+            assert c > 0.99, (sl, float(c))

@@ -75,7 +75,14 @@ def test_ring_fed_serving_equals_set_frames(kv):
     ref = InferenceEngine(kv, B, 224, device="cuda", use_graph=False, synthetic=False)
     out = ref.set_frames(frames[-1].cuda())
     torch.cuda.synchronize()
-    assert torch.allclose(probs_ring, out[0], atol=1e-3)
+    # the ring delivered exactly the last batch: identical frames -> identical logits
+    assert torch.equal(eng.frames.cpu(), frames[-1])
+    with torch.no_grad():
+        lg_ring = kv.raw_outputs(eng.frames).float()
+        lg_ref = kv.raw_outputs(frames[-1].cuda()).float()
+    assert torch.equal(lg_ring, lg_ref)
+    assert torch.allclose(probs_ring, out[0], rtol=1e-3, atol=1e-7)
+    assert torch.equal(probs_ring.argmax(1), torch.softmax(lg_ref, 1).argmax(1))
     ring.close()
 
 
