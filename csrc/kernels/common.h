@@ -27,6 +27,21 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// Division by a runtime-uniform divisor d without the ~20-instruction VALU expansion of
+// an integer divide (there is no hardware divider): q = umulhi(n, ceil(2^32 / d)), exact
+// for 0 <= n, d < 2^16 (error term n * (m*d - 2^32) / (d * 2^32) < 1/d).  The direct-conv
+// and stem kernels divide pixel indices by row pitches per fetched chunk and per output
+// block; with this the divide is one v_mul_hi_u32.
+struct FastDiv {
+  unsigned m;
+  int d;
+};
+__host__ __device__ __forceinline__ FastDiv make_fastdiv(int d) {
+  return FastDiv{(unsigned)((0x100000000ull + (unsigned long long)d - 1) / (unsigned long long)d), d};
+}
+__device__ __forceinline__ int fdiv(int n, FastDiv f) { return (int)__umulhi((unsigned)n, f.m); }
+__device__ __forceinline__ int fmod_(int n, int q, FastDiv f) { return n - q * f.d; }
+
 __device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
 __device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }  // v_cvt_pk_bf16_f32, NaN-safe
 

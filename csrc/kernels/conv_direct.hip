@@ -75,10 +75,13 @@ __host__ __device__ constexpr int direct_patch_alloc(int patch_bytes, bool dma) 
 // 180 weight VGPRs and had room for a single 80-pixel output row per band otherwise).
 // Lane-linear DMA slots of 16 B; slot q = (pixel q / SL, chunk q % SL) with SL = PB / 16,
 // the pitch-padding chunk (q % SL == CPP) gets an out-of-range offset (zero fill).
-template <int CIN, int COUT, int S, int KK, int ACT, bool RES, bool U8 = false, bool DMA = false>
+template <int CIN, int COUT, int S, int KK, int ACT, bool RES, bool U8 = false, bool DMA = false,
+          bool PAIRS = false>
 __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvParams p, int kR,
-                                                                int PW, int patch_rows) {
+                                                                int PW, int patch_rows,
+                                                                FastDiv fPW, FastDiv fWo) {
   static_assert(!U8 || (CIN == 16 && KK == 2 && S == 1), "frames-in form: the 2x2 s2d stem");
+  static_assert(!PAIRS || U8, "paired raw-row loads: frames-in form only");
   using C = DirectCfg<CIN, KK>;
   constexpr int NCB = (COUT + 31) / 32;  // 32-channel blocks
   static_assert(NCB >= 1 && NCB <= 4, "channel blocks");
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
   // lanes walk one raw frame row (coalesced 6-B groups); otherwise pixel-major.
   auto chunk_of = [&](int q, int& pp, int& c) __attribute__((always_inline)) {
     if constexpr (U8) {
-      const int rc = q / PW, pc = q - rc * PW;
+      const int rc = fdiv(q, fPW), pc = q - rc * PW;
       c = rc & 1;
       pp = (rc >> 1) * PW + pc;
     } else {
@@ -133,16 +136,47 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
       c = q - pp * C::CPP;
     }
   };
+  // U8 with even W: one 12-B buffer_load_dwordx3 = two neighbouring s2d pixels (ix even,
+  // 4-B aligned) of one raw row; patch column 0 (the left padding, ix = -1) is zeroed once
+  // and never fetched.  Item u -> (rc = u / NPR, pair k = u % NPR): patch row rc >> 1, raw
+  // row parity rc & 1, patch columns 2k+1, 2k+2.  (Odd W: the 3 x 16-bit loads per chunk.)
+  // (PAIRS is instantiated for even W only: direct_plan picks the form by W's parity)
+  const int NPR = W >> 1;
+  constexpr bool pairs = PAIRS;
+  const FastDiv fNPR = make_fastdiv(NPR > 0 ? NPR : 1);
+  static_assert(!U8 || C::PRE % 2 == 0, "pairs: two chunks per prefetch pair");
+  // pairs: the RAW 12 bytes stay in registers until commit (after the band's MFMAs), so
+  // the loads' latency hides under the MFMA phase; bit i of okp = pair i's row in range
+  typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+  u32x3 raw[PAIRS ? C::PRE / 2 : 1];
+  unsigned okp = 0;
   auto fetch = [&](int item) __attribute__((always_inline)) {
     const int n = item / nbands, band = item - n * nbands;
     const int iy0 = band * kR * S - 1;
     const bool live = item < total;
+    if constexpr (PAIRS) {
+      {
+        okp = 0;
+        const int nitems = patch_rows * 2 * NPR;
+#pragma unroll
+        for (int i = 0; i < C::PRE / 2; ++i) {
+          const int u = tid + kNT * i;
+          const int rc = fdiv(u, fNPR), k = u - rc * NPR;
+          const int iy = iy0 + (rc >> 1), ix = 2 * k;
+          const bool rowok = live && u < nitems && (unsigned)iy < (unsigned)H;
+          const int off = rowok ? ((n * 2 * H + 2 * iy + (rc & 1)) * 2 * W + 2 * ix) * 3 : kOOB;
+          raw[i] = __builtin_amdgcn_raw_buffer_load_b96(rx, off, 0, 0);
+          okp |= rowok ? 1u << i : 0u;
+        }
+        return;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < C::PRE; ++i) {
       const int q = tid + kNT * i;
       int pp, c;
       chunk_of(q, pp, c);
-      const int pr = pp / PW, pc = pp - pr * PW;
+      const int pr = fdiv(pp, fPW), pc = pp - pr * PW;
       const int iy = iy0 + pr, ix = pc - 1;
       const bool ok = live && q < nchunks && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
       if constexpr (U8) {
@@ -163,6 +197,32 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
     }
   };
   auto commit = [&]() __attribute__((always_inline)) {
+    if constexpr (PAIRS) {
+      {
+        const int nitems = patch_rows * 2 * NPR;
+        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int i = 0; i < C::PRE / 2; ++i) {
+          const int u = tid + kNT * i;
+          if (u >= nitems) continue;
+          const int rc = fdiv(u, fNPR), k = u - rc * NPR;
+          const int pp = (rc >> 1) * PW + 2 * k + 1;
+          unsigned char* dst = patch + pp * C::PB + (rc & 1) * 16;
+          // bytes 0-5: pixel ix (raw cols 2ix, 2ix+1), bytes 6-11: pixel ix+1 -> two s2d
+          // chunks [r g b 0 r' g' b' 0] in bf16 (0..255 exact); out-of-image rows: zeros
+          const u32x3 v = raw[i];
+          auto bf = [](unsigned w, int b) { return __float_as_uint((float)((w >> (8 * b)) & 0xffu)) >> 16; };
+          const bool ok = (okp >> i) & 1u;
+          *reinterpret_cast<uint4*>(dst) =
+              ok ? make_uint4(bf(v[0], 0) | (bf(v[0], 1) << 16), bf(v[0], 2),
+                              bf(v[0], 3) | (bf(v[1], 0) << 16), bf(v[1], 1)) : z;
+          *reinterpret_cast<uint4*>(dst + C::PB) =
+              ok ? make_uint4(bf(v[1], 2) | (bf(v[1], 3) << 16), bf(v[2], 0),
+                              bf(v[2], 1) | (bf(v[2], 2) << 16), bf(v[2], 3)) : z;
+        }
+        return;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < C::PRE; ++i) {
       const int q = tid + kNT * i;
@@ -181,7 +241,7 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
     for (int j = wv; j * 64 < nslots; j += kNT / 64) {  // one 1-KB DMA per wave per j
       const int q = j * 64 + lane;
       const int pp = q / SL, c = q - pp * SL;
-      const int pr = pp / PW, pc = pp - pr * PW;
+      const int pr = fdiv(pp, fPW), pc = pp - pr * PW;
       const int iy = iy0 + pr, ix = pc - 1;
       const bool ok = live && q < nslots && c < C::CPP && (unsigned)iy < (unsigned)H &&
                       (unsigned)ix < (unsigned)W;
@@ -198,6 +258,12 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
   const int rowb = PW * C::PB;
   int item = xcd_remap(blockIdx.x, gridDim.x);  // neighbour bands share an XCD
   int cur = 0;
+  if constexpr (PAIRS) {
+    // patch column 0 = left padding of every patch row, both parities: zero
+      for (int q = tid; q < patch_rows * 2; q += kNT)
+        *reinterpret_cast<uint4*>(patch + (q >> 1) * PW * C::PB + (q & 1) * 16) =
+            make_uint4(0u, 0u, 0u, 0u);
+  }
   if constexpr (DMA) {
     dma_fetch(item, patch);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -217,7 +283,7 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
 
     for (int b = ph < NPH ? ph : nblk; b < nblk; b += NPH) {
       const int j = min(b * 32 + fr, npix - 1);  // clamp: pixels past npix are discarded
-      const int yl = j / Wo, xc = j - yl * Wo;
+      const int yl = fdiv(j, fWo), xc = j - yl * Wo;
       const unsigned char* pa0 = pbase + (yl * S * PW + xc * S) * C::PB + fh * 16;
       const unsigned char* pa[KK];
 #pragma unroll
@@ -278,7 +344,7 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
     constexpr int OCH = COUT / 8;
     for (int q = tid; q < npix * OCH; q += kNT) {
       const int px = q / OCH, c = q - (q / OCH) * OCH;
-      const int yl = px / Wo, xc = px - yl * Wo;
+      const int yl = fdiv(px, fWo), xc = px - yl * Wo;
       const int oy = oy0 + yl;
       if (oy >= Ho) continue;
       const long long m = (long long)(n * Ho + oy) * Wo + xc;
@@ -300,7 +366,7 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
   }
 }
 
-typedef void (*DirectFn)(const KvConvParams, int, int, int);
+typedef void (*DirectFn)(const KvConvParams, int, int, int, FastDiv, FastDiv);
 
 struct DirectEntry {
   int cin, cout, stride, kk, act;
@@ -308,6 +374,7 @@ struct DirectEntry {
   DirectFn fn;
   bool u8 = false;
   bool dma = false;
+  bool pairs = false;  // frames-in with even W: 12-B paired raw-row loads
 };
 
 #define KV_DIRECT(CI, CO, S, A, R) {CI, CO, S, 3, A, R, conv3x3_direct_kernel<CI, CO, S, 3, A, R>}
@@ -337,7 +404,9 @@ static const DirectEntry kDirect[] = {
     KV_DIRECT_DMA(80, 80, 1, kActSilu, false),
     // YOLO b0 stem in space-to-depth form: 2x2 over [N,320,320,16]
     {16, 16, 1, 2, kActSilu, false, conv3x3_direct_kernel<16, 16, 1, 2, kActSilu, false>},
-    // ... and its frames-in form (preprocess fused)
+    // ... and its frames-in form (preprocess fused): even W (paired loads) / odd W
+    {16, 16, 1, 2, kActSilu, false,
+     conv3x3_direct_kernel<16, 16, 1, 2, kActSilu, false, true, false, true>, true, false, true},
     {16, 16, 1, 2, kActSilu, false, conv3x3_direct_kernel<16, 16, 1, 2, kActSilu, false, true>,
      true},
 };
@@ -368,6 +437,7 @@ static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* r
       const DirectEntry& e = kDirect[i];
       if (e.cin == p->Cin && e.cout == p->Cout && e.stride == p->stride && e.kk == kk &&
           e.act == act && e.res == res && e.u8 == (p->in_u8 != 0) &&
+          (!e.u8 || e.pairs == (p->W % 2 == 0)) &&
           (pass == 1 || e.dma == (tile == 1))) {
         idx = i;
         break;
@@ -423,7 +493,8 @@ static int direct_launch_one(const KvConvParams* p, int tile, hipStream_t stream
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
     return -7;
-  hipLaunchKernelGGL(fn, dim3(g), dim3(kNT), (unsigned)lds, stream, *p, kR, PW, rows);
+  hipLaunchKernelGGL(fn, dim3(g), dim3(kNT), (unsigned)lds, stream, *p, kR, PW, rows,
+                     make_fastdiv(PW), make_fastdiv(p->Wo));
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }
 

@@ -56,20 +56,29 @@ __device__ __forceinline__ void wait_vm() {
 // BKT = K elements per ring stage.  64: 128-B rows, 8 rows per DMA instruction.  32: 64-B
 // rows, 16 rows per instruction -- half the bytes per stage, so twice the stages fit the
 // same LDS (a 128x128 tile can keep 4 K steps in flight at 2 workgroups per CU, D = 5).
+//
+// WM x WN waves: 4 (256 threads, up to 2 workgroups per CU) or 8 (512 threads, one
+// workgroup per CU = 2 waves per SIMD).  The 8-wave 256x256 tile gives every wave a
+// 128x64 (or 64x128) sub-tile -- 0.75 fragment reads per MFMA -- while keeping two waves
+// per SIMD for latency hiding, which no 4-wave tile combines (a 4-wave 256x128 tile has
+// the sub-tile but one wave per SIMD).
 template <int BM, int BN, int WM, int WN, int MODE, int D, int BKT = 64>
-__global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p) {
+__global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_kernel(
+    const KvConvParams p) {
+  constexpr int NW = WM * WN;     // waves per workgroup
+  constexpr int NT = 64 * NW;     // threads per workgroup
   constexpr int BK = BKT;         // shadows the file-scope 64
   constexpr int CH = BK / 8;      // 16-B chunks per LDS row
   constexpr int RPI = 64 / CH;    // rows per DMA instruction (64 lanes x 16 B)
   constexpr int KS = BK / 16;     // MFMA K steps per stage
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
-  constexpr int A_INS = BM / (4 * RPI);  // DMA instructions per wave per stage
-  constexpr int B_INS = BN / (4 * RPI);
+  constexpr int A_INS = BM / (NW * RPI);  // DMA instructions per wave per stage
+  constexpr int B_INS = BN / (NW * RPI);
   constexpr int STAGE = (BM + BN) * BK;
   static_assert(BK == 64 || BK == 32, "BK");
   static_assert(A_INS >= 1 && B_INS >= 1, "tile too small for BK");
-  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1 && D >= 2 && D <= 6, "tile");
+  static_assert((NW == 4 || NW == 8) && TM >= 1 && TN >= 1 && D >= 2 && D <= 6, "tile");
   // chunk swizzle of row r: ds_read_b128 of 16 rows x one logical chunk is conflict-free
   auto sw = [](int r) __attribute__((always_inline)) {
     return BK == 64 ? ((r >> 1) & 7) : ((r >> 2) & 3);
@@ -90,19 +99,28 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
 
   // ---- residual prefetch: issued before the K loop, consumed by the epilogue, so its
   // latency hides under the GEMM instead of serialising after it (memory-bound layers).
-  constexpr int CPR = BN / 8;
-  constexpr int PER = BM * CPR / 256;
+  // The epilogue stages the C tile through LDS in NSPLIT column halves when the whole
+  // (padded) tile does not fit the ring (256x256); chunk j of half h -> rpre[h * PERH + j].
+  constexpr int NSPLIT = BM * (BN + 8) <= D * STAGE ? 1 : 2;
+  constexpr int BNH = BN / NSPLIT;  // columns per epilogue pass
+  static_assert(WTN <= BNH && BNH % WTN == 0, "a wave's columns lie in one epilogue pass");
+  static_assert(BM * (BNH + 8) <= D * STAGE, "C tile (pass) fits");
+  constexpr int CPR = BNH / 8;
+  constexpr int PERH = BM * CPR / NT;
+  constexpr int PER = PERH * NSPLIT;
   constexpr bool kPrefetchRes = PER <= 8;
   bf16x8 rpre[kPrefetchRes ? PER : 1];
   if (kPrefetchRes && p.res) {
     const bf16* R = reinterpret_cast<const bf16*>(p.res);
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int idx = threadIdx.x + 256 * j;
-      const int m = m0 + idx / CPR, n = n0 + (idx % CPR) * 8;
-      if (m < p.M && n < p.Cout)
-        rpre[j] = *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
-    }
+    for (int h = 0; h < NSPLIT; ++h)
+#pragma unroll
+      for (int j = 0; j < PERH; ++j) {
+        const int idx = threadIdx.x + NT * j;
+        const int m = m0 + idx / CPR, n = n0 + h * BNH + (idx % CPR) * 8;
+        if (m < p.M && n < p.Cout)
+          rpre[h * PERH + j] = *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
+      }
   }
 
   // ---- per-lane source descriptors (constant over the K loop) -------------
@@ -317,47 +335,52 @@ __global__ __launch_bounds__(256, 2) void conv_glds_kernel(const KvConvParams p)
   __syncthreads();
 
   // ---- fused epilogue through LDS (see conv_igemm.hip) ----------------------
-  constexpr int CS = BN + 8;
-  static_assert(BM * CS <= D * STAGE, "C tile fits");
+  constexpr int CS = BNH + 8;
   const bool has_res = p.res != nullptr;
   bf16* __restrict__ Y = reinterpret_cast<bf16*>(p.y);
   const bf16* __restrict__ R = reinterpret_cast<const bf16*>(p.res);
   dispatch_act(p.act, has_res, [&](auto A1, auto A2) __attribute__((always_inline)) {
     constexpr int act1 = decltype(A1)::value, act2 = decltype(A2)::value;
 #pragma unroll
-    for (int tn = 0; tn < TN; ++tn) {
+    for (int h = 0; h < NSPLIT; ++h) {
+      if (h > 0) __syncthreads();  // previous pass's C tile fully read
+      if (wn * WTN / BNH == h) {   // this wave's columns belong to pass h
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int nl = wn * WTN + tn * 32 + g * 8 + fh * 4;
-        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (p.bias && n0 + nl < p.Cout) bv = *reinterpret_cast<const float4*>(p.bias + n0 + nl);
+        for (int tn = 0; tn < TN; ++tn) {
 #pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
-          const int ml = wm * WTM + tm * 32 + fr;
-          bf16x4 o;
-          o[0] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 0] + bv.x));
-          o[1] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 1] + bv.y));
-          o[2] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 2] + bv.z));
-          o[3] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 3] + bv.w));
-          *reinterpret_cast<bf16x4*>(smem + ml * CS + nl) = o;
+          for (int g = 0; g < 4; ++g) {
+            const int nl = wn * WTN + tn * 32 + g * 8 + fh * 4;
+            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (p.bias && n0 + nl < p.Cout) bv = *reinterpret_cast<const float4*>(p.bias + n0 + nl);
+#pragma unroll
+            for (int tm = 0; tm < TM; ++tm) {
+              const int ml = wm * WTM + tm * 32 + fr;
+              bf16x4 o;
+              o[0] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 0] + bv.x));
+              o[1] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 1] + bv.y));
+              o[2] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 2] + bv.z));
+              o[3] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 3] + bv.w));
+              *reinterpret_cast<bf16x4*>(smem + ml * CS + nl - h * BNH) = o;
+            }
+          }
         }
       }
-    }
-    __syncthreads();
+      __syncthreads();
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int idx = tid + 256 * j;
-      const int ml = idx / CPR, ch = idx % CPR;
-      const int m = m0 + ml, n = n0 + ch * 8;
-      if (m >= p.M || n >= p.Cout) continue;
-      bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + ml * CS + ch * 8);
-      if (has_res) {
-        const bf16x8 rv = kPrefetchRes ? rpre[kPrefetchRes ? j : 0]
-                                       : *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
+      for (int j = 0; j < PERH; ++j) {
+        const int idx = tid + NT * j;
+        const int ml = idx / CPR, ch = idx % CPR;
+        const int m = m0 + ml, n = n0 + h * BNH + ch * 8;
+        if (m >= p.M || n >= p.Cout) continue;
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + ml * CS + ch * 8);
+        if (has_res) {
+          const bf16x8 rv = kPrefetchRes ? rpre[kPrefetchRes ? h * PERH + j : 0]
+                                         : *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = f2bf(act_c<act2>((float)v[e] + (float)rv[e]));
+          for (int e = 0; e < 8; ++e) v[e] = f2bf(act_c<act2>((float)v[e] + (float)rv[e]));
+        }
+        *reinterpret_cast<bf16x8*>(Y + (size_t)m * p.ldy + p.y_coff + n) = v;
       }
-      *reinterpret_cast<bf16x8*>(Y + (size_t)m * p.ldy + p.y_coff + n) = v;
     }
   });
 }
@@ -379,6 +402,7 @@ ConvKernelFn glds_get(int mode) {
 struct GldsTile {
   int bm, bn;
   ConvKernelFn (*get)(int);
+  int nt = 256;  // threads per workgroup (64 x waves)
 };
 
 static const GldsTile kGldsTiles[] = {
@@ -406,6 +430,14 @@ static const GldsTile kGldsTiles[] = {
     // cls convs waste 17 % of the MFMA columns here instead of 37.5 % on a BN = 128 tile
     {128, 96, &glds_get<128, 96, 4, 1>},
     {256, 96, &glds_get<256, 96, 4, 1>},
+    // 8 waves (512 threads), one workgroup per CU, two waves per SIMD: 256x256 with a
+    // 128x64 / 64x128 sub-tile per wave (epilogue in two column passes), and 256x128 /
+    // 128x256 with 64x64 per wave but the B / A tile shared by twice the waves
+    {256, 256, &glds_get<256, 256, 2, 4>, 512},
+    {256, 256, &glds_get<256, 256, 4, 2>, 512},
+    {256, 128, &glds_get<256, 128, 4, 2>, 512},
+    {128, 256, &glds_get<128, 256, 2, 4>, 512},
+    {256, 128, &glds_get<256, 128, 4, 2, 3>, 512},
     // (BK = 32 rings -- glds_get<128, 128, 2, 2, 5, 32> etc., 4-5 K steps in flight at 2
     // workgroups per CU -- measured 10-40 % SLOWER than {128, 128} D = 2 on every 3x3 and
     // 1x1 layer of ResNet-50 at batch 640 (profiles/r1_v10_tile_probe_bk32.md): the 3x3
@@ -430,7 +462,7 @@ int glds_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   const GldsTile& e = kGldsTiles[tile];
   const long long nwg = (long long)((p->M + e.bm - 1) / e.bm) * ((p->Cout + e.bn - 1) / e.bn);
   if (nwg <= 0) return 0;
-  hipLaunchKernelGGL(e.get(mode), dim3((unsigned)nwg), dim3(256), 0, stream, *p);
+  hipLaunchKernelGGL(e.get(mode), dim3((unsigned)nwg), dim3(e.nt), 0, stream, *p);
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }
 

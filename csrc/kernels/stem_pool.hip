@@ -184,6 +184,7 @@ __global__ __launch_bounds__(NT, 1) void stem_pool_kernel(
     }
   };
 
+  const FastDiv fW = make_fastdiv(W);  // once per thread; j / W per row block below
   int item = blockIdx.x;
   fetch(item);
   commit();
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(NT, 1) void stem_pool_kernel(
     const int nrb = (npix + 31) / 32;
     for (int rb = wv; rb < nrb; rb += kNW) {
       const int j = min(rb * 32 + fr, npix - 1);  // clamp: rows past npix are discarded
-      const int yl = j / W, xc = j - yl * W;
+      const int yl = fdiv(j, fW), xc = j - yl * W;
       const unsigned char* pa = patch + patch_off(yl * kPW + xc, fh);
       floatx16 acc[2];
 #pragma unroll

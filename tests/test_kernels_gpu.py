@@ -82,9 +82,10 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale + 0.02
 
 
-N_TILES = 43  # v1 register-staged (0-5) + v2 LDS-DMA (6-23) + v3 streaming (24-40) + v4 direct (41-42)
-STREAM0 = 24  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
-DIRECT0 = 41  # v4 direct 3x3 (conv_direct.hip): its instantiation table only
+N_TILES = 48  # v1 register-staged (0-5) + v2 LDS-DMA (6-28) + v3 streaming (29-45) + v4 direct (46-47)
+STREAM0 = 29  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
+DIRECT0 = 46  # v4 direct 3x3 (conv_direct.hip): its instantiation table only
+GLDS8 = list(range(24, 29))  # v2 8-wave (512-thread) tiles: 256x256 x2, 256x128, 128x256, 256x128 D3
 # v3 (bm, bn, ring depth, weight slice resident in LDS) -- conv_stream.hip kStreamTiles
 STREAM_TILES = [(64, 64, 4, True), (64, 128, 4, True), (128, 64, 4, True), (64, 64, 6, True),
                 (64, 128, 3, True), (64, 64, 4, False), (128, 64, 4, False), (128, 128, 3, False),

@@ -39,8 +39,11 @@ def main():
         for _ in range(3):
             eng.run()
         dt = eng.run_timed(a.steps)
+        lat = eng.measure_latency(a.steps)  # synchronised per step: edge-module latency
         r = {"model": a.model, "batch": b, "microbatch": mb, "mb_blocks": nb,
-             "images_per_s": round(b * a.steps / dt, 1), "ms_per_step": round(dt / a.steps * 1e3, 3)}
+             "images_per_s": round(b * a.steps / dt, 1), "ms_per_step": round(dt / a.steps * 1e3, 3),
+             "latency_p50_ms": round(lat.percentile(50), 3),
+             "latency_p99_ms": round(lat.percentile(99), 3)}
         print(json.dumps(r), flush=True)
         with open(a.out, "a") as f:
             f.write(json.dumps(r) + "\n")
