@@ -29,6 +29,12 @@
 #include "kvedge_kernels.h"
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+template <int MF>
+struct AccOf { typedef floatx16 type; static constexpr int n = 16; };
+template <>
+struct AccOf<16> { typedef floatx4 type; static constexpr int n = 4; };
 
 namespace kvedge {
 namespace {
@@ -62,7 +68,12 @@ __device__ __forceinline__ void wait_vm() {
 // 128x64 (or 64x128) sub-tile -- 0.75 fragment reads per MFMA -- while keeping two waves
 // per SIMD for latency hiding, which no 4-wave tile combines (a 4-wave 256x128 tile has
 // the sub-tile but one wave per SIMD).
-template <int BM, int BN, int WM, int WN, int MODE, int D, int BKT = 64>
+//
+// MF = MFMA shape: 32 = v_mfma_f32_32x32x16_bf16, 16 = v_mfma_f32_16x16x32_bf16.  Same LDS
+// image and the same fragment bytes per FLOP (a 16x16x32 fragment is 16 rows x 32 k, a
+// 32x32x16 one 32 rows x 16 k: both one ds_read_b128); the 16x16x32 loop holds a higher
+// clock under load (MI355X_MICROARCH.md, DVFS item 7) at twice the MFMA count.
+template <int BM, int BN, int WM, int WN, int MODE, int D, int BKT = 64, int MF = 32>
 __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_kernel(
     const KvConvParams p) {
   constexpr int NW = WM * WN;     // waves per workgroup
@@ -70,9 +81,12 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
   constexpr int BK = BKT;         // shadows the file-scope 64
   constexpr int CH = BK / 8;      // 16-B chunks per LDS row
   constexpr int RPI = 64 / CH;    // rows per DMA instruction (64 lanes x 16 B)
-  constexpr int KS = BK / 16;     // MFMA K steps per stage
+  constexpr int KS = BK / (MF == 32 ? 16 : 32);  // MFMA K steps per stage
   constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int TM = WTM / MF, TN = WTN / MF;
+  static_assert(MF == 32 || MF == 16, "MFMA shape");
+  using Acc = typename AccOf<MF>::type;
+  constexpr int NACC = AccOf<MF>::n;
   constexpr int A_INS = BM / (NW * RPI);  // DMA instructions per wave per stage
   constexpr int B_INS = BN / (NW * RPI);
   constexpr int STAGE = (BM + BN) * BK;
@@ -255,15 +269,17 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
     for (int i = 0; i < B_INS; ++i) glds16(rw, Bs + (wv * B_INS + i) * 512, b_off[i], kt * BK * 2);
   };
 
-  floatx16 acc[TN][TM];
+  Acc acc[TN][TM];
 #pragma unroll
   for (int a = 0; a < TN; ++a)
 #pragma unroll
     for (int b = 0; b < TM; ++b)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+      for (int e = 0; e < NACC; ++e) acc[a][b][e] = 0.f;
 
-  const int fr = lane & 31, fh = lane >> 5;
+  // fragment lane roles: 32x32x16 -> row lane & 31, k half lane >> 5 (8 of 16);
+  // 16x16x32 -> row lane & 15, k quarter lane >> 4 (8 of 32)
+  const int fr = lane & (MF - 1), fh = lane / MF;
   auto compute = [&](int stage) {
     const bf16* As = smem + stage * STAGE;
     const bf16* Bs = As + BM * BK;
@@ -272,15 +288,15 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
     // an lgkmcnt(0) stall in front of every group of MFMAs
     bf16x8 af[2][TM], bfg[2][TN];
     auto load = [&](int buf, int ks) __attribute__((always_inline)) {
-      const int q = ks * 2 + fh;
+      const int q = ks * (64 / MF) + fh;  // logical 16-B chunk of the row
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
-        const int row = wm * WTM + tm * 32 + fr;
+        const int row = wm * WTM + tm * MF + fr;
         af[buf][tm] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((q ^ sw(row)) << 3));
       }
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
-        const int row = wn * WTN + tn * 32 + fr;
+        const int row = wn * WTN + tn * MF + fr;
         bfg[buf][tn] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((q ^ sw(row)) << 3));
       }
     };
@@ -291,9 +307,14 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
-        for (int tm = 0; tm < TM; ++tm)
-          acc[tn][tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfg[ks & 1][tn], af[ks & 1][tm],
-                                                                acc[tn][tm], 0, 0, 0);
+        for (int tm = 0; tm < TM; ++tm) {
+          if constexpr (MF == 32)
+            acc[tn][tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfg[ks & 1][tn], af[ks & 1][tm],
+                                                                  acc[tn][tm], 0, 0, 0);
+          else
+            acc[tn][tm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[ks & 1][tn], af[ks & 1][tm],
+                                                                  acc[tn][tm], 0, 0, 0);
+        }
     }
     // pin the order for the scheduler (it otherwise re-coalesces both register sets):
     // reads(0) | reads(1) MFMAs(0) | reads(2) MFMAs(1) | reads(3) MFMAs(2) | MFMAs(3)
@@ -345,16 +366,18 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
     for (int h = 0; h < NSPLIT; ++h) {
       if (h > 0) __syncthreads();  // previous pass's C tile fully read
       if (wn * WTN / BNH == h) {   // this wave's columns belong to pass h
+        // accumulator register r of a lane: 32x32 -> channel g*8 + fh*4 + j (g = r / 4,
+        // j = r % 4), pixel lane & 31;  16x16 -> channel fh*4 + j, pixel lane & 15
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn) {
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int nl = wn * WTN + tn * 32 + g * 8 + fh * 4;
+          for (int g = 0; g < NACC / 4; ++g) {
+            const int nl = wn * WTN + tn * MF + g * 8 + fh * 4;
             float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
             if (p.bias && n0 + nl < p.Cout) bv = *reinterpret_cast<const float4*>(p.bias + n0 + nl);
 #pragma unroll
             for (int tm = 0; tm < TM; ++tm) {
-              const int ml = wm * WTM + tm * 32 + fr;
+              const int ml = wm * WTM + tm * MF + fr;
               bf16x4 o;
               o[0] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 0] + bv.x));
               o[1] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 1] + bv.y));
@@ -389,13 +412,13 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
 
 typedef void (*ConvKernelFn)(const KvConvParams);
 
-template <int BM, int BN, int WM, int WN, int D = 2, int BKT = 64>
+template <int BM, int BN, int WM, int WN, int D = 2, int BKT = 64, int MF = 32>
 ConvKernelFn glds_get(int mode) {
   switch (mode) {
-    case 0: return conv_glds_kernel<BM, BN, WM, WN, 0, D, BKT>;
-    case 1: return conv_glds_kernel<BM, BN, WM, WN, 1, D, BKT>;
-    case 4: return conv_glds_kernel<BM, BN, WM, WN, 4, D, BKT>;
-    default: return conv_glds_kernel<BM, BN, WM, WN, 3, D, BKT>;
+    case 0: return conv_glds_kernel<BM, BN, WM, WN, 0, D, BKT, MF>;
+    case 1: return conv_glds_kernel<BM, BN, WM, WN, 1, D, BKT, MF>;
+    case 4: return conv_glds_kernel<BM, BN, WM, WN, 4, D, BKT, MF>;
+    default: return conv_glds_kernel<BM, BN, WM, WN, 3, D, BKT, MF>;
   }
 }
 
@@ -438,6 +461,10 @@ static const GldsTile kGldsTiles[] = {
     {256, 128, &glds_get<256, 128, 4, 2>, 512},
     {128, 256, &glds_get<128, 256, 2, 4>, 512},
     {256, 128, &glds_get<256, 128, 4, 2, 3>, 512},
+    // the same loops on v_mfma_f32_16x16x32_bf16 (MF = 16)
+    {128, 128, &glds_get<128, 128, 2, 2, 2, 64, 16>},
+    {256, 256, &glds_get<256, 256, 4, 2, 2, 64, 16>, 512},
+    {256, 128, &glds_get<256, 128, 4, 2, 2, 64, 16>, 512},
     // (BK = 32 rings -- glds_get<128, 128, 2, 2, 5, 32> etc., 4-5 K steps in flight at 2
     // workgroups per CU -- measured 10-40 % SLOWER than {128, 128} D = 2 on every 3x3 and
     // 1x1 layer of ResNet-50 at batch 640 (profiles/r1_v10_tile_probe_bk32.md): the 3x3

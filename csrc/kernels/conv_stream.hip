@@ -27,7 +27,13 @@
 #include <cstdlib>
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int MF>
+struct SAccOf { typedef floatx16 type; static constexpr int n = 16; };
+template <>
+struct SAccOf<16> { typedef floatx4 type; static constexpr int n = 4; };
 
 namespace kvedge {
 namespace {
@@ -68,14 +74,18 @@ __host__ __device__ constexpr int stream_lds_bytes(int bm, int bn, int d, bool r
 
 // NT1 > 0: fused bottleneck tail -- after the y tile is written, z = ReLU(y . Wt^T + bt)
 // (the next block's 1x1 reduce, NT1 output channels) is computed from the y tile in LDS.
-template <int BM, int BN, int D, int MODE, bool RES, bool BRES, int POL, int NT1 = 0>
+// MF: main-GEMM MFMA shape (32 = 32x32x16, 16 = 16x16x32; see conv_glds.hip); the fused
+// tail GEMM always runs on 32x32x16.
+template <int BM, int BN, int D, int MODE, bool RES, bool BRES, int POL, int NT1 = 0, int MF = 32>
 // 128x128 resident-weight tiles (and the tail tiles) hold >100 KB of weights: one
 // workgroup per CU, so they may use the whole 512-entry register file
 __global__ __launch_bounds__(256, (NT1 || (BM * BN >= 128 * 128 && BRES)) ? 1 : 2)
 void conv_stream_kernel(const KvConvParams p) {
   constexpr int WM = 2, WN = 2;
   constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int TM = WTM / MF, TN = WTN / MF;
+  using Acc = typename SAccOf<MF>::type;
+  constexpr int NACC = SAccOf<MF>::n;
   constexpr int A_INS = BM / 32, B_INS = BN / 32;
   constexpr int CS = BN + 8;
   constexpr int CPR = BN / 8;
@@ -182,17 +192,19 @@ void conv_stream_kernel(const KvConvParams p) {
     }
   };
 
-  floatx16 acc[TN][TM];
+  Acc acc[TN][TM];
   auto zero_acc = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int a = 0; a < TN; ++a)
 #pragma unroll
       for (int b = 0; b < TM; ++b)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+        for (int e = 0; e < NACC; ++e) acc[a][b][e] = 0.f;
   };
 
-  const int fr = lane & 31, fh = lane >> 5;
+  // main-GEMM fragment roles (MF); the tail GEMM keeps the 32x32 roles fr32/fh32
+  const int fr = lane & (MF - 1), fh = lane / MF;
+  const int fr32 = lane & 31, fh32 = lane >> 5;
   auto compute = [&](int slot, int kt) __attribute__((always_inline)) {
     const bf16* As = smem + slot * SLOT;
     const bf16* Bs = BRES ? Bres + kt * BN * BK : As + SA;
@@ -200,36 +212,42 @@ void conv_stream_kernel(const KvConvParams p) {
     // before the MFMAs of step ks, so LDS latency hides under the MFMA pipe instead of
     // an lgkmcnt(0) stall in front of every group of MFMAs
     bf16x8 af[2][TM], bfg[2][TN];
+    constexpr int KS = BK / (MF == 32 ? 16 : 32);
     auto load = [&](int buf, int ks) __attribute__((always_inline)) {
-      const int q = ks * 2 + fh;
+      const int q = ks * (64 / MF) + fh;
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
-        const int row = wm * WTM + tm * 32 + fr;
+        const int row = wm * WTM + tm * MF + fr;
         af[buf][tm] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((q ^ ((row >> 1) & 7)) << 3));
       }
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
-        const int row = wn * WTN + tn * 32 + fr;
+        const int row = wn * WTN + tn * MF + fr;
         bfg[buf][tn] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((q ^ ((row >> 1) & 7)) << 3));
       }
     };
     load(0, 0);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      if (ks < 3) load((ks + 1) & 1, ks + 1);
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks < KS - 1) load((ks + 1) & 1, ks + 1);
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
-        for (int tm = 0; tm < TM; ++tm)
-          acc[tn][tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfg[ks & 1][tn], af[ks & 1][tm],
-                                                                acc[tn][tm], 0, 0, 0);
+        for (int tm = 0; tm < TM; ++tm) {
+          if constexpr (MF == 32)
+            acc[tn][tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfg[ks & 1][tn], af[ks & 1][tm],
+                                                                  acc[tn][tm], 0, 0, 0);
+          else
+            acc[tn][tm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[ks & 1][tn], af[ks & 1][tm],
+                                                                  acc[tn][tm], 0, 0, 0);
+        }
     }
     // pin the order for the scheduler (it otherwise re-coalesces both register sets):
     // reads(0) | reads(1) MFMAs(0) | reads(2) MFMAs(1) | reads(3) MFMAs(2) | MFMAs(3)
     __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      if (ks < 3) __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks < KS - 1) __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
     }
   };
@@ -237,12 +255,12 @@ void conv_stream_kernel(const KvConvParams p) {
 
   // this lane's bias values for the whole run (the N slice is fixed): registers, not
   // LDS -- an LDS read in the epilogue would make hipcc drain the in-flight DMA.
-  float4 bias_r[TN][4];
+  float4 bias_r[TN][NACC / 4];
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int n = n0 + wn * WTN + tn * 32 + g * 8 + fh * 4;
+    for (int g = 0; g < NACC / 4; ++g) {
+      const int n = n0 + wn * WTN + tn * MF + g * 8 + fh * 4;
       bias_r[tn][g] = (p.bias && n < p.Cout) ? *reinterpret_cast<const float4*>(p.bias + n)
                                              : make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -256,7 +274,7 @@ void conv_stream_kernel(const KvConvParams p) {
     for (int tn = 0; tn < TN1; ++tn)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int n = (wv & 1) * (NT1 / 2) + tn * 32 + g * 8 + fh * 4;
+        const int n = (wv & 1) * (NT1 / 2) + tn * 32 + g * 8 + fh32 * 4;
         bias1_r[tn][g] = p.bias_t ? *reinterpret_cast<const float4*>(p.bias_t + n)
                                   : make_float4(0.f, 0.f, 0.f, 0.f);
       }
@@ -280,11 +298,11 @@ void conv_stream_kernel(const KvConvParams p) {
       }
 #pragma unroll
     for (int kk = 0; kk < BN / 16; ++kk) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(Cs + (wm2 * 32 + fr) * CS + kk * 16 + fh * 8);
-      const int kt = kk >> 2, q = (kk & 3) * 2 + fh;
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(Cs + (wm2 * 32 + fr32) * CS + kk * 16 + fh32 * 8);
+      const int kt = kk >> 2, q = (kk & 3) * 2 + fh32;
 #pragma unroll
       for (int tn = 0; tn < TN1; ++tn) {
-        const int row = wn2 * (NT1 / 2) + tn * 32 + fr;
+        const int row = wn2 * (NT1 / 2) + tn * 32 + fr32;
         const bf16x8 b = *reinterpret_cast<const bf16x8*>(
             W1s + kt * NT1 * BK + row * BK + ((q ^ ((row >> 1) & 7)) << 3));
         acc2[tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, a, acc2[tn], 0, 0, 0);
@@ -298,13 +316,13 @@ void conv_stream_kernel(const KvConvParams p) {
     for (int tn = 0; tn < TN1; ++tn)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int nl = wn2 * (NT1 / 2) + tn * 32 + g * 8 + fh * 4;
+        const int nl = wn2 * (NT1 / 2) + tn * 32 + g * 8 + fh32 * 4;
         bf16x4 o;
         o[0] = f2bf(fmaxf(acc2[tn][4 * g + 0], 0.f));
         o[1] = f2bf(fmaxf(acc2[tn][4 * g + 1], 0.f));
         o[2] = f2bf(fmaxf(acc2[tn][4 * g + 2], 0.f));
         o[3] = f2bf(fmaxf(acc2[tn][4 * g + 3], 0.f));
-        *reinterpret_cast<bf16x4*>(Cs + (wm2 * 32 + fr) * CZ + nl) = o;
+        *reinterpret_cast<bf16x4*>(Cs + (wm2 * 32 + fr32) * CZ + nl) = o;
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -328,12 +346,12 @@ void conv_stream_kernel(const KvConvParams p) {
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int nl = wn * WTN + tn * 32 + g * 8 + fh * 4;
+      for (int g = 0; g < NACC / 4; ++g) {
+        const int nl = wn * WTN + tn * MF + g * 8 + fh * 4;
         const float4 bv = bias_r[tn][g];
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm) {
-          const int ml = wm * WTM + tm * 32 + fr;
+          const int ml = wm * WTM + tm * MF + fr;
           bf16x4 o;
           o[0] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 0] + bv.x));
           o[1] = f2bf(act_c<act1>(acc[tn][tm][4 * g + 1] + bv.y));
@@ -429,26 +447,26 @@ void conv_stream_kernel(const KvConvParams p) {
 
 typedef void (*StreamFn)(const KvConvParams);
 
-template <int BM, int BN, int D, bool BRES, int POL = 0>
+template <int BM, int BN, int D, bool BRES, int POL = 0, int MF = 32>
 StreamFn stream_get(int mode, bool res, int nt) {
   if (nt) return nullptr;
-  if (mode == 4) return conv_stream_kernel<BM, BN, D, 4, false, BRES, POL>;
-  return res ? conv_stream_kernel<BM, BN, D, 1, true, BRES, POL>
-             : conv_stream_kernel<BM, BN, D, 1, false, BRES, POL>;
+  if (mode == 4) return conv_stream_kernel<BM, BN, D, 4, false, BRES, POL, 0, MF>;
+  return res ? conv_stream_kernel<BM, BN, D, 1, true, BRES, POL, 0, MF>
+             : conv_stream_kernel<BM, BN, D, 1, false, BRES, POL, 0, MF>;
 }
 
 // tail-capable tile: plain BRES tile for nt == 0, fused bottleneck tail for nt = 64 / 128
 // (conv3 + residual -> next conv1, or the fused-downsample dual GEMM -> next conv1)
-template <int BM, int BN, int D>
+template <int BM, int BN, int D, int MF = 32>
 StreamFn stream_get_tail(int mode, bool res, int nt) {
-  if (nt == 0) return stream_get<BM, BN, D, true>(mode, res, 0);
+  if (nt == 0) return stream_get<BM, BN, D, true, 0, MF>(mode, res, 0);
   if constexpr (D == 3) if (nt == 64) {
-    if (mode == 4) return conv_stream_kernel<BM, BN, D, 4, false, true, 0, 64>;
-    return res ? conv_stream_kernel<BM, BN, D, 1, true, true, 0, 64> : nullptr;
+    if (mode == 4) return conv_stream_kernel<BM, BN, D, 4, false, true, 0, 64, MF>;
+    return res ? conv_stream_kernel<BM, BN, D, 1, true, true, 0, 64, MF> : nullptr;
   }
   if constexpr (D == 2) if (nt == 128) {
-    if (mode == 4) return conv_stream_kernel<BM, BN, D, 4, false, true, 0, 128>;
-    return res ? conv_stream_kernel<BM, BN, D, 1, true, true, 0, 128> : nullptr;
+    if (mode == 4) return conv_stream_kernel<BM, BN, D, 4, false, true, 0, 128, MF>;
+    return res ? conv_stream_kernel<BM, BN, D, 1, true, true, 0, 128, MF> : nullptr;
   }
   return nullptr;
 }
@@ -480,6 +498,13 @@ static const StreamTile kStreamTiles[] = {
     {128, 128, 3, true, &stream_get<128, 128, 3, true>},
     {128, 128, 2, true, &stream_get<128, 128, 2, true>},
     {128, 128, 3, true, &stream_get<128, 128, 3, true, 2>},
+    // v_mfma_f32_16x16x32 main GEMM (MF = 16) of the tiles the autotuner picks for
+    // ResNet-50 (stage-3 expand, stage-2 expand / reduce) and of both tail tiles
+    {64, 64, 4, true, &stream_get<64, 64, 4, true, 0, 16>},
+    {64, 128, 3, true, &stream_get<64, 128, 3, true, 0, 16>},
+    {128, 128, 3, false, &stream_get<128, 128, 3, false, 2, 16>},
+    {64, 256, 3, true, &stream_get_tail<64, 256, 3, 16>},
+    {64, 256, 2, true, &stream_get_tail<64, 256, 2, 16>},
     // 64 x 256 resident slice; also the fused bottleneck-tail tiles (stream_tail_tile):
     // D = 3 for a 64-channel tail, D = 2 for a 128-channel one (register budget)
     {64, 256, 3, true, &stream_get_tail<64, 256, 3>},

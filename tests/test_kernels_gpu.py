@@ -82,15 +82,18 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale + 0.02
 
 
-N_TILES = 48  # v1 register-staged (0-5) + v2 LDS-DMA (6-28) + v3 streaming (29-45) + v4 direct (46-47)
-STREAM0 = 29  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
-DIRECT0 = 46  # v4 direct 3x3 (conv_direct.hip): its instantiation table only
-GLDS8 = list(range(24, 29))  # v2 8-wave (512-thread) tiles: 256x256 x2, 256x128, 128x256, 256x128 D3
+N_TILES = 56  # v1 register-staged (0-5) + v2 LDS-DMA (6-31) + v3 streaming (32-53) + v4 direct (54-55)
+STREAM0 = 32  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
+DIRECT0 = 54  # v4 direct 3x3 (conv_direct.hip): its instantiation table only
+# v2 8-wave (512-thread) tiles 24-28 (256x256 x2, 256x128, 128x256, 256x128 D3) and the
+# v_mfma_f32_16x16x32 forms 29-31 (128x128 4-wave, 256x256 and 256x128 8-wave)
 # v3 (bm, bn, ring depth, weight slice resident in LDS) -- conv_stream.hip kStreamTiles
 STREAM_TILES = [(64, 64, 4, True), (64, 128, 4, True), (128, 64, 4, True), (64, 64, 6, True),
                 (64, 128, 3, True), (64, 64, 4, False), (128, 64, 4, False), (128, 128, 3, False),
                 (64, 128, 4, False), (64, 128, 3, True), (64, 64, 4, True), (128, 128, 3, False),
                 (128, 128, 3, True), (128, 128, 2, True), (128, 128, 3, True),
+                (64, 64, 4, True), (64, 128, 3, True), (128, 128, 3, False),  # MF = 16 forms
+                (64, 256, 3, True), (64, 256, 2, True),                       # MF = 16 tails
                 (64, 256, 3, True), (64, 256, 2, True)]
 
 
@@ -425,11 +428,14 @@ def test_stem_pool_fused(shape):
     (2, 28, 28, 64, 64, 1, 64),    # fused downsample dual form (layer1 block 0)
     (1, 9, 7, 64, 64, 2, 64),      # dual with a strided second source
 ])
-def test_conv_tail_fused(case):
+@pytest.mark.parametrize("mf", [32, 16])
+def test_conv_tail_fused(case, mf):
     """v3 fused bottleneck tail: y = ReLU(t . W3 (+ x . Wd) + b (+ res)) and the next
     block's conv1 z = ReLU(y . W1 + b1) in one kernel, vs the reference composition."""
     N, H, W, k1, k2, s2, nt = case
     cout = 256
+    # default tile = the 32x32x16 tail of this n_t; the v_mfma_f32_16x16x32 tails sit 2 before
+    tile = -1 if mf == 32 else DIRECT0 - (4 if nt == 64 else 3)
     g = torch.Generator().manual_seed(nt + k2 + H)
     t = _rand((N, H, W, k1), 1)
     w = (torch.randn(cout, k1 + k2, generator=g) * (2.0 / (k1 + k2)) ** 0.5).to(torch.bfloat16)
@@ -440,12 +446,12 @@ def test_conv_tail_fused(case):
         x2 = _rand((N, H * s2, W * s2, k2), 2)
         y_ref, z_ref = ops.conv_tail(t, w, b, ops.ACT_RELU, w1, b1, x2=x2, stride2=s2)
         y, z = ops.conv_tail(t.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, w1.cuda(), b1.cuda(),
-                             x2=x2.cuda(), stride2=s2)
+                             x2=x2.cuda(), stride2=s2, tile=tile)
     else:
         r = _rand((N, H, W, cout), 3)
         y_ref, z_ref = ops.conv_tail(t, w, b, ops.ACT_RELU, w1, b1, res=r)
         y, z = ops.conv_tail(t.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, w1.cuda(), b1.cuda(),
-                             res=r.cuda())
+                             res=r.cuda(), tile=tile)
     torch.cuda.synchronize()
     for got, ref in ((y, y_ref), (z, z_ref)):
         err = (got.cpu().float() - ref.float()).abs().max().item()
