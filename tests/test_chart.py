@@ -411,3 +411,16 @@ def test_config_toml_is_git_ignored():
     if subprocess.run(["git", "-C", ROOT, "rev-parse"], capture_output=True).returncode == 0:
         r = subprocess.run(["git", "-C", ROOT, "check-ignore", "-q", "config.toml"])
         assert r.returncode == 0
+
+
+def test_guest_image_build_targets_guest_kernel():
+    """DKMS under virt-customize builds for the appliance kernel unless
+    told otherwise.  The build script builds amdgpu for the image's own kernel, fails the
+    build if the module is missing, and pre-loads the edge runtime images (no pull at boot)."""
+    p = os.path.join(ROOT, "deploy", "image", "build-disk.sh")
+    txt = open(p).read()
+    assert subprocess.run(["bash", "-n", p]).returncode == 0
+    assert "dkms autoinstall -k \\$KVER" in txt and "modinfo -k \\$KVER amdgpu" in txt
+    assert "set -euo pipefail" in txt
+    assert "kvedge-preload.service" in txt and "Before=aziot-edged.service" in txt
+    assert "docker save" in txt and "--copy-in build/images:/var/lib/kvedge" in txt
