@@ -82,6 +82,11 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
                                                                 FastDiv fPW, FastDiv fWo) {
   static_assert(!U8 || (CIN == 16 && KK == 2 && S == 1), "frames-in form: the 2x2 s2d stem");
   static_assert(!PAIRS || U8, "paired raw-row loads: frames-in form only");
+  // KK = 1: a 1x1 conv through the same band machinery (pad 0): YOLO's narrow C2f / Detect
+  // 1x1 convs at 160^2 / 80^2 are pure streaming, and the GEMM tiles' per-tile epilogue
+  // overhead (K = 32..192, one or three K steps per tile) held them at 2.4-3.5 TB/s
+  static_assert(KK != 1 || S == 1, "1x1 form: stride 1");
+  constexpr int PADK = KK == 1 ? 0 : 1;
   using C = DirectCfg<CIN, KK>;
   constexpr int NCB = (COUT + 31) / 32;  // 32-channel blocks
   static_assert(NCB >= 1 && NCB <= 4, "channel blocks");
@@ -152,7 +157,7 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
   unsigned okp = 0;
   auto fetch = [&](int item) __attribute__((always_inline)) {
     const int n = item / nbands, band = item - n * nbands;
-    const int iy0 = band * kR * S - 1;
+    const int iy0 = band * kR * S - PADK;
     const bool live = item < total;
     if constexpr (PAIRS) {
       {
@@ -177,7 +182,7 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
       int pp, c;
       chunk_of(q, pp, c);
       const int pr = fdiv(pp, fPW), pc = pp - pr * PW;
-      const int iy = iy0 + pr, ix = pc - 1;
+      const int iy = iy0 + pr, ix = pc - PADK;
       const bool ok = live && q < nchunks && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
       if constexpr (U8) {
         // s2d chunk c of pixel (iy, ix) = raw row 2*iy + c, raw cols 2*ix, 2*ix + 1, RGB:
@@ -236,13 +241,13 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
   const int nslots = patch_rows * PW * SL;
   auto dma_fetch = [&](int item, unsigned char* dst) __attribute__((always_inline)) {
     const int n = item / nbands, band = item - n * nbands;
-    const int iy0 = band * kR * S - 1;
+    const int iy0 = band * kR * S - PADK;
     const bool live = item < total;
     for (int j = wv; j * 64 < nslots; j += kNT / 64) {  // one 1-KB DMA per wave per j
       const int q = j * 64 + lane;
       const int pp = q / SL, c = q - pp * SL;
       const int pr = fdiv(pp, fPW), pc = pp - pr * PW;
-      const int iy = iy0 + pr, ix = pc - 1;
+      const int iy = iy0 + pr, ix = pc - PADK;
       const bool ok = live && q < nslots && c < C::CPP && (unsigned)iy < (unsigned)H &&
                       (unsigned)ix < (unsigned)W;
       const int off = ok ? (((n * H + iy) * W + ix) * p.ldx + p.x_coff + c * 8) * 2 : kOOB;
@@ -280,6 +285,30 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
     if constexpr (DMA) dma_fetch(item + gridDim.x, patch + (cur ^ 1) * psz);
     else fetch(item + gridDim.x);
     const unsigned char* pbase = patch + cur * psz;
+    // residual of THIS band, loaded now so its HBM latency hides under the MFMA phase
+    // (a load in the store pass stalled every band: 69 % of wave cycles waiting on the
+    // 16-channel YOLO bottleneck conv, profiles/r2_v2_yolov8n_b384_pmc.md)
+    constexpr int OCH = COUT / 8;
+    // VGPR budget: narrow forms only; the VGPR-prefetch form also holds the next patch
+    constexpr int RPF = RES && CIN <= 32 ? (DMA ? 12 : CIN <= 16 ? 6 : 0) : 0;
+    uint4 rpf[RPF > 0 ? RPF : 1];
+    const bool rpre = RPF > 0 && npix * OCH <= RPF * kNT;
+    if constexpr (RPF > 0) {
+      if (rpre) {
+#pragma unroll
+        for (int i = 0; i < RPF; ++i) {
+          const int q = tid + kNT * i;
+          const int px = q / OCH, c = q - (q / OCH) * OCH;
+          const int yl = fdiv(px, fWo), xc = px - yl * Wo;
+          const int oy = oy0 + yl;
+          rpf[i] = make_uint4(0u, 0u, 0u, 0u);
+          if (q < npix * OCH && oy < Ho) {
+            const long long m = (long long)(n * Ho + oy) * Wo + xc;
+            rpf[i] = *reinterpret_cast<const uint4*>(R + m * p.ldr + p.r_coff + c * 8);
+          }
+        }
+      }
+    }
 
     for (int b = ph < NPH ? ph : nblk; b < nblk; b += NPH) {
       const int j = min(b * 32 + fr, npix - 1);  // clamp: pixels past npix are discarded
@@ -341,8 +370,26 @@ __global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvPara
     if constexpr (!DMA) commit();
 
     // ---- store the band (+ residual after the activation): 16-B channel chunks
-    constexpr int OCH = COUT / 8;
-    for (int q = tid; q < npix * OCH; q += kNT) {
+    if constexpr (RPF > 0) {
+      if (rpre) {
+#pragma unroll
+        for (int i = 0; i < RPF; ++i) {
+          const int q = tid + kNT * i;
+          if (q >= npix * OCH) break;
+          const int px = q / OCH, c = q - (q / OCH) * OCH;
+          const int yl = fdiv(px, fWo), xc = px - yl * Wo;
+          const int oy = oy0 + yl;
+          if (oy >= Ho) continue;
+          const long long m = (long long)(n * Ho + oy) * Wo + xc;
+          bf16x8 o8 = *reinterpret_cast<const bf16x8*>(otile + px * OS + c * 8);
+          const bf16x8 r8 = __builtin_bit_cast(bf16x8, rpf[i]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o8[e] = f2bf((float)o8[e] + (float)r8[e]);
+          *reinterpret_cast<uint4*>(Y + m * p.ldy + p.y_coff + c * 8) = __builtin_bit_cast(uint4, o8);
+        }
+      }
+    }
+    for (int q = RPF > 0 && rpre ? npix * OCH : tid; q < npix * OCH; q += kNT) {
       const int px = q / OCH, c = q - (q / OCH) * OCH;
       const int yl = fdiv(px, fWo), xc = px - yl * Wo;
       const int oy = oy0 + yl;
@@ -382,6 +429,9 @@ struct DirectEntry {
 #define KV_DIRECT_DMA(CI, CO, S, A, R) \
   {CI, CO, S, 3, A, R, conv3x3_direct_kernel<CI, CO, S, 3, A, R, false, true>, false, true}
 #define KV_DIRECT2(CI, CO, S, A, R) KV_DIRECT(CI, CO, S, A, R), KV_DIRECT_DMA(CI, CO, S, A, R)
+#define KV_DIRECT1(CI, CO, A)                                                        \
+  {CI, CO, 1, 1, A, false, conv3x3_direct_kernel<CI, CO, 1, 1, A, false>},           \
+  {CI, CO, 1, 1, A, false, conv3x3_direct_kernel<CI, CO, 1, 1, A, false, false, true>, false, true}
 // the 3x3 shapes of ResNet-50 stage 1 and YOLOv8n's narrow layers (backbone, C2f
 // bottlenecks, PAN downsamplers, Detect 64-channel branches)
 static const DirectEntry kDirect[] = {
@@ -399,6 +449,11 @@ static const DirectEntry kDirect[] = {
     KV_DIRECT2(64, 64, 2, kActSilu, false),   // h16
     KV_DIRECT2(64, 128, 1, kActSilu, false),  // Detect P3 merged branch stem 64 -> 144 =
     KV_DIRECT2(64, 16, 1, kActSilu, false),   //   128 + 16 (Cout split, direct_launch)
+    // 1x1 (KK = 1, pad 0): YOLO C2f cv1 / cv2 at 160^2 and 80^2, the neck's 80^2 C2f, and the
+    // Detect heads' final 1x1 convs (no activation, written into the 144-channel head map)
+    KV_DIRECT1(32, 32, kActSilu), KV_DIRECT1(48, 32, kActSilu), KV_DIRECT1(64, 64, kActSilu),
+    KV_DIRECT1(128, 64, kActSilu), KV_DIRECT1(192, 64, kActSilu), KV_DIRECT1(96, 64, kActSilu),
+    KV_DIRECT1(64, 64, kActNone), KV_DIRECT1(80, 80, kActNone),
     // Detect cls branch 3x3 (c3 = 80), NCB = 3: DMA form only (the VGPR-prefetch form
     // spills with 180 weight VGPRs and fits one output row per band)
     KV_DIRECT_DMA(80, 80, 1, kActSilu, false),
@@ -411,6 +466,7 @@ static const DirectEntry kDirect[] = {
      true},
 };
 #undef KV_DIRECT2
+#undef KV_DIRECT1
 #undef KV_DIRECT_DMA
 #undef KV_DIRECT
 
@@ -425,7 +481,11 @@ int direct_num_tiles() { return 2; }
 // Returns the instantiation index for p (or < 0), and the band geometry it would use.
 static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* rows, int* lds) {
   const int kk = p->KH;
-  if (p->mode != 0 || p->KW != kk || (kk != 2 && kk != 3) || p->pad != 1) return -8;
+  if (p->KW != kk || kk < 1 || kk > 3) return -8;
+  if (kk == 1 ? (p->pad != 0 || p->stride != 1 || p->Ho != p->H || p->Wo != p->W ||
+                 (p->mode != 0 && p->mode != 1))
+              : (p->mode != 0 || p->pad != 1))
+    return -8;
   if (p->stride != 1 && p->stride != 2) return -8;
   if (kk == 2 && (p->stride != 1 || p->Ho != p->H || p->Wo != p->W)) return -8;  // s2d stem
   const int act = p->act & 3;

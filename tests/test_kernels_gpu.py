@@ -121,10 +121,15 @@ def test_tile_count():
 ])
 def test_conv_every_tile(tile, case):
     N, H, W, cin, cout, k, s, p, act, res, lx, xc = case
-    if tile >= DIRECT0:  # none of these shapes is in the direct-conv instantiation table
-        with pytest.raises(RuntimeError):
-            _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
-                       tile=tile)
+    if tile >= DIRECT0:
+        # the direct family takes only its instantiated shapes (a 1x1 64 -> 128 runs as two
+        # Cout slices of the 64 -> 64 form); anything else must be refused, never run wrong
+        try:
+            err, scale = _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx,
+                                    x_coff=xc, tile=tile)
+        except RuntimeError:
+            return
+        assert err <= 0.02 * scale + 0.02, (tile, case, err, scale)
         return
     if tile >= STREAM0 and (k != 1 or s != 1 or not _stream_fits(tile, (cin * k * k + 63) // 64 * 64, res)):
         with pytest.raises(RuntimeError):
@@ -365,6 +370,29 @@ def test_conv_direct3x3(case, dtile):
     N, H, W, cin, cout, s, act, res, lx, xc, ly, yc = case
     a = act | (ops.RES_AFTER_ACT if res and act != ops.ACT_NONE else 0)
     err, scale = _conv_case(N, H, W, cin, cout, 3, s, 1, a, res=res, ldx_extra=lx, x_coff=xc,
+                            ldy_extra=ly, y_coff=yc, tile=DIRECT0 + dtile)
+    assert err <= 0.02 * scale + 0.02, (case, err, scale)
+
+
+@pytest.mark.parametrize("case", [
+    # (N, H, W, cin, cout, act, ldx_extra, x_coff, ldy_extra, y_coff) -- YOLO's 1x1 convs
+    (2, 160, 160, 32, 32, ops.ACT_SILU, 0, 0, 16, 0),    # C2f b2 cv1 into the 48-ch buffer
+    (2, 160, 160, 48, 32, ops.ACT_SILU, 0, 0, 0, 0),     # C2f b2 cv2
+    (2, 80, 80, 64, 64, ops.ACT_SILU, 0, 0, 64, 0),
+    (2, 80, 80, 128, 64, ops.ACT_SILU, 0, 0, 128, 64),
+    (2, 80, 80, 192, 64, ops.ACT_SILU, 0, 0, 32, 32),
+    (2, 80, 80, 96, 64, ops.ACT_SILU, 32, 16, 0, 0),     # input channel slice
+    (2, 80, 80, 64, 64, ops.ACT_NONE, 0, 0, 80, 0),      # Detect box 1x1 into the head map
+    (2, 80, 80, 80, 80, ops.ACT_NONE, 0, 0, 64, 64),     # Detect cls 1x1 (NCB = 3)
+    (3, 13, 11, 32, 32, ops.ACT_SILU, 0, 0, 0, 0),       # pixel-block / band tails
+    (1, 1, 1, 48, 32, ops.ACT_SILU, 0, 0, 0, 0),
+])
+@pytest.mark.parametrize("dtile", [0, 1])
+def test_conv_direct1x1(case, dtile):
+    """v4 direct family in its 1x1 form (KK = 1, pad 0) vs the fp32 reference: channel
+    slices in and out, tails, both patch-fetch forms."""
+    N, H, W, cin, cout, act, lx, xc, ly, yc = case
+    err, scale = _conv_case(N, H, W, cin, cout, 1, 1, 0, act, ldx_extra=lx, x_coff=xc,
                             ldy_extra=ly, y_coff=yc, tile=DIRECT0 + dtile)
     assert err <= 0.02 * scale + 0.02, (case, err, scale)
 
