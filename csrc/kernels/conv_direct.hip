@@ -76,8 +76,14 @@ __host__ __device__ constexpr int direct_patch_alloc(int patch_bytes, bool dma) 
 // Lane-linear DMA slots of 16 B; slot q = (pixel q / SL, chunk q % SL) with SL = PB / 16,
 // the pitch-padding chunk (q % SL == CPP) gets an out-of-range offset (zero fill).
 template <int CIN, int COUT, int S, int KK, int ACT, bool RES, bool U8 = false, bool DMA = false,
-          bool PAIRS = false>
-__global__ __launch_bounds__(kNT, 1) void conv3x3_direct_kernel(const KvConvParams p, int kR,
+          bool PAIRS = false, int OCC = 1>
+// OCC = workgroups per CU the launch plans for (1 or 2); the second launch-bounds argument
+// is HIP's minimum waves per SIMD (512 threads = 2 per SIMD per workgroup).  The narrow
+// (16/32-channel) layers are latency-bound at one workgroup per CU -- one band in flight,
+// 55-67 % of wave cycles waiting (profiles/r2_v5_yolov8n_b256_pmc.md) -- so their OCC = 2
+// forms take shorter bands (LDS <= 80 KB) and <= 128 VGPRs, and two independent band
+// pipelines share every CU.  Only the DMA forms fit 128 VGPRs without spilling.
+__global__ __launch_bounds__(kNT, 2 * OCC) void conv3x3_direct_kernel(const KvConvParams p, int kR,
                                                                 int PW, int patch_rows,
                                                                 FastDiv fPW, FastDiv fWo) {
   static_assert(!U8 || (CIN == 16 && KK == 2 && S == 1), "frames-in form: the 2x2 s2d stem");
@@ -422,6 +428,7 @@ struct DirectEntry {
   bool u8 = false;
   bool dma = false;
   bool pairs = false;  // frames-in with even W: 12-B paired raw-row loads
+  int occ = 1;         // workgroups per CU (launch bounds, LDS budget, grid)
 };
 
 #define KV_DIRECT(CI, CO, S, A, R) {CI, CO, S, 3, A, R, conv3x3_direct_kernel<CI, CO, S, 3, A, R>}
@@ -429,6 +436,10 @@ struct DirectEntry {
 #define KV_DIRECT_DMA(CI, CO, S, A, R) \
   {CI, CO, S, 3, A, R, conv3x3_direct_kernel<CI, CO, S, 3, A, R, false, true>, false, true}
 #define KV_DIRECT2(CI, CO, S, A, R) KV_DIRECT(CI, CO, S, A, R), KV_DIRECT_DMA(CI, CO, S, A, R)
+// two workgroups per CU (direct tiles 2 / 3)
+#define KV_DIRECT_OCC2(CI, CO, S, KK, A, R)                                                       \
+  {CI, CO, S, KK, A, R, conv3x3_direct_kernel<CI, CO, S, KK, A, R, false, true, false, 2>, false, \
+   true, false, 2}
 #define KV_DIRECT1(CI, CO, A)                                                        \
   {CI, CO, 1, 1, A, false, conv3x3_direct_kernel<CI, CO, 1, 1, A, false>},           \
   {CI, CO, 1, 1, A, false, conv3x3_direct_kernel<CI, CO, 1, 1, A, false, false, true>, false, true}
@@ -454,6 +465,10 @@ static const DirectEntry kDirect[] = {
     KV_DIRECT1(32, 32, kActSilu), KV_DIRECT1(48, 32, kActSilu), KV_DIRECT1(64, 64, kActSilu),
     KV_DIRECT1(128, 64, kActSilu), KV_DIRECT1(192, 64, kActSilu), KV_DIRECT1(96, 64, kActSilu),
     KV_DIRECT1(64, 64, kActNone), KV_DIRECT1(80, 80, kActNone),
+    // two-workgroups-per-CU forms of the narrow, latency-bound YOLO layers
+    KV_DIRECT_OCC2(16, 32, 2, 3, kActSilu, false), KV_DIRECT_OCC2(16, 16, 1, 3, kActSilu, false),
+    KV_DIRECT_OCC2(32, 64, 2, 3, kActSilu, false), KV_DIRECT_OCC2(32, 32, 1, 3, kActSilu, false),
+    KV_DIRECT_OCC2(32, 32, 1, 1, kActSilu, false), KV_DIRECT_OCC2(48, 32, 1, 1, kActSilu, false),
     // Detect cls branch 3x3 (c3 = 80), NCB = 3: DMA form only (the VGPR-prefetch form
     // spills with 180 weight VGPRs and fits one output row per band)
     KV_DIRECT_DMA(80, 80, 1, kActSilu, false),
@@ -467,6 +482,7 @@ static const DirectEntry kDirect[] = {
 };
 #undef KV_DIRECT2
 #undef KV_DIRECT1
+#undef KV_DIRECT_OCC2
 #undef KV_DIRECT_DMA
 #undef KV_DIRECT
 
@@ -476,7 +492,8 @@ int direct_max_patch(int cin) { return (cin >= 80 ? 6 : cin >= 64 ? 7 : 10) * kN
 }  // namespace
 
 // tile 0: the VGPR-prefetch form where one exists; tile 1: the DMA form where one exists
-int direct_num_tiles() { return 2; }
+// tile bit 0: DMA patch fetch; bit 1: two workgroups per CU (the OCC = 2 forms)
+int direct_num_tiles() { return 4; }
 
 // Returns the instantiation index for p (or < 0), and the band geometry it would use.
 static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* rows, int* lds) {
@@ -498,7 +515,7 @@ static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* r
       if (e.cin == p->Cin && e.cout == p->Cout && e.stride == p->stride && e.kk == kk &&
           e.act == act && e.res == res && e.u8 == (p->in_u8 != 0) &&
           (!e.u8 || e.pairs == (p->W % 2 == 0)) &&
-          (pass == 1 || e.dma == (tile == 1))) {
+          (pass == 1 || (e.dma == ((tile & 1) != 0) && e.occ == 1 + ((tile >> 1) & 1)))) {
         idx = i;
         break;
       }
@@ -529,7 +546,8 @@ static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* r
   for (; r >= 1; --r) {
     const int prows = (r - 1) * S + kk;
     const int patch = prows * *PW * pb;
-    if ((dma || patch <= direct_max_patch(p->Cin)) && lds_of(prows, r) <= kLds) break;
+    if ((dma || patch <= direct_max_patch(p->Cin)) && lds_of(prows, r) <= kLds / kDirect[idx].occ)
+      break;
   }
   if (r < 1) return -11;
   if (r > p->Ho) r = p->Ho;
@@ -548,7 +566,8 @@ static int direct_launch_one(const KvConvParams* p, int tile, hipStream_t stream
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  const unsigned g = (unsigned)(items < ncu ? items : ncu);  // persistent: one per CU
+  const long long slots = (long long)ncu * kDirect[idx].occ;  // persistent: occ per CU
+  const unsigned g = (unsigned)(items < slots ? items : slots);
   const DirectFn fn = kDirect[idx].fn;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)

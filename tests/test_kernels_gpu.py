@@ -82,7 +82,7 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale + 0.02
 
 
-N_TILES = 56  # v1 register-staged (0-5) + v2 LDS-DMA (6-31) + v3 streaming (32-53) + v4 direct (54-55)
+N_TILES = 58  # v1 register-staged (0-5) + v2 LDS-DMA (6-31) + v3 streaming (32-53) + v4 direct (54-57)
 STREAM0 = 32  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
 DIRECT0 = 54  # v4 direct 3x3 (conv_direct.hip): its instantiation table only
 # v2 8-wave (512-thread) tiles 24-28 (256x256 x2, 256x128, 128x256, 256x128 D3) and the
@@ -362,11 +362,12 @@ def test_conv_poisoned_canary(tile, k):
     (3, 13, 11, 80, 80, 1, ops.ACT_SILU, False, 0, 0, 8, 8),     # pixel-block tails, y slice
     (2, 40, 40, 80, 80, 1, ops.ACT_SILU, False, 64, 64, 0, 0),   # Detect P4 cls
 ])
-@pytest.mark.parametrize("dtile", [0, 1])
+@pytest.mark.parametrize("dtile", [0, 1, 3])
 def test_conv_direct3x3(case, dtile):
     """v4 persistent direct 3x3 conv (csrc/kernels/conv_direct.hip) vs the fp32 reference:
     both strides, odd sizes, channel slices in/out, residual after the activation.
-    dtile 0: VGPR-prefetched band patch; 1: the DMA (buffer_load ... lds) double buffer."""
+    dtile 0: VGPR-prefetched band patch; 1: the DMA (buffer_load ... lds) double buffer;
+    3: the DMA form at two workgroups per CU (narrow shapes; others fall back to 0/1)."""
     N, H, W, cin, cout, s, act, res, lx, xc, ly, yc = case
     a = act | (ops.RES_AFTER_ACT if res and act != ops.ACT_NONE else 0)
     err, scale = _conv_case(N, H, W, cin, cout, 3, s, 1, a, res=res, ldx_extra=lx, x_coff=xc,
@@ -387,7 +388,7 @@ def test_conv_direct3x3(case, dtile):
     (3, 13, 11, 32, 32, ops.ACT_SILU, 0, 0, 0, 0),       # pixel-block / band tails
     (1, 1, 1, 48, 32, ops.ACT_SILU, 0, 0, 0, 0),
 ])
-@pytest.mark.parametrize("dtile", [0, 1])
+@pytest.mark.parametrize("dtile", [0, 1, 3])
 def test_conv_direct1x1(case, dtile):
     """v4 direct family in its 1x1 form (KK = 1, pad 0) vs the fp32 reference: channel
     slices in and out, tails, both patch-fetch forms."""
