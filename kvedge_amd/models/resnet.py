@@ -159,6 +159,29 @@ class DeployedBottleneck:
         return ops.conv_tail(y, self.c3.w, self.c3.b, self.c3.spec.act, c1.w, c1.b, res=x,
                              out=out, z=z)
 
+    def can_block(self, nxt: "DeployedBottleneck") -> bool:
+        """conv2 (3x3, 64 -> 64, stride 1) + the fused tail as ONE kernel (ops.conv_block):
+        the 64-channel conv2 output never reaches HBM.  Stage 1 of ResNet-50 (the dual
+        form with a stride-1 64-channel downsample source, or the residual form)."""
+        c2 = self.c2.spec
+        if not (c2.kh == 3 and c2.stride == 1 and c2.pad == 1 and c2.cin == 64 and
+                c2.cout == 64 and c2.act == ACT_RELU and self.can_tail(nxt)):
+            return False
+        if self.dual is not None:
+            return (self.dual.stride2 == 1 and self.dual.k1 == 64 and
+                    self.dual.w.shape[1] == 128 and nxt.c1.spec.cout == 64)
+        return True
+
+    def call_block(self, x, nxt: "DeployedBottleneck", t1=None):
+        """-> (this block's output y, the next block's conv1 output z) with conv2, conv3
+        (+ residual or fused downsample) and the next conv1 in one kernel."""
+        t = self.c1(x) if t1 is None else t1
+        c1 = nxt.c1
+        if self.dual is not None:
+            return ops.conv_block(t, self.c2.w, self.c2.b, self.dual.w, self.dual.b, c1.w, c1.b,
+                                  x2=x)
+        return ops.conv_block(t, self.c2.w, self.c2.b, self.c3.w, self.c3.b, c1.w, c1.b, res=x)
+
     def out_shape(self, x_shape):
         N, H, W, _ = x_shape
         Ho, Wo = self.c2.spec.out_hw(H, W)
@@ -218,6 +241,9 @@ class KvResNet50:
     # conv3 (+ fused downsample) and the NEXT block's conv1 as one kernel wherever the
     # tail tile fits (layer1 -> layer2 boundary included): y is never re-read from HBM
     fuse_tail: bool = True
+    # stage 1: conv2 (3x3) + the fused tail in ONE kernel (conv_block.hip): the 64-channel
+    # conv2 output is never written to HBM
+    fuse_block: bool = False
 
     def stem_and_pool(self, x: torch.Tensor, frames_in: bool = False) -> torch.Tensor:
         if frames_in:
@@ -263,7 +289,10 @@ class KvResNet50:
             rest = self.blocks
         for i, b in enumerate(rest):
             nxt = rest[i + 1] if i + 1 < len(rest) else None
-            if self.fuse_tail and x.is_cuda and nxt is not None and b.can_tail(nxt):
+            if (self.fuse_block and x.is_cuda and nxt is not None and b.can_block(nxt) and
+                    ops.conv_block_fits(x)):
+                x, t1 = b.call_block(x, nxt, t1=t1)
+            elif self.fuse_tail and x.is_cuda and nxt is not None and b.can_tail(nxt):
                 x, t1 = b.call_tail(x, nxt, t1=t1)
             else:
                 x, t1 = b(x, t1=t1), None

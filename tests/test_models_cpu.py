@@ -124,3 +124,23 @@ def test_yolo_frames_in_stem_matches_preprocess_path():
         plain = kv.b0(kv.preprocess(fr)).float()
     assert fused.shape == plain.shape == (2, 32, 48, 16)
     assert (fused - plain).abs().max().item() <= 0.02 * plain.abs().max().item() + 0.02
+
+
+def test_resnet_stage1_block_fusion_plumbing():
+    """The three stage-1 bottlenecks take the fused conv2 + tail kernel (ops.conv_block) on
+    the GPU; on CPU its reference composition equals the two-kernel path bit for bit."""
+    import torch
+
+    from kvedge_amd.models.resnet import KvResNet50, init_resnet50
+
+    kv = KvResNet50(init_resnet50(0, calibrate=False), "cpu")
+    fused = [i for i, b in enumerate(kv.blocks[:-1]) if b.can_block(kv.blocks[i + 1])]
+    assert fused == [0, 1, 2]
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(1, 10, 9, 64, generator=g).relu().to(torch.bfloat16)
+    for i in fused:
+        b, nxt = kv.blocks[i], kv.blocks[i + 1]
+        y_f, z_f = b.call_block(x, nxt)
+        y_t, z_t = b.call_tail(x, nxt)
+        assert torch.equal(y_f, y_t) and torch.equal(z_f, z_t)
+        x = y_f
