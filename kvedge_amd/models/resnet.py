@@ -242,7 +242,9 @@ class KvResNet50:
     # tail tile fits (layer1 -> layer2 boundary included): y is never re-read from HBM
     fuse_tail: bool = True
     # stage 1: conv2 (3x3) + the fused tail in ONE kernel (conv_block.hip): the 64-channel
-    # conv2 output is never written to HBM
+    # conv2 output is never written to HBM.  Opt-in: it moves 17-22 % fewer bytes but, with
+    # one workgroup per CU, cannot overlap its 3x3 phase with its memory phase, and measures
+    # level with or slower than direct + tail (docs/kernels.md, profiles/r2_v8_block_probe.md)
     fuse_block: bool = False
 
     def stem_and_pool(self, x: torch.Tensor, frames_in: bool = False) -> torch.Tensor:
