@@ -42,6 +42,34 @@ __host__ __device__ __forceinline__ FastDiv make_fastdiv(int d) {
 __device__ __forceinline__ int fdiv(int n, FastDiv f) { return (int)__umulhi((unsigned)n, f.m); }
 __device__ __forceinline__ int fmod_(int n, int q, FastDiv f) { return n - q * f.d; }
 
+// 16-B-per-lane global -> LDS DMA (buffer_load_dwordx4 ... lds) that the compiler does NOT
+// see as an LDS write.  With the builtin (__builtin_amdgcn_raw_ptr_buffer_load_lds) hipcc
+// assumes the pending DMA may alias every later LDS read and puts an s_waitcnt vmcnt(0) in
+// front of them: a next-tile prefetch into a SECOND buffer then drains before the current
+// tile's fragment reads, i.e. the double buffer does nothing (seen in conv_direct.hip's
+// pixel-block loop).  Callers of this form own the synchronisation: an explicit
+// s_waitcnt vmcnt(...) + barrier before the destination buffer is read.  An out-of-range
+// voff (>= the descriptor's byte count) zero-fills the 16 B, as with the builtin.
+typedef int kv_i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ kv_i32x4 kv_rsrc4(const void* base, int bytes) {
+  const unsigned long long a = (unsigned long long)base;
+  kv_i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((unsigned)(a >> 32) & 0xffffu));  // stride 0
+  r[2] = __builtin_amdgcn_readfirstlane(bytes);                                  // num_records
+  r[3] = 0x00020000;                                                             // as make_buffer_rsrc
+  return r;
+}
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is set here and never assumed preserved
+__device__ __forceinline__ void kv_lds_dma16(kv_i32x4 rs, void* lds, int voff) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(
+      (unsigned)(unsigned long long)(__attribute__((address_space(3))) void*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :: "s"(m0), "v"(voff), "s"(rs) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 __device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
 __device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }  // v_cvt_pk_bf16_f32, NaN-safe
 

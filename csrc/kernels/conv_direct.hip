@@ -76,14 +76,16 @@ __host__ __device__ constexpr int direct_patch_alloc(int patch_bytes, bool dma) 
 // Lane-linear DMA slots of 16 B; slot q = (pixel q / SL, chunk q % SL) with SL = PB / 16,
 // the pitch-padding chunk (q % SL == CPP) gets an out-of-range offset (zero fill).
 template <int CIN, int COUT, int S, int KK, int ACT, bool RES, bool U8 = false, bool DMA = false,
-          bool PAIRS = false, int OCC = 1>
+          bool PAIRS = false, int OCC = 1, int NT = kNT>
 // OCC = workgroups per CU the launch plans for (1 or 2); the second launch-bounds argument
 // is HIP's minimum waves per SIMD (512 threads = 2 per SIMD per workgroup).  The narrow
 // (16/32-channel) layers are latency-bound at one workgroup per CU -- one band in flight,
 // 55-67 % of wave cycles waiting (profiles/r2_v5_yolov8n_b256_pmc.md) -- so their OCC = 2
 // forms take shorter bands (LDS <= 80 KB) and <= 128 VGPRs, and two independent band
 // pipelines share every CU.  Only the DMA forms fit 128 VGPRs without spilling.
-__global__ __launch_bounds__(kNT, 2 * OCC) void conv3x3_direct_kernel(const KvConvParams p, int kR,
+// NT = 256 (4 waves, one workgroup per CU, one wave per SIMD): the whole 512-entry register
+// file per lane, for weight blocks that do not fit 256 (CIN = 128: 288 weight VGPRs)
+__global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_kernel(const KvConvParams p, int kR,
                                                                 int PW, int patch_rows,
                                                                 FastDiv fPW, FastDiv fWo) {
   static_assert(!U8 || (CIN == 16 && KK == 2 && S == 1), "frames-in form: the 2x2 s2d stem");
@@ -95,10 +97,10 @@ __global__ __launch_bounds__(kNT, 2 * OCC) void conv3x3_direct_kernel(const KvCo
   constexpr int PADK = KK == 1 ? 0 : 1;
   using C = DirectCfg<CIN, KK>;
   constexpr int NCB = (COUT + 31) / 32;  // 32-channel blocks
-  static_assert(NCB >= 1 && NCB <= 4, "channel blocks");
+  static_assert(NCB >= 1 && NCB <= 4 && NCB <= NT / 64, "channel blocks");
   // pixel-block phases; with NCB = 3 (YOLO's 80-channel Detect cls branch) waves 6 and 7
   // sit out the MFMA phase and only help with the patch fetch and the store pass
-  constexpr int NPH = 8 / NCB;
+  constexpr int NPH = (NT / 64) / NCB;
   constexpr int OS = COUT + 8;           // output tile pixel stride (elements)
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   static_assert(!(DMA && U8), "DMA patch fetch: bf16 NHWC inputs only");
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(kNT, 2 * OCC) void conv3x3_direct_kernel(const KvCo
         const int nitems = patch_rows * 2 * NPR;
 #pragma unroll
         for (int i = 0; i < C::PRE / 2; ++i) {
-          const int u = tid + kNT * i;
+          const int u = tid + NT * i;
           const int rc = fdiv(u, fNPR), k = u - rc * NPR;
           const int iy = iy0 + (rc >> 1), ix = 2 * k;
           const bool rowok = live && u < nitems && (unsigned)iy < (unsigned)H;
@@ -184,7 +186,7 @@ __global__ __launch_bounds__(kNT, 2 * OCC) void conv3x3_direct_kernel(const KvCo
     }
 #pragma unroll
     for (int i = 0; i < C::PRE; ++i) {
-      const int q = tid + kNT * i;
+      const int q = tid + NT * i;
       int pp, c;
       chunk_of(q, pp, c);
       const int pr = fdiv(pp, fPW), pc = pp - pr * PW;
@@ -214,7 +216,7 @@ __global__ __launch_bounds__(kNT, 2 * OCC) void conv3x3_direct_kernel(const KvCo
         const uint4 z = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
         for (int i = 0; i < C::PRE / 2; ++i) {
-          const int u = tid + kNT * i;
+          const int u = tid + NT * i;
           if (u >= nitems) continue;
           const int rc = fdiv(u, fNPR), k = u - rc * NPR;
           const int pp = (rc >> 1) * PW + 2 * k + 1;
@@ -236,7 +238,7 @@ __global__ __launch_bounds__(kNT, 2 * OCC) void conv3x3_direct_kernel(const KvCo
     }
 #pragma unroll
     for (int i = 0; i < C::PRE; ++i) {
-      const int q = tid + kNT * i;
+      const int q = tid + NT * i;
       int pp, c;
       chunk_of(q, pp, c);
       if (q < nchunks) *reinterpret_cast<uint4*>(patch + pp * C::PB + c * 16) = pre[i];
@@ -245,11 +247,12 @@ __global__ __launch_bounds__(kNT, 2 * OCC) void conv3x3_direct_kernel(const KvCo
 
   constexpr int SL = C::PB / 16;  // 16-B slots per patch pixel (CPP data + 1 padding)
   const int nslots = patch_rows * PW * SL;
+  const kv_i32x4 rx4 = kv_rsrc4(p.x, U8 ? 0 : p.N * H * W * p.ldx * 2);
   auto dma_fetch = [&](int item, unsigned char* dst) __attribute__((always_inline)) {
     const int n = item / nbands, band = item - n * nbands;
     const int iy0 = band * kR * S - PADK;
     const bool live = item < total;
-    for (int j = wv; j * 64 < nslots; j += kNT / 64) {  // one 1-KB DMA per wave per j
+    for (int j = wv; j * 64 < nslots; j += NT / 64) {  // one 1-KB DMA per wave per j
       const int q = j * 64 + lane;
       const int pp = q / SL, c = q - pp * SL;
       const int pr = fdiv(pp, fPW), pc = pp - pr * PW;
@@ -257,8 +260,9 @@ __global__ __launch_bounds__(kNT, 2 * OCC) void conv3x3_direct_kernel(const KvCo
       const bool ok = live && q < nslots && c < C::CPP && (unsigned)iy < (unsigned)H &&
                       (unsigned)ix < (unsigned)W;
       const int off = ok ? (((n * H + iy) * W + ix) * p.ldx + p.x_coff + c * 8) * 2 : kOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rx, (__attribute__((address_space(3))) void*)(dst + j * 1024), 16, off, 0, 0, 0);
+      // opaque to the compiler (common.h): the builtin made hipcc drain this prefetch with a
+      // vmcnt(0) in front of the current band's fragment reads
+      kv_lds_dma16(rx4, dst + j * 1024, off);
     }
   };
 
@@ -271,7 +275,7 @@ __global__ __launch_bounds__(kNT, 2 * OCC) void conv3x3_direct_kernel(const KvCo
   int cur = 0;
   if constexpr (PAIRS) {
     // patch column 0 = left padding of every patch row, both parities: zero
-      for (int q = tid; q < patch_rows * 2; q += kNT)
+      for (int q = tid; q < patch_rows * 2; q += NT)
         *reinterpret_cast<uint4*>(patch + (q >> 1) * PW * C::PB + (q & 1) * 16) =
             make_uint4(0u, 0u, 0u, 0u);
   }
@@ -298,12 +302,12 @@ __global__ __launch_bounds__(kNT, 2 * OCC) void conv3x3_direct_kernel(const KvCo
     // VGPR budget: narrow forms only; the VGPR-prefetch form also holds the next patch
     constexpr int RPF = RES && CIN <= 32 ? (DMA ? 12 : CIN <= 16 ? 6 : 0) : 0;
     uint4 rpf[RPF > 0 ? RPF : 1];
-    const bool rpre = RPF > 0 && npix * OCH <= RPF * kNT;
+    const bool rpre = RPF > 0 && npix * OCH <= RPF * NT;
     if constexpr (RPF > 0) {
       if (rpre) {
 #pragma unroll
         for (int i = 0; i < RPF; ++i) {
-          const int q = tid + kNT * i;
+          const int q = tid + NT * i;
           const int px = q / OCH, c = q - (q / OCH) * OCH;
           const int yl = fdiv(px, fWo), xc = px - yl * Wo;
           const int oy = oy0 + yl;
@@ -335,7 +339,7 @@ __global__ __launch_bounds__(kNT, 2 * OCC) void conv3x3_direct_kernel(const KvCo
       // fragment ring: the read for step kk + PD is issued before the MFMA of step kk, so
       // PD LDS reads are in flight behind the MFMA pipe (PD = 1 left the MFMAs waiting on
       // ds_read latency: 29 % MFMA busy in PMC)
-      constexpr int PD = KPD;
+      constexpr int PD = NT == kNT ? KPD : 6;  // one wave per SIMD: a deeper read ring
       bf16x8 af[PD + 1];
       auto load = [&](int buf, int kk) __attribute__((always_inline)) {
         const int tap = kk / C::KPT, s4 = kk - (kk / C::KPT) * C::KPT;
@@ -380,7 +384,7 @@ __global__ __launch_bounds__(kNT, 2 * OCC) void conv3x3_direct_kernel(const KvCo
       if (rpre) {
 #pragma unroll
         for (int i = 0; i < RPF; ++i) {
-          const int q = tid + kNT * i;
+          const int q = tid + NT * i;
           if (q >= npix * OCH) break;
           const int px = q / OCH, c = q - (q / OCH) * OCH;
           const int yl = fdiv(px, fWo), xc = px - yl * Wo;
@@ -395,7 +399,7 @@ __global__ __launch_bounds__(kNT, 2 * OCC) void conv3x3_direct_kernel(const KvCo
         }
       }
     }
-    for (int q = RPF > 0 && rpre ? npix * OCH : tid; q < npix * OCH; q += kNT) {
+    for (int q = RPF > 0 && rpre ? npix * OCH : tid; q < npix * OCH; q += NT) {
       const int px = q / OCH, c = q - (q / OCH) * OCH;
       const int yl = fdiv(px, fWo), xc = px - yl * Wo;
       const int oy = oy0 + yl;
@@ -429,6 +433,7 @@ struct DirectEntry {
   bool dma = false;
   bool pairs = false;  // frames-in with even W: 12-B paired raw-row loads
   int occ = 1;         // workgroups per CU (launch bounds, LDS budget, grid)
+  int nt = kNT;        // threads per workgroup
 };
 
 #define KV_DIRECT(CI, CO, S, A, R) {CI, CO, S, 3, A, R, conv3x3_direct_kernel<CI, CO, S, 3, A, R>}
@@ -469,6 +474,12 @@ static const DirectEntry kDirect[] = {
     KV_DIRECT_OCC2(16, 32, 2, 3, kActSilu, false), KV_DIRECT_OCC2(16, 16, 1, 3, kActSilu, false),
     KV_DIRECT_OCC2(32, 64, 2, 3, kActSilu, false), KV_DIRECT_OCC2(32, 32, 1, 3, kActSilu, false),
     KV_DIRECT_OCC2(32, 32, 1, 1, kActSilu, false), KV_DIRECT_OCC2(48, 32, 1, 1, kActSilu, false),
+    // ResNet-50 stage-2 conv2 (128 -> 128 @28^2, stride 1): 4 waves, each holding one 32-channel
+    // block's 288 weight VGPRs, one workgroup per CU; the band patch is staged once per band
+    // instead of once per tap (the implicit GEMM re-reads every input pixel 9x through L2)
+    {128, 128, 1, 3, kActRelu, false,
+     conv3x3_direct_kernel<128, 128, 1, 3, kActRelu, false, false, true, false, 1, 256>, false, true,
+     false, 1, 256},
     // Detect cls branch 3x3 (c3 = 80), NCB = 3: DMA form only (the VGPR-prefetch form
     // spills with 180 weight VGPRs and fits one output row per band)
     KV_DIRECT_DMA(80, 80, 1, kActSilu, false),
@@ -572,7 +583,7 @@ static int direct_launch_one(const KvConvParams* p, int tile, hipStream_t stream
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
     return -7;
-  hipLaunchKernelGGL(fn, dim3(g), dim3(kNT), (unsigned)lds, stream, *p, kR, PW, rows,
+  hipLaunchKernelGGL(fn, dim3(g), dim3(kDirect[idx].nt), (unsigned)lds, stream, *p, kR, PW, rows,
                      make_fastdiv(PW), make_fastdiv(p->Wo));
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }

@@ -361,6 +361,8 @@ def test_conv_poisoned_canary(tile, k):
     (2, 80, 80, 80, 80, 1, ops.ACT_SILU, False, 64, 64, 0, 0),   # Detect P3 cls 3x3 (NCB = 3)
     (3, 13, 11, 80, 80, 1, ops.ACT_SILU, False, 0, 0, 8, 8),     # pixel-block tails, y slice
     (2, 40, 40, 80, 80, 1, ops.ACT_SILU, False, 64, 64, 0, 0),   # Detect P4 cls
+    (3, 28, 28, 128, 128, 1, ops.ACT_RELU, False, 0, 0, 0, 0),   # ResNet stage-2 conv2 (4 waves)
+    (2, 13, 11, 128, 128, 1, ops.ACT_RELU, False, 0, 0, 8, 8),   # band / pixel-block tails
 ])
 @pytest.mark.parametrize("dtile", [0, 1, 3])
 def test_conv_direct3x3(case, dtile):
