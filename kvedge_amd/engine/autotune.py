@@ -33,6 +33,28 @@ def _time(fn: Callable[[int], object], tile: int, iters: int) -> float:
     return ts[len(ts) // 2]
 
 
+def _time_interleaved(cands, rounds: int):
+    """Median ms per (fn, tile) with the candidates timed round-robin (A B C A B C ...):
+    a clock or thermal drift during the measurement then biases every candidate alike,
+    where timing each candidate's launches back to back let a drift decide near-ties."""
+    for fn, t in cands:
+        fn(t)  # warm: code object loaded, first-launch costs out of the way
+    evs = [[] for _ in cands]
+    for _ in range(rounds):
+        for i, (fn, t) in enumerate(cands):
+            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            st.record()
+            fn(t)
+            en.record()
+            evs[i].append((st, en))
+    torch.cuda.synchronize()
+    out = []
+    for e in evs:
+        ts = sorted(a.elapsed_time(b) for a, b in e)
+        out.append(ts[len(ts) // 2])
+    return out
+
+
 def _fleet_mean(rows):
     """Mean over data-parallel ranks of a [keys][tiles] timing matrix (identity when not
     distributed).  +inf (tile invalid for the layer) is the same on every rank."""
@@ -68,7 +90,7 @@ def _near_ties(rows, tol: float):
 
 def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
              cache_path: str = None, verbose: bool = False, refine_iters: int = None,
-             refine_tol: float = 0.05) -> Dict:
+             refine_tol: float = 0.15) -> Dict:
     """Tune every conv of ``model`` for ``example_input``'s shape. Returns {key: (tile, us)}."""
     if not example_input.is_cuda:
         return {}
@@ -103,12 +125,18 @@ def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
     fleet = _fleet_mean([v[2] for v in todo.values()])
     # phase 3: near-ties (within ``refine_tol`` of the best, by the fleet mean -- so every
     # rank re-times the same (key, tile) list in the same order) are re-timed with
-    # ``refine_iters`` launches; a 5-launch median alone flipped picks between runs
+    # ``refine_iters`` launches each, the candidates of one layer interleaved round-robin; a
+    # 5-launch median alone flipped picks between runs (a stage-2 expand layer took a tile
+    # 15 % slower in the graph than the runner-up on one box)
     if refine_iters > iters:
         fns = [(ks, fn) for ks, (_, fn, _) in todo.items()]
         cand = [(fns[i][0], fns[i][1], t) for i, t in _near_ties(fleet, refine_tol)]
         if cand:
-            re = _fleet_mean([[_time(fn, t, refine_iters) * 1e3 for ks, fn, t in cand]])[0]
+            times = []
+            for ks in dict.fromkeys(c[0] for c in cand):  # per layer, in first-seen order
+                grp = [(fn, t) for k, fn, t in cand if k == ks]
+                times += [x * 1e3 for x in _time_interleaved(grp, refine_iters)]
+            re = _fleet_mean([times])[0]
             idx = {ks: i for i, ks in enumerate(todo)}
             for (ks, _, t), us in zip(cand, re):
                 row = fleet[idx[ks]]
