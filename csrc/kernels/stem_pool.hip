@@ -19,8 +19,10 @@
 //    seeded with the folded-BN bias;
 //  * ReLU, bf16, into an LDS stem tile; then the 3x3/2 pool reads the tile and writes
 //    the pooled [RB, W/2, 64] band with 16-B stores.
-// 5 stem rows per 4 pooled-input rows is a 25 % recompute of the conv, paid to never
-// write or re-read the 112x112x64 intermediate.
+// A band's pool windows touch 5 stem rows, the first shared with the previous band.  Each
+// workgroup walks a contiguous range of bands and keeps the stem tile as a 5-row ring, so
+// the shared row is computed once (only the first band of a range recomputes it): the
+// 112x112x64 intermediate is never written to HBM, and no conv row is computed twice.
 //
 // VALU diet (PMC of the previous version, profiles/r1_v7_stem_pmc.md: 17 VALU per MFMA,
 // i.e. VALU-issue-bound at ~2x the MFMA time):
@@ -185,22 +187,33 @@ __global__ __launch_bounds__(NT, 1) void stem_pool_kernel(
   };
 
   const FastDiv fW = make_fastdiv(W);  // once per thread; j / W per row block below
-  int item = blockIdx.x;
+  // each workgroup walks a CONTIGUOUS range of bands, so consecutive bands of one image
+  // run back to back here: a band's first stem row (y0) is the previous band's last one,
+  // still in the stem tile, and only 4 of the 5 rows are computed (the tile's rows are a
+  // ring: stem row y lives in slot (y + kSR) % kSR).  Band 0's row -1 is padding the pool
+  // skips, so it is never computed either.  20 % fewer MFMAs than recomputing the shared row;
+  // measured time barely moves (376-407 -> 381 us at batch 640): the kernel is bound by its
+  // fetch / commit / pool phases, not the MFMAs (profiles/r2_v12_stem_ring.md)
+  const int per = (total + gridDim.x - 1) / gridDim.x;
+  const int item0 = blockIdx.x * per, item1 = min(item0 + per, total);
+  int item = item0;
   fetch(item);
   commit();
   __syncthreads();
-  for (; item < total; item += gridDim.x) {
+  for (; item < item1; ++item) {
     const int n = item / nbands, band = item - n * nbands;
     const int P0 = band * kRB;  // first pooled row
     const int y0 = 2 * P0 - 1;  // first stem row (may be -1)
-    fetch(item + gridDim.x);    // next band's patch: in flight during this band's MFMAs
+    fetch(item + 1 < item1 ? item + 1 : total);  // next band's patch, during these MFMAs
+    const int skip = (band == 0 || item > item0) ? 1 : 0;  // row y0 padding or already in the tile
 
     // ---- stem rows of the band: 32-pixel row blocks round-robin over the kNW waves
-    const int npix = kSR * W;
+    const int npix = (kSR - skip) * W;
     const int nrb = (npix + 31) / 32;
     for (int rb = wv; rb < nrb; rb += kNW) {
-      const int j = min(rb * 32 + fr, npix - 1);  // clamp: rows past npix are discarded
+      const int j = min(rb * 32 + fr, npix - 1) + skip * W;  // clamp: rows past npix discarded
       const int yl = fdiv(j, fW), xc = j - yl * W;
+      const int slot = (y0 + yl + kSR) % kSR;
       const unsigned char* pa = patch + patch_off(yl * kPW + xc, fh);
       floatx16 acc[2];
 #pragma unroll
@@ -231,8 +244,7 @@ __global__ __launch_bounds__(NT, 1) void stem_pool_kernel(
       }
       // ReLU -> bf16 stem tile.  Stem rows outside the image (above the first band, below
       // an odd-H image) are written but never pooled: the pool skips them as padding.
-      const int jr = rb * 32 + fr;
-      if (jr < npix) {
+      if (rb * 32 + fr < npix) {
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
@@ -242,7 +254,7 @@ __global__ __launch_bounds__(NT, 1) void stem_pool_kernel(
             o[1] = f2bf(fmaxf(acc[cb][4 * g + 1], 0.f));
             o[2] = f2bf(fmaxf(acc[cb][4 * g + 2], 0.f));
             o[3] = f2bf(fmaxf(acc[cb][4 * g + 3], 0.f));
-            *reinterpret_cast<bf16x4*>(tile + jr * kTS + cb * 32 + g * 8 + fh * 4) = o;
+            *reinterpret_cast<bf16x4*>(tile + (slot * W + xc) * kTS + cb * 32 + g * 8 + fh * 4) = o;
           }
       }
     }
@@ -268,7 +280,8 @@ __global__ __launch_bounds__(NT, 1) void stem_pool_kernel(
           for (int dx = -1; dx <= 1; ++dx) {
             const int xs = 2 * px + dx;
             if ((unsigned)xs >= (unsigned)W) continue;
-            const uint4 v = *reinterpret_cast<const uint4*>(tile + (yl * W + xs) * kTS + c8 * 8);
+            const int slot = (y0 + yl + kSR) % kSR;
+            const uint4 v = *reinterpret_cast<const uint4*>(tile + (slot * W + xs) * kTS + c8 * 8);
             m.x = pk_max_u16(m.x, v.x);
             m.y = pk_max_u16(m.y, v.y);
             m.z = pk_max_u16(m.z, v.z);

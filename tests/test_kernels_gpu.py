@@ -425,9 +425,13 @@ def test_conv_direct3x3_rejects():
         _conv_case(1, 8, 8, 48, 48, 3, 1, 1, ops.ACT_RELU, tile=DIRECT0)
 
 
-@pytest.mark.parametrize("shape", [(2, 112, 112), (3, 17, 13), (1, 8, 30)])
+@pytest.mark.parametrize("shape", [(2, 112, 112), (3, 17, 13), (1, 8, 30), (20, 112, 112),
+                                   (120, 17, 13), (300, 6, 8)])
 def test_stem_pool_fused(shape):
-    """Fused s2d stem conv + ReLU + 3x3/2 max pool == reference conv then reference pool."""
+    """Fused s2d stem conv + ReLU + 3x3/2 max pool == reference conv then reference pool.
+    More bands than CUs (the last three shapes) make every workgroup walk several bands,
+    reusing the shared stem row from its 5-row tile ring, with ranges that cross image
+    boundaries (odd H: a last band whose lower stem rows are outside the image)."""
     from kvedge_amd.models.layers import DeployedConv
     import torch.nn as nn
     N, H, W = shape

@@ -124,12 +124,14 @@ def test_yolov8n_fused_stem_parity(yolo):
         assert cos > 0.999, float(cos)
 
 
-@pytest.mark.parametrize("hw", [(224, 224), (64, 96), (36, 20)])
-def test_stem_pool_frames_kernel(resnet, hw):
+@pytest.mark.parametrize("hw,n", [((224, 224), 5), ((64, 96), 5), ((36, 20), 5), ((224, 224), 40),
+                                  ((36, 20), 160)])
+def test_stem_pool_frames_kernel(resnet, hw, n):
     """Frames-in ResNet stem + pool (preprocess fused into the fetch) vs the CPU reference
-    preprocess -> s2d stem -> pool; borders (padding must be 0, not -mean/std) included."""
+    preprocess -> s2d stem -> pool; borders (padding must be 0, not -mean/std) included.
+    n = 40 / 160: more bands than CUs, so workgroups walk band ranges (shared stem row)."""
     _, kv, kv_cpu = resnet
-    fr = torch.randint(0, 256, (5, hw[0], hw[1], 3), dtype=torch.uint8,
+    fr = torch.randint(0, 256, (n, hw[0], hw[1], 3), dtype=torch.uint8,
                        generator=torch.Generator().manual_seed(11))
     s = kv_cpu.stem
     ref = ops.stem_pool_frames(fr, s.spec, s.w, s.b).float()
