@@ -40,8 +40,8 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("KVEDGE_BENCH_BATCH", 0)),
-                    help="per-GPU batch (0 = model default: ResNet-50 640, YOLOv8n 384 -- the "
-                         "throughput knees of the batch sweep, profiles/r1_v13_batch_sweep.jsonl)")
+                    help="per-GPU batch (0 = kvedge_amd.engine.BENCH_BATCH: ResNet-50 1280, "
+                         "YOLOv8n 384, from the batch sweeps in profiles/)")
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "yolov8n"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-autotune", action="store_true")
@@ -66,7 +66,7 @@ def main(argv=None):
 
     import torch
     from kvedge_amd import ops, parallel
-    from kvedge_amd.engine import InferenceEngine
+    from kvedge_amd.engine import BENCH_BATCH, InferenceEngine
 
     if a.gpus < 1:
         print("--gpus must be >= 1", file=sys.stderr)
@@ -95,7 +95,7 @@ def main(argv=None):
             torch.cuda.synchronize()
 
     if a.batch <= 0:
-        a.batch = (640 if a.model == "resnet50" else 384) if on_gpu else 1
+        a.batch = BENCH_BATCH[a.model] if on_gpu else 1
     t_build = time.perf_counter()
     if a.model == "resnet50":
         from kvedge_amd.models.resnet import KvResNet50

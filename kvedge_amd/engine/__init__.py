@@ -19,6 +19,14 @@ import torch
 
 from .. import ops
 
+# Per-GPU batch bench.py times by default (and tests/test_bench_config_gpu.py checks).
+# ResNet-50: 1280, from the same-box batch sweeps (profiles/r2_v8_batch_sweep.jsonl):
+# 79.6-80.3k img/s at 1280 against 78.1-78.2k at 640, the largest batch whose activations
+# still fit one launch per conv (2 GiB per operand; ~1330 images).  YOLOv8n: 384 (sweep knee,
+# profiles/r1_v13_batch_sweep.jsonl).  Edge-module serving uses its own, latency-bound batch
+# (module twin `batch`, default 64).
+BENCH_BATCH = {"resnet50": 1280, "yolov8n": 384}
+
 
 @dataclass
 class StepTimes:
