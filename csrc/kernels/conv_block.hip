@@ -9,26 +9,23 @@
 // never leaves the chip: each 64-pixel tile's 3x3 output goes from the accumulators into
 // LDS, and the conv3 GEMM reads it from there.
 //
-// Per 64-pixel tile (persistent workgroup of 4 waves, one per CU, walking tiles):
-//  * 9 ring stages (+1 for the downsample source): stage = one 3x3 tap x 64 channels of the
-//    conv1 output t for the tile's 64 pixels, global -> LDS by buffer_load ... lds (the
-//    buffer range check zero-fills conv padding and the M tail).  The 3x3 weights of a
-//    wave's 32 output channels live in 144 VGPRs for the whole kernel (as v4), so the ring
-//    carries activations only;
-//  * 3x3 epilogue: bias + ReLU -> bf16 c2 tile [64][64] in LDS (144-B pixel pitch:
-//    conflict-free 16-B fragment reads);
-//  * conv3 GEMM: A = c2 from LDS (+ the downsample source from the ring), B = the resident
-//    conv3 (| downsample) weights; then the v3 tail epilogue: bias + residual + ReLU, y
+// Per image row (tile = one row of W <= 64 pixels; a persistent workgroup of 4 waves, one
+// per CU, walks a contiguous range of rows):
+//  * a rolling window of three input rows of t (the conv1 output) sits in LDS at a 144-B
+//    pixel pitch (conflict-free 16-B fragment reads, as v4); each tile brings ONE new row,
+//    prefetched into VGPRs a whole tile ahead (an image's first row brings two);
+//  * 3x3: 9 taps x 4 k-steps of v_mfma_f32_32x32x16_bf16 per 32 x 32 block, the weights of a
+//    wave's 32 output channels held in 144 VGPRs for the whole kernel;
+//  * c2 = ReLU(. + b2) -> bf16 tile in LDS; conv3 (| the downsample source row, also in LDS)
+//    against the resident conv3 weights; then the v3 tail epilogue: bias + residual + ReLU, y
 //    stored in 16-B chunks and kept in LDS, z = ReLU(y . W1^T + b1) from LDS, z stored;
-//  * the ring is fed D-1 stages ahead ACROSS tile boundaries; every stage issues the same
-//    number of DMA ops and the residual is loaded (into registers) right after the DMA of
-//    the tile's last stage, so each wait is an exact s_waitcnt vmcnt over (ring depth,
-//    residual loads, epilogue stores) -- the stores of one tile drain under the next tile's
-//    stages.
-// Bytes per pixel: t 128 + residual 512 + y 512 + z 128..256 (the 3x3 halo re-reads come
-// from L2: the workgroups of one XCD walk neighbouring tiles together).
-#include <stdlib.h>
-
+//  * the next row's residual is loaded right after this row's stores, so it has the whole
+//    next tile to land; every wait is an exact s_waitcnt vmcnt over (prefetch loads, stores,
+//    residual loads).
+// Bytes per pixel: t 128 + residual 512 + y 512 + z 128..256.  Measured (batch 640,
+// profiles/r2_v8_block_probe.md): level with or slower than direct + tail -- with one
+// workgroup per CU (LDS 123-157 KB) the 3x3 phase and the memory phase of a row cannot
+// overlap.  Opt-in: KvResNet50.fuse_block.
 #include "common.h"
 #include "kvedge_kernels.h"
 
@@ -40,13 +37,12 @@ namespace {
 
 constexpr int kBM = 64;            // pixels per tile
 constexpr int kBN = 256;           // conv3 output channels (= y row)
-constexpr int kBK = 64;            // K per ring stage / per resident block
+constexpr int kBK = 64;            // K per resident weight block
 constexpr int kC2 = 64;            // bottleneck width (3x3 in/out channels)
 constexpr int kNT = 256;           // 4 waves, 2 x 2
 constexpr int kCS = kBN + 8;       // y tile pitch (elements)
 constexpr int kCS2 = kC2 + 8;      // c2 tile pitch (elements): 144 B
 constexpr int kPER = kBM * (kBN / 8) / kNT;  // 16-B y / residual chunks per thread (8)
-constexpr int kAINS = kBM / 32;    // DMA instructions per wave per stage (2)
 constexpr int kOOB = 0x7ffffff0;
 constexpr int kLdsMax = 160 * 1024;
 // s_waitcnt immediate (gfx9 encoding): vmcnt 0, expcnt 7 and lgkmcnt 15 (no wait on those)
@@ -76,22 +72,7 @@ __device__ __forceinline__ void bwait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N < 63 ? N : 63) : "memory");
 }
 
-__device__ __forceinline__ void bdivmod(int n, int d, float rcp, int& q, int& r) {
-  q = (int)((float)n * rcp);  // n < 2^24: off by at most one, corrected once
-  r = n - q * d;
-  if (r < 0) { --q; r += d; }
-  else if (r >= d) { ++q; r -= d; }
-}
-
-template <int N, int I = 0, class F>
-__device__ __forceinline__ void bstatic_for(F&& f) {
-  if constexpr (I < N) {
-    f(IC<I>{});
-    bstatic_for<N, I + 1>(f);
-  }
-}
-
-// chunk swizzle of ring / resident-weight rows (as v2/v3): 16-B chunk c of row r at c ^ sw(r)
+// chunk swizzle of resident-weight rows (as v2/v3): 16-B chunk c of row r at c ^ sw(r)
 __device__ __forceinline__ int bsw(int r) { return (r >> 1) & 7; }
 
 template <int NT1, bool DUAL>
