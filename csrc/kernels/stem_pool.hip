@@ -31,7 +31,7 @@
 //    exactly once (conflict-free with a LINEAR layout), so a tap's fragment address is
 //    the block base plus a compile-time constant = the ds_read immediate offset;
 //  * the bias seeds the accumulators (no per-element add) and out-of-image stem rows
-//    are skipped by the pool instead of being zeroed per element;
+//    are never read (the pool clamps its padding taps in-image) instead of being zeroed;
 //  * the pool runs packed 16-bit unsigned max (v_pk_max_u16) on the bf16 bit patterns:
 //    post-ReLU values are >= 0 and non-negative IEEE values order like their bits;
 //  * 512 threads (2 waves per SIMD): one wave's LDS reads / epilogue / pool overlap the
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(NT, 1) void stem_pool_kernel(
   // run back to back here: a band's first stem row (y0) is the previous band's last one,
   // still in the stem tile, and only 4 of the 5 rows are computed (the tile's rows are a
   // ring: stem row y lives in slot (y + kSR) % kSR).  Band 0's row -1 is padding the pool
-  // skips, so it is never computed either.  20 % fewer MFMAs than recomputing the shared row;
+  // never reads, so it is never computed either.  20 % fewer MFMAs than recomputing the shared row;
   // measured time barely moves (376-407 -> 381 us at batch 640): the kernel is bound by its
   // fetch / commit / pool phases, not the MFMAs (profiles/r2_v12_stem_ring.md)
   const int per = (total + gridDim.x - 1) / gridDim.x;
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(NT, 1) void stem_pool_kernel(
         __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
       }
       // ReLU -> bf16 stem tile.  Stem rows outside the image (above the first band, below
-      // an odd-H image) are written but never pooled: the pool skips them as padding.
+      // an odd-H image) are written but never read: the pool clamps padding taps in-image.
       if (rb * 32 + fr < npix) {
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
@@ -263,30 +263,39 @@ __global__ __launch_bounds__(NT, 1) void stem_pool_kernel(
     // after them waited for this band's stores to land)
     commit();
 
-    // ---- 3x3/2 max pool (pad 1) of the band -> global, 16 B per thread-iteration
+    // ---- 3x3/2 max pool (pad 1) of the band -> global, 16 B per thread-iteration.  Window
+    // taps outside the image are clamped onto the nearest in-image tap of the SAME window
+    // (x -1 -> 0, x W -> W-1, row -1 -> 0, row H -> H-1; the centre tap 2P / 2px is always
+    // inside): a duplicate never changes a max, so the nine tile reads issue back to back
+    // with no divergent branch.  The branchy form (skip padding taps) waited on each read in
+    // turn: 9 serialised LDS round trips per output, ~1/3 of the kernel's time
+    // (profiles/r2_v15_stem_pool_pmc.md)
 #pragma unroll
     for (int pr = 0; pr < kRB; ++pr) {
       const int P = P0 + pr;
       if (P >= Hp) break;
       bf16* yrow = y + (long long)(n * Hp + P) * Wp * ldy + y_coff;
+      int rbase[3];
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+        rbase[dy] = (min(max(2 * P - 1 + dy, 0), H - 1) % kSR) * W;  // ring slot of the row
       for (int q = tid; q < Wp * (kCo / 8); q += NT) {
         const int px = q >> 3, c8 = q & 7;
-        uint4 m = make_uint4(0u, 0u, 0u, 0u);
+        const int xs[3] = {max(2 * px - 1, 0), 2 * px, min(2 * px + 1, W - 1)};
+        uint4 v[9];
 #pragma unroll
-        for (int dy = 0; dy < 3; ++dy) {
-          const int yl = 2 * pr + dy;  // stem row y0 + yl
-          if ((unsigned)(y0 + yl) >= (unsigned)H) continue;  // padding row
+        for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-          for (int dx = -1; dx <= 1; ++dx) {
-            const int xs = 2 * px + dx;
-            if ((unsigned)xs >= (unsigned)W) continue;
-            const int slot = (y0 + yl + kSR) % kSR;
-            const uint4 v = *reinterpret_cast<const uint4*>(tile + (slot * W + xs) * kTS + c8 * 8);
-            m.x = pk_max_u16(m.x, v.x);
-            m.y = pk_max_u16(m.y, v.y);
-            m.z = pk_max_u16(m.z, v.z);
-            m.w = pk_max_u16(m.w, v.w);
-          }
+          for (int dx = 0; dx < 3; ++dx)
+            v[dy * 3 + dx] =
+                *reinterpret_cast<const uint4*>(tile + (rbase[dy] + xs[dx]) * kTS + c8 * 8);
+        uint4 m = v[0];
+#pragma unroll
+        for (int k = 1; k < 9; ++k) {
+          m.x = pk_max_u16(m.x, v[k].x);
+          m.y = pk_max_u16(m.y, v[k].y);
+          m.z = pk_max_u16(m.z, v[k].z);
+          m.w = pk_max_u16(m.w, v[k].w);
         }
         *reinterpret_cast<uint4*>(yrow + px * ldy + c8 * 8) = m;
       }
