@@ -44,6 +44,9 @@ def main(argv=None):
                          "YOLOv8n 384, from the batch sweeps in profiles/)")
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "yolov8n"])
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("KVEDGE_STREAMS", 0)),
+                    help="batch slices per step, one HIP stream each (0 = per-model default, "
+                         "engine.BENCH_STREAMS)")
     ap.add_argument("--no-autotune", action="store_true")
     ap.add_argument("--microbatch", type=int, default=int(os.environ.get("KVEDGE_MICROBATCH", 0)),
                     help="ResNet-50: run the first --mb-blocks bottlenecks in micro-batches "
@@ -66,7 +69,7 @@ def main(argv=None):
 
     import torch
     from kvedge_amd import ops, parallel
-    from kvedge_amd.engine import BENCH_BATCH, InferenceEngine
+    from kvedge_amd.engine import BENCH_BATCH, BENCH_STREAMS, InferenceEngine
 
     if a.gpus < 1:
         print("--gpus must be >= 1", file=sys.stderr)
@@ -96,6 +99,10 @@ def main(argv=None):
 
     if a.batch <= 0:
         a.batch = BENCH_BATCH[a.model] if on_gpu else 1
+    if a.streams <= 0:
+        a.streams = BENCH_STREAMS[a.model] if on_gpu else 1
+    if a.batch % a.streams:
+        a.streams = 1
     t_build = time.perf_counter()
     if a.model == "resnet50":
         from kvedge_amd.models.resnet import KvResNet50
@@ -114,7 +121,7 @@ def main(argv=None):
         with torch.no_grad():
             parallel.model_tensors(model)[-1].add_(0.05)
     eng = InferenceEngine(model, a.batch, hw, device=di.device, seed=a.seed + di.rank,
-                          use_graph=not a.no_graph)
+                          use_graph=not a.no_graph, streams=a.streams)
     eng.prepare(warmup=2, autotune=not a.no_autotune)
     build_s = time.perf_counter() - t_build
     from kvedge_amd.utils.logging import get_logger, log_event
@@ -184,6 +191,7 @@ def main(argv=None):
             "parallelism": f"dp{world}",
             "backend": di.backend,
             "hip_graph": eng.graph is not None,
+            "streams": eng.n_streams,
             "microbatch": getattr(model, "microbatch", 0),
             "mb_blocks": getattr(model, "microbatch_blocks", 0),
         },

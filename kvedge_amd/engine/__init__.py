@@ -26,6 +26,12 @@ from .. import ops
 # profiles/r1_v13_batch_sweep.jsonl).  Edge-module serving uses its own, latency-bound batch
 # (module twin `batch`, default 64).
 BENCH_BATCH = {"resnet50": 1280, "yolov8n": 384}
+# Batch slices per step, each on its own HIP stream (parallel branches of one hipGraph).
+# Two slices run concurrently fill each other's kernel drain/fill bubbles (same-box A/B,
+# profiles/r2_v17_streams_ab.jsonl): ResNet-50 b1280 75.4k -> 79.9k img/s, YOLOv8n b384
+# 38.4k -> 39.8k.  3-4 slices, or slices phase-shifted by event dependencies, lose
+# (profiles/r2_v17_stream_probe.jsonl).
+BENCH_STREAMS = {"resnet50": 2, "yolov8n": 2}
 
 
 @dataclass
@@ -48,14 +54,25 @@ class StepTimes:
         return s[i]
 
 
+def _cat_outputs(parts):
+    """Per-slice model outputs (a tensor or a tuple of tensors) -> full-batch outputs."""
+    if isinstance(parts[0], torch.Tensor):
+        return torch.cat(parts, 0)
+    return tuple(torch.cat(xs, 0) for xs in zip(*parts))
+
+
 class InferenceEngine:
     """Runs ``model(frames_u8) -> outputs`` on static-shape batches.
 
     model: any callable taking a uint8 NHWC3 frame batch (KvResNet50, KvYoloV8n).
+    streams: split each step's batch into this many equal slices, each run by the model on
+    its own HIP stream (forked from and joined back into the step's stream, so one hipGraph
+    holds them as parallel branches); per-slice outputs are concatenated along the batch.
     """
 
     def __init__(self, model: Callable, batch: int, image_size: int, device="cuda",
-                 seed: int = 0, use_graph: bool = True, synthetic: bool = True):
+                 seed: int = 0, use_graph: bool = True, synthetic: bool = True,
+                 streams: int = 1):
         self.model = model
         self.batch = batch
         self.hw = image_size
@@ -71,12 +88,32 @@ class InferenceEngine:
         self.outputs = None
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.times = StepTimes()
+        if streams < 1 or batch % streams:
+            raise ValueError(f"batch {batch} does not split into {streams} equal slices")
+        self.n_streams = streams if self.device.type == "cuda" else 1
+        self._side = [torch.cuda.Stream(device=self.device)
+                      for _ in range(self.n_streams)] if self.n_streams > 1 else []
 
     # one full edge-module step: synthesize frames, run the model
     def _step(self):
         if self.synthetic:
             ops.synth_frames(self.frames, self.seed, self.step_ctr)
-        self.outputs = self.model(self.frames)
+        return self._forward()
+
+    def _forward(self):
+        if not self._side:
+            self.outputs = self.model(self.frames)
+            return self.outputs
+        cur = torch.cuda.current_stream(self.device)
+        per = self.batch // self.n_streams
+        parts = []
+        for i, s in enumerate(self._side):
+            s.wait_stream(cur)
+            with torch.cuda.stream(s):
+                parts.append(self.model(self.frames[i * per:(i + 1) * per]))
+        for s in self._side:
+            cur.wait_stream(s)
+        self.outputs = _cat_outputs(parts)
         return self.outputs
 
     def prepare(self, warmup: int = 2, autotune: bool = True, verbose: bool = False):
@@ -87,7 +124,9 @@ class InferenceEngine:
             from .autotune import autotune as _tune
 
             ops.synth_frames(self.frames, self.seed, 0)
-            self.tuning = _tune(self.model, self.frames, verbose=verbose)
+            # tiles are pinned per layer for the shape the model actually runs: one slice
+            self.tuning = _tune(self.model, self.frames[:self.batch // self.n_streams],
+                                verbose=verbose)
         if not self.use_graph:
             for _ in range(warmup):
                 self._step()
@@ -159,5 +198,4 @@ class InferenceEngine:
     def set_frames(self, frames_u8: torch.Tensor):
         """Feed real frames instead of synthetic (disables the synthetic step)."""
         self.frames.copy_(frames_u8)
-        self.outputs = self.model(self.frames)
-        return self.outputs
+        return self._forward()

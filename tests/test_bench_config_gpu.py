@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from kvedge_amd import ops
-from kvedge_amd.engine import BENCH_BATCH, InferenceEngine
+from kvedge_amd.engine import BENCH_BATCH, BENCH_STREAMS, InferenceEngine
 
 pytestmark = pytest.mark.gpu
 
@@ -27,8 +27,8 @@ def test_resnet50_bench_config_vs_fp32_reference():
 
     ref = init_resnet50(seed=0)
     kv = KvResNet50(ref, "cuda")
-    B = BENCH_BATCH["resnet50"]
-    eng = InferenceEngine(kv, B, 224, device="cuda", seed=0, use_graph=True)
+    B, S = BENCH_BATCH["resnet50"], BENCH_STREAMS["resnet50"]
+    eng = InferenceEngine(kv, B, 224, device="cuda", seed=0, use_graph=True, streams=S)
     eng.prepare(warmup=1, autotune=True)
     assert eng.graph is not None and eng.tuning  # the timed configuration
     eng.run()
@@ -37,7 +37,8 @@ def test_resnet50_bench_config_vs_fp32_reference():
     probs_graph = eng.outputs[0][:n].float().cpu()
     frames = eng.frames[:n].cpu()
     with torch.no_grad():
-        lg_bench = kv.raw_outputs(eng.frames)[:n].float().cpu()  # same autotuned tiles
+        # one stream's slice: the shape (and autotuned tiles) the graph ran
+        lg_bench = kv.raw_outputs(eng.frames[:B // S])[:n].float().cpu()
         lg_ref = ref(frames_to_nchw(frames)).float()
         # yard-stick: the same fp32 weights run by PyTorch-ROCm (MIOpen) in bf16
         ref_bf16 = copy.deepcopy(ref).cuda().to(torch.bfloat16).to(memory_format=torch.channels_last)
@@ -55,7 +56,7 @@ def test_resnet50_bench_config_vs_fp32_reference():
     margins = (top2[:, 0] - top2[:, 1]).tolist()
     flips = (lg_bench.argmax(1) != lg_ref.argmax(1)).nonzero().flatten().tolist()
     flips_t = (lg_torch16.argmax(1) != lg_ref.argmax(1)).nonzero().flatten().tolist()
-    stats = {"images": n, "batch": B, "cos_logits": float(cos), "cos_logits_torch_bf16": float(cos_t),
+    stats = {"images": n, "batch": B, "streams": S, "cos_logits": float(cos), "cos_logits_torch_bf16": float(cos_t),
              "min_cos_per_image": float(per_img.min()), "top1_agree": agree,
              "top1_agree_torch_bf16": agree_t, "flip_margins": [margins[i] for i in flips],
              "flip_margins_torch_bf16": [margins[i] for i in flips_t],

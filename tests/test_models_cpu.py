@@ -1,4 +1,5 @@
 """CPU tests: BN folding, deployed ResNet-50 vs the fp32 module, engine plumbing."""
+import pytest
 import torch
 import torch.nn as nn
 
@@ -144,3 +145,21 @@ def test_resnet_stage1_block_fusion_plumbing():
         y_t, z_t = b.call_tail(x, nxt)
         assert torch.equal(y_f, y_t) and torch.equal(z_f, z_t)
         x = y_f
+
+
+def test_engine_streams_cpu_and_split_check():
+    from kvedge_amd.engine import _cat_outputs
+
+    class Tiny:
+        def __call__(self, frames):
+            return ops.softmax_rows(ops.preprocess(frames).float().mean((1, 2)).to(torch.bfloat16))
+
+    # CPU: slicing onto HIP streams collapses to one stream
+    eng = InferenceEngine(Tiny(), 4, 16, device="cpu", seed=1, streams=2).prepare(warmup=1)
+    assert eng.n_streams == 1 and eng.run()[0].shape == (4, 4)
+    with pytest.raises(ValueError):
+        InferenceEngine(Tiny(), 3, 16, device="cpu", streams=2)
+    a, b = torch.arange(6).view(2, 3), torch.arange(6, 12).view(2, 3)
+    assert torch.equal(_cat_outputs([a, b]), torch.arange(12).view(4, 3))
+    t = _cat_outputs([(a, a[:, 0]), (b, b[:, 0])])
+    assert torch.equal(t[0], torch.arange(12).view(4, 3)) and t[1].tolist() == [0, 3, 6, 9]
