@@ -11,6 +11,7 @@ On CPU the same engine runs the reference path eagerly (tests, no GPU).
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional
@@ -125,8 +126,9 @@ class InferenceEngine:
 
             ops.synth_frames(self.frames, self.seed, 0)
             # tiles are pinned per layer for the shape the model actually runs: one slice
+            conc = self.n_streams if os.environ.get("KVEDGE_TUNE_CONCURRENT", "1") != "0" else 1
             self.tuning = _tune(self.model, self.frames[:self.batch // self.n_streams],
-                                verbose=verbose)
+                                verbose=verbose, concurrency=conc)
         if not self.use_graph:
             for _ in range(warmup):
                 self._step()

@@ -33,6 +33,29 @@ def _time(fn: Callable[[int], object], tile: int, iters: int) -> float:
     return ts[len(ts) // 2]
 
 
+def _time_concurrent(fn: Callable[[int], object], tile: int, iters: int, streams) -> float:
+    """Median ms of ``len(streams)`` launches of ``fn(tile)`` issued together, one per
+    stream: the layer as the multi-stream engine runs it, its copies co-resident on the
+    CUs (a tile that fills every CU alone can lose to a leaner one under concurrency)."""
+    cur = torch.cuda.current_stream()
+    fn(tile)
+    evs = []
+    for _ in range(iters):
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        for s in streams:
+            s.wait_stream(cur)
+            with torch.cuda.stream(s):
+                fn(tile)
+        for s in streams:
+            cur.wait_stream(s)
+        en.record()
+        evs.append((st, en))
+    torch.cuda.synchronize()
+    ts = sorted(s.elapsed_time(e) for s, e in evs)
+    return ts[len(ts) // 2]
+
+
 def _time_interleaved(cands, rounds: int):
     """Median ms per (fn, tile) with the candidates timed round-robin (A B C A B C ...):
     a clock or thermal drift during the measurement then biases every candidate alike,
@@ -90,8 +113,12 @@ def _near_ties(rows, tol: float):
 
 def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
              cache_path: str = None, verbose: bool = False, refine_iters: int = None,
-             refine_tol: float = 0.15) -> Dict:
-    """Tune every conv of ``model`` for ``example_input``'s shape. Returns {key: (tile, us)}."""
+             refine_tol: float = 0.15, concurrency: int = 1) -> Dict:
+    """Tune every conv of ``model`` for ``example_input``'s shape. Returns {key: (tile, us)}.
+
+    concurrency > 1: time each tile as that many copies launched together on separate
+    streams (the multi-stream engine's situation); the near-tie refine pass then does
+    the same."""
     if not example_input.is_cuda:
         return {}
     if refine_iters is None:
@@ -105,6 +132,8 @@ def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
     torch.cuda.synchronize()
     ntiles = int(torch.ops.kvedge.conv_num_tiles())
     results: Dict = {}
+    side = [torch.cuda.Stream() for _ in range(concurrency)] if concurrency > 1 else None
+    timer = (lambda f, t, n: _time_concurrent(f, t, n, side)) if side else _time
     # phase 1: time every (distinct key, tile) on this GPU; invalid tiles stay +inf
     todo = {}  # key string -> (key, fn, [us per tile])
     for layer, key, fn in rec:
@@ -114,7 +143,7 @@ def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
         ts = [float("inf")] * ntiles
         for t in range(ntiles):
             try:
-                ts[t] = _time(fn, t, iters) * 1e3
+                ts[t] = timer(fn, t, iters) * 1e3
             except RuntimeError:  # tile not valid for this layer kind
                 continue
         todo[ks] = (key, fn, ts)
@@ -135,7 +164,10 @@ def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
             times = []
             for ks in dict.fromkeys(c[0] for c in cand):  # per layer, in first-seen order
                 grp = [(fn, t) for k, fn, t in cand if k == ks]
-                times += [x * 1e3 for x in _time_interleaved(grp, refine_iters)]
+                if side:
+                    times += [timer(f, t, refine_iters) * 1e3 for f, t in grp]
+                else:
+                    times += [x * 1e3 for x in _time_interleaved(grp, refine_iters)]
             re = _fleet_mean([times])[0]
             idx = {ks: i for i, ks in enumerate(todo)}
             for (ks, _, t), us in zip(cand, re):
