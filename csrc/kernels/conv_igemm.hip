@@ -312,10 +312,14 @@ int stream_tail_tile(int n_t);
 // v4 family (conv_direct.hip): persistent direct 3x3 conv for narrow channel counts
 int direct_num_tiles();
 int direct_launch(const KvConvParams* p, int tile, hipStream_t stream);
+// v6 A-resident N-loop 1x1 GEMM (conv_nloop.hip): indices after v4
+int nloop_num_tiles();
+int nloop_launch(const KvConvParams* p, int tile, hipStream_t stream);
 }  // namespace kvedge
 
 extern "C" int kv_conv_num_tiles(void) {
-  return kNumTiles + glds_num_tiles() + stream_num_tiles() + direct_num_tiles();
+  return kNumTiles + glds_num_tiles() + stream_num_tiles() + direct_num_tiles() +
+         nloop_num_tiles();
 }
 
 extern "C" int kv_conv_pick_tile(const KvConvParams* p) {
@@ -453,7 +457,9 @@ static int kv_conv2d_one(const KvConvParams* p, int tile, hipStream_t stream) {
   if (tile < 0) tile = kv_conv_pick_tile(p);
   const int v3 = kNumTiles + glds_num_tiles();
   const int v4 = v3 + stream_num_tiles();
-  if (tile >= v4 + direct_num_tiles()) return -6;
+  const int v6 = v4 + direct_num_tiles();
+  if (tile >= v6 + nloop_num_tiles()) return -6;
+  if (tile >= v6) return nloop_launch(p, tile - v6, stream);
   if (tile >= v4) return direct_launch(p, tile - v4, stream);
   if (tile >= v3) return stream_launch(p, tile - v3, stream);
   if (tile >= kNumTiles) return glds_launch(p, tile - kNumTiles, stream);

@@ -131,6 +131,10 @@ def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
         model(example_input)
     torch.cuda.synchronize()
     ntiles = int(torch.ops.kvedge.conv_num_tiles())
+    # A/B knob: tune over the first KVEDGE_TILE_LIMIT tiles only (e.g. without a new family)
+    lim = int(os.environ.get("KVEDGE_TILE_LIMIT", "0"))
+    if 0 < lim < ntiles:
+        ntiles = lim
     results: Dict = {}
     side = [torch.cuda.Stream() for _ in range(concurrency)] if concurrency > 1 else None
     timer = (lambda f, t, n: _time_concurrent(f, t, n, side)) if side else _time

@@ -82,7 +82,10 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale + 0.02
 
 
-N_TILES = 58  # v1 register-staged (0-5) + v2 LDS-DMA (6-31) + v3 streaming (32-53) + v4 direct (54-57)
+N_TILES = 63  # v1 register-staged (0-5) + v2 LDS-DMA (6-31) + v3 streaming (32-53) + v4 direct (54-57)
+# + v6 A-resident N-loop 1x1 GEMM (58-62, conv_nloop.hip kNlTiles: one Kpad per tile)
+NLOOP0 = 58
+NLOOP_KPAD = [128, 256, 256, 256, 256]
 STREAM0 = 32  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
 DIRECT0 = 54  # v4 direct 3x3 (conv_direct.hip): its instantiation table only
 # v2 8-wave (512-thread) tiles 24-28 (256x256 x2, 256x128, 128x256, 256x128 D3) and the
@@ -155,6 +158,32 @@ def test_conv_stream_gemm(tile, case):
     tiles, residual before/after the activation, sliced operands, tails."""
     N, H, W, cin, cout, act, res, lx, xc, ly, yc = case
     if tile >= STREAM0 and not _stream_fits(tile, (cin + 63) // 64 * 64, res):
+        with pytest.raises(RuntimeError):
+            _conv_case(N, H, W, cin, cout, 1, 1, 0, act, res=res, ldx_extra=lx, x_coff=xc,
+                       ldy_extra=ly, y_coff=yc, tile=tile)
+        return
+    err, scale = _conv_case(N, H, W, cin, cout, 1, 1, 0, act, res=res, ldx_extra=lx, x_coff=xc,
+                            ldy_extra=ly, y_coff=yc, tile=tile)
+    assert err <= 0.02 * scale + 0.02, (tile, case, err, scale)
+
+
+@pytest.mark.parametrize("tile", list(range(NLOOP0, N_TILES)))
+@pytest.mark.parametrize("case", [
+    # (N, H, W, cin, cout, act, res, ldx_extra, x_coff, ldy_extra, y_coff)
+    (4, 14, 14, 256, 1024, ops.ACT_RELU, True, 0, 0, 0, 0),     # ResNet stage-3 expand + res
+    (2, 28, 28, 128, 512, ops.ACT_RELU, True, 0, 0, 0, 0),      # stage-2 expand + res
+    (3, 7, 7, 512, 2048, ops.ACT_RELU, True, 0, 0, 0, 0),       # stage-4 expand, M tail
+    (2, 15, 13, 256, 136, ops.ACT_SILU | ops.RES_AFTER_ACT, True, 0, 0, 0, 0),  # N tail
+    (2, 9, 11, 200, 320, ops.ACT_SILU, False, 64, 40, 32, 16),  # K tail, slices in and out
+    (1, 3, 5, 120, 72, ops.ACT_NONE, False, 0, 0, 0, 0),        # one partial M tile, K 120
+])
+def test_conv_nloop_gemm(tile, case):
+    """v6 A-resident N-loop kernel: the counted-wait schedule across many N tiles (warm-up
+    and steady state), residual ring, in-place epilogue, K / M / N tails and slices;
+    tiles whose K does not match must refuse."""
+    N, H, W, cin, cout, act, res, lx, xc, ly, yc = case
+    kpad = (cin + 63) // 64 * 64
+    if kpad != NLOOP_KPAD[tile - NLOOP0]:
         with pytest.raises(RuntimeError):
             _conv_case(N, H, W, cin, cout, 1, 1, 0, act, res=res, ldx_extra=lx, x_coff=xc,
                        ldy_extra=ly, y_coff=yc, tile=tile)

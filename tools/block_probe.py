@@ -41,7 +41,7 @@ def main():
         return st.elapsed_time(en) / a.iters * 1e3
 
     spec2 = ConvSpec.auto(64, 64, 3, 1, 1, ops.ACT_RELU)
-    direct_tile = int(torch.ops.kvedge.conv_num_tiles()) - 4  # v4 tile 0 (VGPR prefetch)
+    direct_tile = 54  # v4 tile 0 (VGPR prefetch); tests/test_kernels_gpu.py DIRECT0
     print("| form | fused us | direct + tail us | saved | fused GB/s |")
     print("|---|---|---|---|---|")
     for name, dual, nt in (("dual (block 0)", True, 64), ("res nt64 (block 1)", False, 64),

@@ -29,7 +29,7 @@ def main():
               ("s3.c1", 14, 1024, 256, False), ("s3.c3", 14, 256, 1024, True),
               ("s4.c3", 7, 512, 2048, True), ("s4.c1", 7, 2048, 512, False),
               ("s3.c1a", 28, 512, 256, False), ("s4.c1a", 14, 1024, 512, False), ("s1.c3-nores", 56, 64, 256, False),
-              ("s2.c3-nores", 28, 128, 512, False), ("s1.c1a-wide", 56, 64, 512, False),
+              ("s2.c3-nores", 28, 128, 512, False), ("s3.c3-nores", 14, 256, 1024, False), ("s1.c1a-wide", 56, 64, 512, False),
               ("s1.c2", 56, 64, 64, False, 3), ("s2.c2", 28, 128, 128, False, 3),
               ("s3.c2", 14, 256, 256, False, 3), ("s4.c2", 7, 512, 512, False, 3)]
     if a.only:
