@@ -111,8 +111,11 @@ struct NlSched {
 
 __device__ __forceinline__ int nl_sw(int r) { return (r >> 1) & 7; }
 
-// BM = 16 * NW rows per workgroup (NW waves, 2 x (NW / 2) of 32 x 32 sub-tiles)
-template <int NK, int D, int RD, int NW>
+// BM = 16 * NW rows per workgroup (NW waves, 2 x (NW / 2) of 32 x 32 sub-tiles).
+// DUAL: the bottleneck's conv3 + fused downsample as one GEMM (mode 4): A chunks below K1
+// come from x (row m), the rest from x2 at the strided pixel (img, ho * s2, wo * s2); only
+// the resident-A prologue differs.
+template <int NK, int D, int RD, int NW, bool DUAL = false>
 __global__ __launch_bounds__(64 * NW, 1) void conv_nloop_kernel(const KvConvParams p, int ntiles) {
   using S = NlSched<NK, D, RD, NW>;
   constexpr int kNlNT = 64 * NW, BM = 16 * NW, BPW = 8 / NW;  // BPW: weight DMAs per wave
@@ -133,6 +136,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_nloop_kernel(const KvConvPara
 
   const kv_i32x4 rx = kv_rsrc4(p.x, p.N * p.H * p.W * p.ldx * 2);
   const kv_i32x4 rw = kv_rsrc4(p.w, p.Cout * p.Kpad * 2);
+  const kv_i32x4 rx2 = kv_rsrc4(DUAL ? p.x2 : p.x, DUAL ? p.N * p.H2 * p.W2 * p.ldx2 * 2 : 0);
   const kv_i32x4 rr = kv_rsrc4(p.res, p.res ? p.M * p.ldr * 2 : 0);
   const kv_i32x4 rb = kv_rsrc4(p.bias, p.bias ? p.Cout * 4 : 0);
   const __amdgpu_buffer_rsrc_t ry =
@@ -141,7 +145,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_nloop_kernel(const KvConvPara
   // DMA lane roles: 8 rows x 8 chunks of 16 B per instruction, 2 instructions per wave
   // cover 64 rows; row r's logical chunk (lane & 7) ^ sw(r) lands at position lane & 7
   const int lrow = lane >> 3, pch = lane & 7;
-  int arow_off[2], r_src[2], lc8[2], b_src[BPW];
+  int arow_off[2], a2_off[2], r_src[2], lc8[2], b_src[BPW];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = (wv * 2 + i) * 8 + lrow;
@@ -150,6 +154,12 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_nloop_kernel(const KvConvPara
     const int m = m0 + row;
     arow_off[i] = m < p.M ? (m * p.ldx + p.x_coff + lc * 8) * 2 : kNlOOB;
     r_src[i] = m < p.M ? (m * p.ldr + p.r_coff + lc * 8) * 2 : kNlOOB;
+    a2_off[i] = kNlOOB;
+    if (DUAL && m < p.M) {
+      const int hw = p.Ho * p.Wo, img = m / hw, rem = m - img * hw;
+      const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+      a2_off[i] = (((img * p.H2 + ho * p.stride2) * p.W2 + wo * p.stride2) * p.ldx2 + lc * 8) * 2;
+    }
   }
 #pragma unroll
   for (int i = 0; i < BPW; ++i) {
@@ -189,8 +199,17 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_nloop_kernel(const KvConvPara
   for (int kc = 0; kc < NK; ++kc)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int v = (arow_off[i] != kNlOOB && kc * 64 + lc8[i] < p.Cin) ? arow_off[i] + kc * 128 : kNlOOB;
-      kv_lds_dma16(rx, lds + kc * (BM * 128) + (wv * 2 + i) * 1024, v);
+      char* dst = lds + kc * (BM * 128) + (wv * 2 + i) * 1024;
+      if constexpr (DUAL) {  // K1 and K - K1 are multiples of 64: no K tails
+        if (kc * 64 < p.K1) {
+          kv_lds_dma16(rx, dst, arow_off[i] != kNlOOB ? arow_off[i] + kc * 128 : kNlOOB);
+        } else {
+          kv_lds_dma16(rx2, dst, a2_off[i] != kNlOOB ? a2_off[i] + (kc * 64 - p.K1) * 2 : kNlOOB);
+        }
+      } else {
+        const int v = (arow_off[i] != kNlOOB && kc * 64 + lc8[i] < p.Cin) ? arow_off[i] + kc * 128 : kNlOOB;
+        kv_lds_dma16(rx, dst, v);
+      }
     }
 #pragma unroll
   for (int t = 0; t < RD - 1; ++t) issue_R(t);
@@ -286,7 +305,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_nloop_kernel(const KvConvPara
 typedef void (*NlFn)(const KvConvParams, int);
 
 struct NlTile {
-  int nk, d, rd, nw;
+  int nk, d, rd, nw, dual;
   NlFn fn;
 };
 
@@ -298,11 +317,15 @@ struct NlTile {
 // the weight waits never queue behind HBM-latency ops) lost too (180 us: one wave cannot
 // issue a tile's 32 VMEM instructions fast enough).
 static const NlTile kNlTiles[] = {
-    {2, 6, 2, 8, &conv_nloop_kernel<2, 6, 2, 8>},  // K = 128 (stage-2 expand)
-    {4, 6, 2, 8, &conv_nloop_kernel<4, 6, 2, 8>},  // K = 256 (stage-3 expand)
-    {4, 7, 2, 8, &conv_nloop_kernel<4, 7, 2, 8>},  // K = 256, 7-slot ring (160 KB)
-    {4, 4, 3, 8, &conv_nloop_kernel<4, 4, 3, 8>},  // K = 256, residual two tiles ahead
-    {4, 5, 2, 8, &conv_nloop_kernel<4, 5, 2, 8>},  // K = 256, 5-slot ring
+    {2, 6, 2, 8, 0, &conv_nloop_kernel<2, 6, 2, 8>},  // K = 128 (stage-2 expand)
+    {4, 6, 2, 8, 0, &conv_nloop_kernel<4, 6, 2, 8>},  // K = 256 (stage-3 expand)
+    {4, 7, 2, 8, 0, &conv_nloop_kernel<4, 7, 2, 8>},  // K = 256, 7-slot ring (160 KB)
+    {4, 4, 3, 8, 0, &conv_nloop_kernel<4, 4, 3, 8>},  // K = 256, residual two tiles ahead
+    {4, 5, 2, 8, 0, &conv_nloop_kernel<4, 5, 2, 8>},  // K = 256, 5-slot ring
+    // fused downsample (dual, no residual: a 1-slot staging ring for the epilogue)
+    {6, 5, 1, 8, 1, &conv_nloop_kernel<6, 5, 1, 8, true>},    // K = 128 + 256 (stage 2)
+    {6, 4, 1, 8, 1, &conv_nloop_kernel<6, 4, 1, 8, true>},    // K = 128 + 256, 4-slot ring
+    {12, 5, 1, 4, 1, &conv_nloop_kernel<12, 5, 1, 4, true>},  // K = 256 + 512 (stage 3), BM 64
 };
 
 }  // namespace
@@ -319,8 +342,15 @@ int nloop_lds_bytes(int tile, int cout) {
 int nloop_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   if (tile < 0 || tile >= nloop_num_tiles()) return -6;
   const NlTile& e = kNlTiles[tile];
-  if (p->mode != 1 || p->n_t || p->in_u8) return -8;  // 1x1 stride-1 GEMM only
-  if (p->Kpad != e.nk * 64 || p->Cin > p->Kpad) return -8;
+  if (p->n_t || p->in_u8) return -8;
+  if (e.dual) {  // conv3 + fused downsample only
+    if (p->mode != 4 || p->res || !p->x2 || p->K1 % 64 || (p->Kpad - p->K1) % 64 ||
+        (long long)p->N * p->H2 * p->W2 * p->ldx2 * 2 >= kNlOOB)
+      return -8;
+  } else if (p->mode != 1) {
+    return -8;  // 1x1 stride-1 GEMM
+  }
+  if (p->Kpad != e.nk * 64 || (!e.dual && p->Cin > p->Kpad)) return -8;
   if ((long long)p->M * p->ldy * 2 >= kNlOOB || (p->res && (long long)p->M * p->ldr * 2 >= kNlOOB) ||
       (long long)p->N * p->H * p->W * p->ldx * 2 >= kNlOOB || (long long)p->Cout * p->Kpad * 2 >= kNlOOB)
     return -9;
