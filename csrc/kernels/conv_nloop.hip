@@ -313,9 +313,9 @@ struct NlTile {
 // table (Cout x 4 B, rounded up to nw KB).  Measured at batch 640 (profiles/r2_v18_*):
 // one 8-wave workgroup per CU with BM = 128 and a 5-7 slot ring beats two or three smaller
 // workgroups per CU (BM 64 / 32: 155-234 us on the stage-3 expand against 136-147 us), and
-// a warp-specialised form (8 compute waves + 1 wave issuing every residual DMA and store, so
-// the weight waits never queue behind HBM-latency ops) lost too (180 us: one wave cannot
-// issue a tile's 32 VMEM instructions fast enough).
+// warp-specialised forms (8 compute waves + 1, 2 or 4 waves issuing every residual DMA and
+// store, so the weight waits never queue behind HBM-latency ops in the in-order vmcnt) lost
+// too: 155-180 us (profiles/r2_v18_nloop_tile_probe.md, rounds d and e).
 static const NlTile kNlTiles[] = {
     {2, 6, 2, 8, 0, &conv_nloop_kernel<2, 6, 2, 8>},  // K = 128 (stage-2 expand)
     {4, 6, 2, 8, 0, &conv_nloop_kernel<4, 6, 2, 8>},  // K = 256 (stage-3 expand)
