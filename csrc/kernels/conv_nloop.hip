@@ -61,11 +61,12 @@ __device__ __forceinline__ void nl_wait_vm() {
 //   step s (tile t = s / NK, k = s % NK): WAIT(B(s)) | barrier | B(s + D - 1) |
 //       k == 0: R(t + RD - 1) | MFMAs | k == NK-1: WAIT(R(t)) ... epilogue ... stores(t)
 // In-order completion makes "B(s) landed" = vmcnt(#ops issued after B(s)).
-template <int NK, int D, int RD, int NW>
+template <int NK, int D, int RD, int NW, int KS2 = 1>
 struct NlSched {
   // per-wave instructions: a weight stage is 8 KB (8 DMA instructions over NW waves); an A
   // chunk, a residual tile and a tile's stores are BM x 128 B = 2 instructions per wave
-  static constexpr int kB = 8 / NW, kR = 2, kS = 2, kA = 2 * NK;
+  // (KS2 64-wide K chunks per step: a weight stage is KS2 x 8 KB)
+  static constexpr int kB = KS2 * 8 / NW, kR = 2, kS = 2, kA = 2 * NK * KS2;
   static constexpr int steps_ops(int u) {  // ops of steps 0 .. u-1 (incl. their R / stores)
     return u * kB + ((u + NK - 1) / NK) * kR + (u / NK) * kS;
   }
@@ -115,15 +116,19 @@ __device__ __forceinline__ int nl_sw(int r) { return (r >> 1) & 7; }
 // DUAL: the bottleneck's conv3 + fused downsample as one GEMM (mode 4): A chunks below K1
 // come from x (row m), the rest from x2 at the strided pixel (img, ho * s2, wo * s2); only
 // the resident-A prologue differs.
-template <int NK, int D, int RD, int NW, bool DUAL = false>
+// KS2: 64-wide K chunks per ring step (2 = 128-wide steps: half the barriers and waits per
+// MFMA, the same ring bytes); NK = K steps per N tile = Kpad / (64 KS2).
+template <int NK, int D, int RD, int NW, bool DUAL = false, int KS2 = 1>
 __global__ __launch_bounds__(64 * NW, 1) void conv_nloop_kernel(const KvConvParams p, int ntiles) {
-  using S = NlSched<NK, D, RD, NW>;
+  using S = NlSched<NK, D, RD, NW, KS2>;
+  constexpr int NC = NK * KS2;  // 64-wide K chunks of A
   constexpr int kNlNT = 64 * NW, BM = 16 * NW, BPW = 8 / NW;  // BPW: weight DMAs per wave
   static_assert(NW == 2 || NW == 4 || NW == 8, "waves");
   static_assert(S::steady_B(0) <= 63 && S::steady_E() <= 63, "vmcnt range");
   static_assert(S::kSteady < S::kFar, "schedule must become periodic");
   constexpr int BN = kNlBN;
-  constexpr int A_BYTES = NK * BM * 128, B_STAGE = BN * 128, R_SLOT = BM * BN * 2;
+  constexpr int A_BYTES = NC * BM * 128, B_CHUNK = BN * 128, B_STAGE = KS2 * B_CHUNK;
+  constexpr int R_SLOT = BM * BN * 2;
   constexpr int B_OFF = A_BYTES, R_OFF = B_OFF + D * B_STAGE, BIAS_OFF = R_OFF + RD * R_SLOT;
   extern __shared__ __attribute__((aligned(16))) char nl_smem[];
   char* const lds = nl_smem;
@@ -168,14 +173,16 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_nloop_kernel(const KvConvPara
   }
 
   auto issue_B = [&](int s) __attribute__((always_inline)) {
-    const int t = s / NK, kc = s - (s / NK) * NK;
+    const int t = s / NK, kc = (s - (s / NK) * NK) * KS2;
     char* dst = lds + B_OFF + (s % D) * B_STAGE;
 #pragma unroll
-    for (int i = 0; i < BPW; ++i) {
-      const int n = t * BN + (wv * BPW + i) * 8 + lrow;
-      const int v = (t < ntiles && n < p.Cout) ? b_src[i] + (t * BN * p.Kpad + kc * 64) * 2 : kNlOOB;
-      kv_lds_dma16(rw, dst + (wv * BPW + i) * 1024, v);
-    }
+    for (int j = 0; j < KS2; ++j)
+#pragma unroll
+      for (int i = 0; i < BPW; ++i) {
+        const int n = t * BN + (wv * BPW + i) * 8 + lrow;
+        const int v = (t < ntiles && n < p.Cout) ? b_src[i] + (t * BN * p.Kpad + (kc + j) * 64) * 2 : kNlOOB;
+        kv_lds_dma16(rw, dst + j * B_CHUNK + (wv * BPW + i) * 1024, v);
+      }
   };
   auto issue_R = [&](int t) __attribute__((always_inline)) {
     char* dst = lds + R_OFF + (t % RD) * R_SLOT;
@@ -196,7 +203,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_nloop_kernel(const KvConvPara
     }
   }
 #pragma unroll
-  for (int kc = 0; kc < NK; ++kc)
+  for (int kc = 0; kc < NC; ++kc)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       char* dst = lds + kc * (BM * 128) + (wv * 2 + i) * 1024;
@@ -236,27 +243,30 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_nloop_kernel(const KvConvPara
         asm volatile("" ::: "memory");
         issue_B(s + D - 1);
         if constexpr (k == 0) issue_R(t + RD - 1);
-        const char* As = lds + k * (BM * 128);
-        const char* Bs = lds + B_OFF + (s % D) * B_STAGE;
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const int q = ks * 4 + fh;
-          bf16x8 af[2], bfg[2];
+        for (int j = 0; j < KS2; ++j) {
+          const char* As = lds + (k * KS2 + j) * (BM * 128);
+          const char* Bs = lds + B_OFF + (s % D) * B_STAGE + j * B_CHUNK;
 #pragma unroll
-          for (int tm = 0; tm < 2; ++tm) {
-            const int row = wm * 32 + tm * 16 + fr;
-            af[tm] = *reinterpret_cast<const bf16x8*>(As + row * 128 + ((q ^ nl_sw(row)) << 4));
+          for (int ks = 0; ks < 2; ++ks) {
+            const int q = ks * 4 + fh;
+            bf16x8 af[2], bfg[2];
+#pragma unroll
+            for (int tm = 0; tm < 2; ++tm) {
+              const int row = wm * 32 + tm * 16 + fr;
+              af[tm] = *reinterpret_cast<const bf16x8*>(As + row * 128 + ((q ^ nl_sw(row)) << 4));
+            }
+#pragma unroll
+            for (int tn = 0; tn < 2; ++tn) {
+              const int row = wn * 32 + tn * 16 + fr;
+              bfg[tn] = *reinterpret_cast<const bf16x8*>(Bs + row * 128 + ((q ^ nl_sw(row)) << 4));
+            }
+#pragma unroll
+            for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+              for (int tm = 0; tm < 2; ++tm)
+                acc[tn][tm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[tn], af[tm], acc[tn][tm], 0, 0, 0);
           }
-#pragma unroll
-          for (int tn = 0; tn < 2; ++tn) {
-            const int row = wn * 32 + tn * 16 + fr;
-            bfg[tn] = *reinterpret_cast<const bf16x8*>(Bs + row * 128 + ((q ^ nl_sw(row)) << 4));
-          }
-#pragma unroll
-          for (int tn = 0; tn < 2; ++tn)
-#pragma unroll
-            for (int tm = 0; tm < 2; ++tm)
-              acc[tn][tm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[tn], af[tm], acc[tn][tm], 0, 0, 0);
         }
       });
       // ---- epilogue of tile t: residual slot t % RD holds R(t); y overwrites it in place
@@ -305,7 +315,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_nloop_kernel(const KvConvPara
 typedef void (*NlFn)(const KvConvParams, int);
 
 struct NlTile {
-  int nk, d, rd, nw, dual;
+  int nk, d, rd, nw, dual, ks2;  // nk: K steps per N tile of ks2 x 64 K each
   NlFn fn;
 };
 
@@ -317,15 +327,20 @@ struct NlTile {
 // store, so the weight waits never queue behind HBM-latency ops in the in-order vmcnt) lost
 // too: 155-180 us (profiles/r2_v18_nloop_tile_probe.md, rounds d and e).
 static const NlTile kNlTiles[] = {
-    {2, 6, 2, 8, 0, &conv_nloop_kernel<2, 6, 2, 8>},  // K = 128 (stage-2 expand)
-    {4, 6, 2, 8, 0, &conv_nloop_kernel<4, 6, 2, 8>},  // K = 256 (stage-3 expand)
-    {4, 7, 2, 8, 0, &conv_nloop_kernel<4, 7, 2, 8>},  // K = 256, 7-slot ring (160 KB)
-    {4, 4, 3, 8, 0, &conv_nloop_kernel<4, 4, 3, 8>},  // K = 256, residual two tiles ahead
-    {4, 5, 2, 8, 0, &conv_nloop_kernel<4, 5, 2, 8>},  // K = 256, 5-slot ring
+    {2, 6, 2, 8, 0, 1, &conv_nloop_kernel<2, 6, 2, 8>},  // K = 128 (stage-2 expand)
+    {4, 6, 2, 8, 0, 1, &conv_nloop_kernel<4, 6, 2, 8>},  // K = 256 (stage-3 expand)
+    {4, 7, 2, 8, 0, 1, &conv_nloop_kernel<4, 7, 2, 8>},  // K = 256, 7-slot ring (160 KB)
+    {4, 4, 3, 8, 0, 1, &conv_nloop_kernel<4, 4, 3, 8>},  // K = 256, residual two tiles ahead
+    {4, 5, 2, 8, 0, 1, &conv_nloop_kernel<4, 5, 2, 8>},  // K = 256, 5-slot ring
     // fused downsample (dual, no residual: a 1-slot staging ring for the epilogue)
-    {6, 5, 1, 8, 1, &conv_nloop_kernel<6, 5, 1, 8, true>},    // K = 128 + 256 (stage 2)
-    {6, 4, 1, 8, 1, &conv_nloop_kernel<6, 4, 1, 8, true>},    // K = 128 + 256, 4-slot ring
-    {12, 5, 1, 4, 1, &conv_nloop_kernel<12, 5, 1, 4, true>},  // K = 256 + 512 (stage 3), BM 64
+    {6, 5, 1, 8, 1, 1, &conv_nloop_kernel<6, 5, 1, 8, true>},    // K = 128 + 256 (stage 2)
+    {6, 4, 1, 8, 1, 1, &conv_nloop_kernel<6, 4, 1, 8, true>},    // K = 128 + 256, 4-slot ring
+    {12, 5, 1, 4, 1, 1, &conv_nloop_kernel<12, 5, 1, 4, true>},  // K = 256 + 512 (stage 3), BM 64
+    // 128-wide K steps (two 64-chunks per ring slot): stage-3 expand 143 -> 136 us at b640;
+    // the K = 128 and dual forms of this step lost (266 vs 245 us, 391 vs 353 us) and are not
+    // instantiated (profiles/r2_v18_nloop_tile_probe.md, round f)
+    {2, 3, 2, 8, 0, 2, &conv_nloop_kernel<2, 3, 2, 8, false, 2>},  // K = 256
+    {2, 3, 1, 8, 0, 2, &conv_nloop_kernel<2, 3, 1, 8, false, 2>},  // K = 256, 1-slot residual
 };
 
 }  // namespace
@@ -335,7 +350,7 @@ int nloop_num_tiles() { return (int)(sizeof(kNlTiles) / sizeof(kNlTiles[0])); }
 int nloop_lds_bytes(int tile, int cout) {
   const NlTile& e = kNlTiles[tile];
   const int bm = 16 * e.nw;
-  return e.nk * bm * 128 + e.d * kNlBN * 128 + e.rd * bm * kNlBN * 2 +
+  return e.nk * e.ks2 * bm * 128 + e.d * e.ks2 * kNlBN * 128 + e.rd * bm * kNlBN * 2 +
          ((cout * 4 + e.nw * 1024 - 1) / (e.nw * 1024)) * (e.nw * 1024);
 }
 
@@ -350,7 +365,7 @@ int nloop_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   } else if (p->mode != 1) {
     return -8;  // 1x1 stride-1 GEMM
   }
-  if (p->Kpad != e.nk * 64 || (!e.dual && p->Cin > p->Kpad)) return -8;
+  if (p->Kpad != e.nk * e.ks2 * 64 || (!e.dual && p->Cin > p->Kpad)) return -8;
   if ((long long)p->M * p->ldy * 2 >= kNlOOB || (p->res && (long long)p->M * p->ldr * 2 >= kNlOOB) ||
       (long long)p->N * p->H * p->W * p->ldx * 2 >= kNlOOB || (long long)p->Cout * p->Kpad * 2 >= kNlOOB)
     return -9;

@@ -82,12 +82,12 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale + 0.02
 
 
-N_TILES = 66  # v1 register-staged (0-5) + v2 LDS-DMA (6-31) + v3 streaming (32-53) + v4 direct (54-57)
-# + v6 A-resident N-loop 1x1 GEMM (58-65, conv_nloop.hip kNlTiles: one Kpad per tile;
-# 63-65 are the fused-downsample (dual) forms)
+N_TILES = 68  # v1 register-staged (0-5) + v2 LDS-DMA (6-31) + v3 streaming (32-53) + v4 direct (54-57)
+# + v6 A-resident N-loop 1x1 GEMM (58-67, conv_nloop.hip kNlTiles: one Kpad per tile;
+# 63-65 are the fused-downsample (dual) forms, 66-67 step 128 K at a time)
 NLOOP0 = 58
-NLOOP_KPAD = [128, 256, 256, 256, 256, 384, 384, 768]
-NLOOP_DUAL0 = 63
+NLOOP_KPAD = [128, 256, 256, 256, 256, 384, 384, 768, 256, 256]
+NLOOP_DUAL = {63, 64, 65}
 STREAM0 = 32  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
 DIRECT0 = 54  # v4 direct 3x3 (conv_direct.hip): its instantiation table only
 # v2 8-wave (512-thread) tiles 24-28 (256x256 x2, 256x128, 128x256, 256x128 D3) and the
@@ -185,7 +185,7 @@ def test_conv_nloop_gemm(tile, case):
     tiles whose K does not match must refuse."""
     N, H, W, cin, cout, act, res, lx, xc, ly, yc = case
     kpad = (cin + 63) // 64 * 64
-    if kpad != NLOOP_KPAD[tile - NLOOP0] or tile >= NLOOP_DUAL0:
+    if kpad != NLOOP_KPAD[tile - NLOOP0] or tile in NLOOP_DUAL:
         with pytest.raises(RuntimeError):
             _conv_case(N, H, W, cin, cout, 1, 1, 0, act, res=res, ldx_extra=lx, x_coff=xc,
                        ldy_extra=ly, y_coff=yc, tile=tile)
@@ -309,7 +309,7 @@ def test_nms_dense_overlaps():
     assert (o.cpu() - o_ref).abs().max() < 1e-4
 
 
-@pytest.mark.parametrize("tile", [-1] + list(range(6, DIRECT0)) + list(range(NLOOP_DUAL0, N_TILES)))
+@pytest.mark.parametrize("tile", [-1] + list(range(6, DIRECT0)) + sorted(NLOOP_DUAL) + [NLOOP0 + 8])
 @pytest.mark.parametrize("geom", [(2, 14, 14, 64, 128, 256, 2), (2, 7, 7, 128, 256, 512, 1),
                                   (1, 5, 5, 64, 64, 128, 2),
                                   # the v6 dual tiles' K: 128 + 256 and 256 + 512, tails
@@ -323,7 +323,7 @@ def test_conv_dual_fused_downsample(tile, geom):
     w = (torch.randn(cout, K1 + K2, generator=g) * 0.05).to(torch.bfloat16)
     b = torch.randn(cout, generator=g)
     ref = ops.conv_dual(x1, x2, w, b, ops.ACT_RELU, s)
-    if tile >= NLOOP_DUAL0 and K1 + K2 != NLOOP_KPAD[tile - NLOOP0]:
+    if tile >= NLOOP0 and (tile not in NLOOP_DUAL or K1 + K2 != NLOOP_KPAD[tile - NLOOP0]):
         with pytest.raises(RuntimeError):  # each v6 dual tile is compiled for one K
             ops.conv_dual(x1.cuda(), x2.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, s, tile=tile)
         return
