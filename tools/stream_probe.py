@@ -2,11 +2,12 @@
 hipGraph with S parallel branches) overlap the compute-bound 3x3 convs of one slice with
 the HBM-bound 1x1 / tail kernels of another?
 
-Slice i+1 starts when slice i has finished ``--stagger`` bottlenecks (0 = only its stem),
-so the branches run phase-shifted instead of in lock-step.
+Each config is S:stagger.  stagger -2: no dependency between the branches (lock-step);
+-1: slice i+1 starts when slice i has finished its stem; k >= 0: when slice i has finished
+bottleneck k -- the branches then run phase-shifted.  Measured (profiles/r2_v17_stream_probe.jsonl):
+two slices in lock-step win; 3-4 slices and every phase shift lose.
 
-  python tools/stream_probe.py --batch 1280 --configs 1:0,2:-1,2:0,2:3,2:7
-  (S:stagger; stagger -1 = no dependency between the branches)
+  python tools/stream_probe.py --batch 1280 --configs 1:-2,2:-2,2:-1,2:2,2:6
 """
 from __future__ import annotations
 
