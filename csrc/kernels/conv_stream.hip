@@ -516,7 +516,16 @@ static const StreamTile kStreamTiles[] = {
 namespace kvedge {
 
 int stream_num_tiles() { return (int)(sizeof(kStreamTiles) / sizeof(kStreamTiles[0])); }
-int stream_tail_tile(int n_t) { return stream_num_tiles() - (n_t > 64 ? 1 : 2); }
+// default fused-tail tile: the 32x32x16 forms (last two entries); KVEDGE_TAIL_MF16=1 picks
+// the 16x16x32 forms (the two entries before them) -- an A/B knob, as tails are not autotuned;
+// measured neutral within box noise (profiles/r2_v22_ab_tail_mf16.jsonl)
+int stream_tail_tile(int n_t) {
+  static const int mf16 = [] {
+    const char* s = getenv("KVEDGE_TAIL_MF16");
+    return s && s[0] == '1' ? 2 : 0;
+  }();
+  return stream_num_tiles() - (n_t > 64 ? 1 : 2) - mf16;
+}
 
 int stream_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   if (tile < 0 || tile >= stream_num_tiles()) return -6;
