@@ -147,8 +147,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_nloop_kernel(const KvConvPara
   const __amdgpu_buffer_rsrc_t ry =
       __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, p.M * p.ldy * 2, 0x00020000);
 
-  // DMA lane roles: 8 rows x 8 chunks of 16 B per instruction, 2 instructions per wave
-  // cover 64 rows; row r's logical chunk (lane & 7) ^ sw(r) lands at position lane & 7
+  // DMA lane roles: 8 rows x 8 chunks of 16 B per instruction; 2 instructions per wave
+  // cover the BM = 16 NW rows of A / a residual tile (BPW per wave for a weight chunk);
+  // row r's logical chunk (lane & 7) ^ sw(r) lands at position lane & 7
   const int lrow = lane >> 3, pch = lane & 7;
   int arow_off[2], a2_off[2], r_src[2], lc8[2], b_src[BPW];
 #pragma unroll
