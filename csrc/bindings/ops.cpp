@@ -483,6 +483,7 @@ void batchnorm_nhwc(const at::Tensor& x, at::Tensor& y, const at::Tensor& scale,
 }
 
 int64_t conv_num_tiles() { return kv_conv_num_tiles(); }
+int64_t nloop_sched_check() { return kv_nloop_sched_check(); }
 int64_t set_conv_chunk_bytes(int64_t b) { return kv_set_conv_chunk_bytes(b); }
 
 }  // namespace
@@ -518,6 +519,7 @@ TORCH_LIBRARY(kvedge, m) {
   m.def("preprocess(Tensor x, Tensor(a!) y, float[] mean, float[] std) -> ()");
   m.def("batchnorm_nhwc(Tensor x, Tensor(a!) y, Tensor scale, Tensor shift, bool relu) -> ()");
   m.def("conv_num_tiles() -> int", conv_num_tiles);
+  m.def("nloop_sched_check() -> int", nloop_sched_check);
   m.def("set_conv_chunk_bytes(int bytes) -> int", set_conv_chunk_bytes);
 }
 

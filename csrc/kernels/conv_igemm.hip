@@ -315,7 +315,10 @@ int direct_launch(const KvConvParams* p, int tile, hipStream_t stream);
 // v6 A-resident N-loop 1x1 GEMM (conv_nloop.hip): indices after v4
 int nloop_num_tiles();
 int nloop_launch(const KvConvParams* p, int tile, hipStream_t stream);
+int nloop_sched_check();
 }  // namespace kvedge
+
+extern "C" int kv_nloop_sched_check(void) { return kvedge::nloop_sched_check(); }
 
 extern "C" int kv_conv_num_tiles(void) {
   return kNumTiles + glds_num_tiles() + stream_num_tiles() + direct_num_tiles() +

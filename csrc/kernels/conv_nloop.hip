@@ -313,12 +313,51 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_nloop_kernel(const KvConvPara
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// Host self-check of the counted-wait schedule (tests/test_conv_nloop_sched_cpu.py): replays
+// one wave's VMEM issue order for 3 x kFar N tiles exactly as the kernel issues it and
+// requires every wait the kernel uses to be <= the exact count of ops issued after the
+// awaited one (a larger count would let the wave read LDS before its DMA lands), and equal
+// to it from the steady tile on (a smaller one only over-waits).  Returns 0 when the
+// schedule is safe, else a code naming the first violation.
+template <int NK, int D, int RD, int NW, int KS2>
+int nl_sched_check() {
+  using S = NlSched<NK, D, RD, NW, KS2>;
+  constexpr int T = 3 * S::kFar, NS = T * NK + D + 1;
+  long long endB[NS] = {}, endR[T + RD + 1] = {};
+  long long pos = S::kA;  // bias table DMAs precede everything that is waited on
+  for (int t = 0; t < RD - 1; ++t) endR[t] = (pos += S::kR);
+  for (int s = 0; s < D - 1; ++s) endB[s] = (pos += S::kB);
+  for (int t = 0; t < T; ++t) {
+    for (int k = 0; k < NK; ++k) {
+      const int s = t * NK + k;
+      const long long exact = pos - endB[s];
+      const int used = t < S::kSteady ? S::safe_B(k) : S::steady_B(k);
+      if (used > exact || (t >= S::kSteady && used != exact) || used > 63) return 1000 + s;
+      endB[s + D - 1] = (pos += S::kB);
+      if (k == 0) endR[t + RD - 1] = (pos += S::kR);
+    }
+    const long long exact = pos - endR[t];
+    const int used = t < S::kSteady ? S::safe_E() : S::steady_E();
+    if (used > exact || (t >= S::kSteady && used != exact) || used > 63) return 2000 + t;
+    pos += S::kS;
+  }
+  return 0;
+}
+
 typedef void (*NlFn)(const KvConvParams, int);
 
 struct NlTile {
   int nk, d, rd, nw, dual, ks2;  // nk: K steps per N tile of ks2 x 64 K each
   NlFn fn;
+  int (*sched_check)();
 };
+
+// one table row: the kernel and its schedule check from the same template arguments
+template <int NK, int D, int RD, int NW, bool DUAL = false, int KS2 = 1>
+constexpr NlTile nl_tile() {
+  return NlTile{NK, D, RD, NW, DUAL ? 1 : 0, KS2, &conv_nloop_kernel<NK, D, RD, NW, DUAL, KS2>,
+                &nl_sched_check<NK, D, RD, NW, KS2>};
+}
 
 // LDS = A (K x BM x 2) + d x 8 KB weight ring + rd x BM x 128 B residual ring + the bias
 // table (Cout x 4 B, rounded up to nw KB).  Measured at batch 640 (profiles/r2_v18_*):
@@ -328,25 +367,33 @@ struct NlTile {
 // store, so the weight waits never queue behind HBM-latency ops in the in-order vmcnt) lost
 // too: 155-180 us (profiles/r2_v18_nloop_tile_probe.md, rounds d and e).
 static const NlTile kNlTiles[] = {
-    {2, 6, 2, 8, 0, 1, &conv_nloop_kernel<2, 6, 2, 8>},  // K = 128 (stage-2 expand)
-    {4, 6, 2, 8, 0, 1, &conv_nloop_kernel<4, 6, 2, 8>},  // K = 256 (stage-3 expand)
-    {4, 7, 2, 8, 0, 1, &conv_nloop_kernel<4, 7, 2, 8>},  // K = 256, 7-slot ring (160 KB)
-    {4, 4, 3, 8, 0, 1, &conv_nloop_kernel<4, 4, 3, 8>},  // K = 256, residual two tiles ahead
-    {4, 5, 2, 8, 0, 1, &conv_nloop_kernel<4, 5, 2, 8>},  // K = 256, 5-slot ring
+    nl_tile<2, 6, 2, 8>(),  // K = 128 (stage-2 expand)
+    nl_tile<4, 6, 2, 8>(),  // K = 256 (stage-3 expand)
+    nl_tile<4, 7, 2, 8>(),  // K = 256, 7-slot ring (160 KB)
+    nl_tile<4, 4, 3, 8>(),  // K = 256, residual two tiles ahead
+    nl_tile<4, 5, 2, 8>(),  // K = 256, 5-slot ring
     // fused downsample (dual, no residual: a 1-slot staging ring for the epilogue)
-    {6, 5, 1, 8, 1, 1, &conv_nloop_kernel<6, 5, 1, 8, true>},    // K = 128 + 256 (stage 2)
-    {6, 4, 1, 8, 1, 1, &conv_nloop_kernel<6, 4, 1, 8, true>},    // K = 128 + 256, 4-slot ring
-    {12, 5, 1, 4, 1, 1, &conv_nloop_kernel<12, 5, 1, 4, true>},  // K = 256 + 512 (stage 3), BM 64
+    nl_tile<6, 5, 1, 8, true>(),   // K = 128 + 256 (stage 2)
+    nl_tile<6, 4, 1, 8, true>(),   // K = 128 + 256, 4-slot ring
+    nl_tile<12, 5, 1, 4, true>(),  // K = 256 + 512 (stage 3), BM 64
     // 128-wide K steps (two 64-chunks per ring slot): stage-3 expand 143 -> 136 us at b640;
     // the K = 128 and dual forms of this step lost (266 vs 245 us, 391 vs 353 us) and are not
     // instantiated (profiles/r2_v18_nloop_tile_probe.md, round f)
-    {2, 3, 2, 8, 0, 2, &conv_nloop_kernel<2, 3, 2, 8, false, 2>},  // K = 256
-    {2, 3, 1, 8, 0, 2, &conv_nloop_kernel<2, 3, 1, 8, false, 2>},  // K = 256, 1-slot residual
+    nl_tile<2, 3, 2, 8, false, 2>(),  // K = 256
+    nl_tile<2, 3, 1, 8, false, 2>(),  // K = 256, 1-slot residual
 };
 
 }  // namespace
 
 int nloop_num_tiles() { return (int)(sizeof(kNlTiles) / sizeof(kNlTiles[0])); }
+
+// 0 if every v6 tile's counted-wait schedule is safe (host-side replay), else
+// tile * 10000 + the violation code of nl_sched_check
+int nloop_sched_check() {
+  for (int i = 0; i < nloop_num_tiles(); ++i)
+    if (const int rc = kNlTiles[i].sched_check()) return i * 10000 + rc;
+  return 0;
+}
 
 int nloop_lds_bytes(int tile, int cout) {
   const NlTile& e = kNlTiles[tile];
