@@ -63,7 +63,12 @@ def main(argv=None):
     ap.add_argument("--native-loop", action="store_true",
                     help="time the K steps with the native C++ serve loop (csrc/runtime) "
                          "instead of Python graph.replay() calls")
+    ap.add_argument("--launch-timeout", type=float,
+                    default=float(os.environ.get("KVEDGE_LAUNCH_TIMEOUT", 1500)),
+                    help="self-launch (--gpus N > 1 without torchrun): kill every rank after "
+                         "this many seconds (a hung RCCL init must not hang the job)")
     ap.add_argument("--perturb-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--hang-rank", type=int, default=-1, help=argparse.SUPPRESS)
     raw = list(sys.argv[1:] if argv is None else argv)
     a = ap.parse_args(raw)
 
@@ -80,11 +85,15 @@ def main(argv=None):
             if a.gpus > ndev:
                 print(f"--gpus {a.gpus} but only {ndev} GPU(s) visible", file=sys.stderr)
                 return 2
-        return parallel.launch_local(a.gpus, [os.path.abspath(__file__)] + raw)
+        return parallel.launch_local(a.gpus, [os.path.abspath(__file__)] + raw,
+                                     timeout_s=a.launch_timeout if a.launch_timeout > 0 else None)
     if int(os.environ.get("WORLD_SIZE", "1")) != a.gpus:
         print(f"# note: --gpus {a.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')}; "
               "reporting the launched world size", file=sys.stderr)
 
+    if a.hang_rank >= 0 and a.hang_rank == int(os.environ.get("RANK", "0")):
+        while True:  # test hook (tests/test_bench_cpu.py): a rank that never arrives
+            time.sleep(3600)
     di = parallel.init_from_env(prefer_gpu=not a.cpu)
     on_gpu = di.device.type == "cuda"
     if not on_gpu and not a.cpu:

@@ -20,12 +20,23 @@ but the workload is ResNet-50 / YOLOv8n on the passed-through MI355X:
 Multi-replica lockstep (world_size > 1, one rank per GPU/VM).  Every collective a rank
 issues must be issued by every other rank in the same order, but twin patches, method
 calls, report timers and SIGTERM are per-rank events.  So handlers only QUEUE events;
-every ``sync_every`` module steps all ranks meet at a control boundary, all-gather their
-queues and stop flags (one small object collective) and then apply the union in rank
-order -- rebuilds (weight broadcast), ``benchmark`` (throughput all-reduce), the
-telemetry report (rank 0's clock decides) and shutdown happen on every rank together.
+every ``sync_every`` module steps all ranks meet at a control boundary and exchange their
+queues and stop flags, then apply the union in rank order -- rebuilds (weight
+broadcast), ``benchmark`` (throughput all-reduce), the telemetry report (rank 0's clock
+decides) and shutdown happen on every rank together.  The exchange is kept off the
+inference hot path:
+  * ``sync_every`` = 0 (default) is derived from the measured module-step time so that
+    boundaries are >= ``BOUNDARY_S`` (200 ms) apart; rank 0's value is adopted fleet-wide;
+  * the exchange runs on a CPU gloo group (``parallel.control_group``), never on RCCL or
+    a HIP stream, and is asynchronous with a one-boundary lag: boundary k posts its queue
+    and applies what boundary k-1 posted, so the gather overlaps a whole interval of
+    inference.  A stop vote therefore takes effect one boundary later.
 Methods that need no collective (ping, getStatus) are answered immediately; the others
-reply (``transport.Deferred``) once the boundary has run them.
+reply (``transport.Deferred``) once the boundary has run them.  VM 0's twin (global rank
+0) is the fleet's control point: start() adopts its desired properties, and twin patches
+or collective methods (reconfigure, benchmark) that reach another rank's device are
+rejected with 409, so a patch made on VM i can never silently change, then later revert,
+the whole fleet.
   model "simulated-temperature": the reference demo's CPU-only plumbing workload
              (BASELINE config 1) -- machine/ambient temperature/pressure/humidity.
 """
@@ -44,6 +55,10 @@ from .. import ops, parallel
 from ..utils.logging import get_logger, log_event
 from .config import ModuleConfig
 from .transport import Deferred, Transport, now_iso
+
+BOUNDARY_S = 0.2  # target spacing of lockstep control boundaries (auto sync_every)
+NOT_CONTROL_POINT = ("fleet configuration is controlled by rank 0's twin (VM 0); "
+                     "this device is rank {rank}")
 
 
 class _SimTempModel:
@@ -147,7 +162,10 @@ class ModuleApp:
         self._tick = 0
         self._stop_req = False
         self.sync_every = 1
+        self._since_boundary = 0
         self.boundaries = 0
+        self._xchg = None  # parallel.ObjectExchange at world > 1
+        self._posted_replies: List[Optional[Deferred]] = []
         self._first_inference_stamped = False
         self.log = get_logger("kvedge.module")
         self._gpu = None
@@ -169,22 +187,49 @@ class ModuleApp:
             self.tr.patch_reported({"lastError": f"invalid desired properties: {e}"})
         if self.world > 1:
             # one model config fleet-wide (the weights are rank 0's): adopt rank 0's
-            cfgs = parallel.all_gather_object(self.cfg.to_dict())
+            cfgs = parallel.all_gather_object(self.cfg.to_dict(), group=parallel.control_group())
             if cfgs[0] != self.cfg.to_dict():
                 self.cfg = ModuleConfig(**cfgs[0]).validate()
-        self.sync_every = self.cfg.sync_every or (1 if self.world == 1 else 16)
+            self._xchg = parallel.ObjectExchange()  # async boundary exchange, gloo group
         self._load_state()
         err = self._build_fleet()
         if err is not None:
             log_event(self.log, "start_failed", 40, error=err)
             self.tr.patch_reported({"status": "failed", "lastError": err})
             raise RuntimeError(f"module build failed: {err}")
+        self._set_sync_every()
         log_event(self.log, "started", model=self.cfg.model, batch=self.cfg.batch,
                   world_size=self.world, sync_every=self.sync_every, device=str(self.device),
                   restarts=self.state["restarts"])
         self._report_config()
         self._win_t0 = self._last_report = self.clock()
         return self
+
+    def _module_step_s(self) -> float:
+        """Measured wall time of one module step on this rank (build time, untimed)."""
+        if self.engine is None:
+            return 1e-3  # simulated-temperature: a step is a timer check
+        n = 3
+        dt = self.engine.run_timed(n) / n
+        if self.cfg.native_loop and self.engine.graph is not None and self._hist is not None:
+            dt *= self.cfg.steps_per_poll
+        return max(dt, 1e-6)
+
+    def _set_sync_every(self):
+        """World 1: a boundary every step (no collective).  World > 1: the configured
+        value, or auto = ceil(BOUNDARY_S / step time) with rank 0's measurement adopted
+        by every rank (one blocking gather on the gloo group, at build time only)."""
+        if self.world == 1:
+            self.sync_every = self.cfg.sync_every or 1
+            return
+        if self.cfg.sync_every:
+            self.sync_every = self.cfg.sync_every
+            return
+        import math
+
+        mine = max(1, math.ceil(BOUNDARY_S / self._module_step_s()))
+        self.sync_every = int(parallel.all_gather_object(mine, group=parallel.control_group())[0])
+        log_event(self.log, "sync_every", value=self.sync_every, local_estimate=mine)
 
     def request_stop(self):
         """Signal-safe: the fleet stops together at the next control boundary."""
@@ -277,7 +322,8 @@ class ModuleApp:
             self._build_local()
         except Exception as e:  # noqa: BLE001 -- any build failure must be survivable
             err = f"rank {self.rank}: {type(e).__name__}: {e}"
-        errs = parallel.all_gather_object(err) if self.world > 1 else [err]
+        errs = (parallel.all_gather_object(err, group=parallel.control_group())
+                if self.world > 1 else [err])
         err = next((e for e in errs if e), None)
         if err is not None:
             self.engine = self.model = None
@@ -315,7 +361,9 @@ class ModuleApp:
         elif self.engine is not None:
             self._infer_step()
         self._tick += 1
-        if self._tick % self.sync_every == 0:
+        self._since_boundary += 1
+        if self._since_boundary >= self.sync_every:
+            self._since_boundary = 0
             return self._boundary(want_stop or self._stop_req)
         return False
 
@@ -369,17 +417,54 @@ class ModuleApp:
                     self._stamp("module_first_message")
 
     def _boundary(self, want_stop: bool) -> bool:
-        """Lockstep control boundary (all ranks, same tick)."""
+        """Lockstep control boundary (all ranks, same tick).  World 1: apply this rank's
+        queue now.  World > 1: apply the fleet queue posted at the PREVIOUS boundary
+        (its gather ran asynchronously on the gloo group meanwhile), then post ours."""
         self.boundaries += 1
+        if self._xchg is None:
+            replies, events = self._replies, self._events
+            self._events, self._replies = [], []
+            report_due = (self.engine is not None and
+                          self.clock() - self._last_report >= self.cfg.report_interval_s)
+            fleet = [{"events": events, "stop": bool(want_stop), "report": report_due}]
+            return self._apply_fleet(fleet, replies)
+        stop = False
+        if self._xchg.pending:
+            fleet = self._xchg.wait()
+            replies, self._posted_replies = self._posted_replies, []
+            stop = self._apply_fleet(fleet, replies)
+        # the report flag is computed AFTER applying (a report just ran resets the timer)
         report_due = (self.engine is not None and
                       self.clock() - self._last_report >= self.cfg.report_interval_s)
-        mine = {"events": self._events, "stop": bool(want_stop), "report": report_due}
-        replies, self._events, self._replies = self._replies, [], []
-        fleet = parallel.all_gather_object(mine)
+        events, replies = [], []
+        while self._events:  # as many queued events as fit the fixed exchange slot
+            cand = {"events": events + [self._events[0]], "stop": True, "report": True}
+            if events and not self._xchg.fits(cand):
+                break
+            if not events and not self._xchg.fits(cand):  # a single oversized event
+                self._events.pop(0)
+                d = self._replies.pop(0)
+                if d is not None:
+                    d.resolve(413, {"error": "event too large for the control exchange"})
+                continue
+            events.append(self._events.pop(0))
+            replies.append(self._replies.pop(0))
+        self._xchg.post({"events": events, "stop": bool(want_stop), "report": report_due})
+        self._posted_replies = replies
+        if stop:  # every rank posted at this boundary: drain it so the group is idle
+            self._xchg.wait()
+            for d in self._posted_replies:
+                if d is not None:
+                    d.resolve(503, {"error": "module stopping"})
+            self._posted_replies = []
+        return stop
+
+    def _apply_fleet(self, fleet: List[Dict[str, Any]],
+                     replies: List[Optional[Deferred]]) -> bool:
         for r, part in enumerate(fleet):
             for k, (kind, data) in enumerate(part["events"]):
                 res = self._apply(kind, data)
-                if r == self.rank and replies[k] is not None:
+                if r == self.rank and k < len(replies) and replies[k] is not None:
                     replies[k].resolve(*res)
         if fleet[0]["report"] and self.engine is not None:
             self.report()  # rank 0's clock decides, every rank all-reduces together
@@ -390,11 +475,23 @@ class ModuleApp:
         return stop
 
     def _apply(self, kind: str, data: Any) -> Tuple[int, Dict[str, Any]]:
-        if kind == "twin":
-            return self._apply_patch(data)
-        if kind == "benchmark":
-            return self._benchmark(data)
-        return 404, {"error": f"unknown event {kind}"}
+        """Apply one fleet event.  Never raises: an engine error (HIP OOM in a
+        benchmark, a graph replay failure, a transport error) becomes a 500 reply and
+        the loop -- and the lockstep -- carry on."""
+        try:
+            if kind == "twin":
+                return self._apply_patch(data)
+            if kind == "benchmark":
+                return self._benchmark(data)
+            return 404, {"error": f"unknown event {kind}"}
+        except Exception as e:  # noqa: BLE001
+            self.last_error = f"{kind} failed: {type(e).__name__}: {e}"
+            log_event(self.log, "event_failed", 40, kind=kind, error=self.last_error)
+            try:
+                self.tr.patch_reported({"lastError": self.last_error})
+            except Exception:  # noqa: BLE001
+                pass
+            return 500, {"error": self.last_error}
 
     def run(self, max_steps: Optional[int] = None, duration_s: Optional[float] = None) -> int:
         """Step until this rank wants to stop (max_steps / duration / request_stop) AND
@@ -442,7 +539,7 @@ class ModuleApp:
                "source": self.cfg.source}
         if self.ring is not None:
             msg["frames_dropped"] = self.ring.dropped
-        if self._gpu is not None:
+        if self._gpu is not None and self.rank == 0:  # only rank 0 sends the message
             g = self._gpu.sample()
             if g:
                 msg["gpu"] = g
@@ -475,6 +572,10 @@ class ModuleApp:
     # Handlers run on the module thread from transport.poll(); they only queue work
     # that may involve collectives, to be applied at the next control boundary.
     def on_twin_patch(self, patch: Dict[str, Any]):
+        if self.rank != 0:  # VM 0's twin is the fleet control point
+            self.state["rejected_patches"] += 1
+            self.tr.patch_reported({"lastError": NOT_CONTROL_POINT.format(rank=self.rank)})
+            return
         self._events.append(("twin", dict(patch or {})))
         self._replies.append(None)
 
@@ -497,6 +598,7 @@ class ModuleApp:
             if self.cfg is old:  # rolled back
                 self._report_config()
                 return 409, {"error": self.last_error, "config": self.cfg.to_dict()}
+            self._set_sync_every()  # new step time (every rank, same boundary)
         self._report_config()
         return 200, {"config": self.cfg.to_dict()}
 
@@ -508,13 +610,24 @@ class ModuleApp:
             warm = max(0, int(payload.get("warmup", 3)))
         except (TypeError, ValueError) as e:
             return 400, {"error": f"bad payload: {e}"}
-        for _ in range(warm):
-            self.engine.run()
-        dt = self.engine.run_timed(steps)
-        lat = self.engine.measure_latency(min(steps, 20))
-        ips = steps * self.cfg.batch / dt
-        if self.world > 1:  # every rank is here (same boundary): lockstep all-reduce
-            ips = parallel.allreduce_scalars([ips], op="sum")[0]
+        ips, lat, err = 0.0, None, None
+        try:
+            for _ in range(warm):
+                self.engine.run()
+            dt = self.engine.run_timed(steps)
+            lat = self.engine.measure_latency(min(steps, 20))
+            ips = steps * self.cfg.batch / dt
+        except Exception as e:  # noqa: BLE001
+            err = f"rank {self.rank}: {type(e).__name__}: {e}"
+        if self.world > 1:
+            # every rank is here (same boundary): agree on success first, so either all
+            # ranks all-reduce the throughput or all return the same error together
+            oks = parallel.all_gather_object(err, group=parallel.control_group())
+            err = next((e for e in oks if e), None)
+            if err is None:
+                ips = parallel.allreduce_scalars([ips], op="sum")[0]
+        if err is not None:
+            return 500, {"error": f"benchmark failed: {err}"}
         return 200, {"images_per_s": round(ips, 2), "steps": steps, "world_size": self.world,
                      "batch": self.cfg.batch, "p50_ms": round(lat.percentile(50), 3),
                      "p99_ms": round(lat.percentile(99), 3)}
@@ -529,6 +642,8 @@ class ModuleApp:
                              "last_error": self.last_error, "rank": self.rank,
                              "world_size": self.world}
             if name in ("reconfigure", "benchmark"):
+                if self.rank != 0:
+                    return 409, {"error": NOT_CONTROL_POINT.format(rank=self.rank)}
                 d = Deferred()
                 self._events.append(("twin" if name == "reconfigure" else "benchmark",
                                      dict(payload or {})))

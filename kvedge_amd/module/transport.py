@@ -184,9 +184,20 @@ class StdoutTransport(Transport):
 
 
 class AzureIoTTransport(Transport):
-    """Real edgeHub connection via azure-iot-device (optional dependency)."""
+    """Real edgeHub connection via azure-iot-device (optional dependency; v2 sync API:
+    ``IoTHubModuleClient.create_from_edge_environment``, handler properties, ``Message``,
+    ``MethodResponse.create_from_method_request``).
 
-    def __init__(self):
+    The SDK calls its handlers on its own handler thread; they only enqueue, and
+    ``poll()`` delivers on the module thread, so no callback ever races the GPU loop.
+    The handlers are installed BEFORE ``connect()``: a desired-properties patch or a
+    method request that edgeHub delivers while the connection comes up is queued, not
+    dropped.  Tested against a stub SDK in
+    tests/test_module_cpu.py; parity with the real package stays unpinned (it is not
+    installed in this image).
+    """
+
+    def __init__(self, client=None):
         try:
             from azure.iot.device import IoTHubModuleClient, Message, MethodResponse  # noqa
         except ImportError as e:  # pragma: no cover - not installed in CI
@@ -194,43 +205,56 @@ class AzureIoTTransport(Transport):
                 "azure-iot-device is not installed; install it in the module image or use "
                 "--transport stdout/fake") from e
         self._Message, self._MethodResponse = Message, MethodResponse
-        self.client = IoTHubModuleClient.create_from_edge_environment()
         self._events: "queue.Queue" = queue.Queue()
         self._twin_cb: Optional[TwinHandler] = None
         self._method_cb: Optional[MethodHandler] = None
-
-    def connect(self):  # pragma: no cover
-        self.client.connect()
+        self.client = client or IoTHubModuleClient.create_from_edge_environment()
+        # handlers first: anything edgeHub sends from now on lands in the queue
         self.client.on_twin_desired_properties_patch_received = \
             lambda p: self._events.put(("twin", p))
         self.client.on_method_request_received = lambda r: self._events.put(("method", r))
+        self.connected = False
 
-    def disconnect(self):  # pragma: no cover
-        self.client.shutdown()
+    def connect(self):
+        self.client.connect()
+        self.connected = True
 
-    def get_desired(self):  # pragma: no cover
-        return self.client.get_twin().get("desired", {})
+    def disconnect(self):
+        if self.connected:
+            self.connected = False
+            self.client.shutdown()
 
-    def patch_reported(self, props):  # pragma: no cover
-        self.client.patch_twin_reported_properties(props)
+    def get_desired(self):
+        twin = self.client.get_twin() or {}
+        return {k: v for k, v in dict(twin.get("desired", {})).items()
+                if not k.startswith("$")}  # $version / $metadata are the hub's
 
-    def send_message(self, output, payload):  # pragma: no cover
+    def patch_reported(self, props):
+        self.client.patch_twin_reported_properties(json.loads(json.dumps(props)))
+
+    def send_message(self, output, payload):
         msg = self._Message(json.dumps(payload))
         msg.content_type, msg.content_encoding = "application/json", "utf-8"
         self.client.send_message_to_output(msg, output)
 
-    def poll(self):  # pragma: no cover
+    def _respond(self, req, status: int, res: Dict[str, Any]) -> None:
+        self.client.send_method_response(
+            self._MethodResponse.create_from_method_request(req, status, res))
+
+    def poll(self):
         while True:
             try:
                 kind, data = self._events.get_nowait()
             except queue.Empty:
                 return
             if kind == "twin" and self._twin_cb:
-                self._twin_cb(data)
-            elif kind == "method" and self._method_cb:
+                self._twin_cb({k: v for k, v in dict(data).items() if not k.startswith("$")})
+            elif kind == "method":
+                if self._method_cb is None:
+                    self._respond(data, 503, {"error": "module not ready"})
+                    continue
                 _deliver(self._method_cb(data.name, data.payload or {}),
-                         lambda st, res, req=data: self.client.send_method_response(
-                             self._MethodResponse.create_from_method_request(req, st, res)))
+                         lambda st, res, req=data: self._respond(req, st, res))
 
 
 def make_transport(kind: str, desired: Optional[Dict[str, Any]] = None) -> Transport:

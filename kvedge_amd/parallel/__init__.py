@@ -42,9 +42,35 @@ def info() -> DistInfo:
     return _INFO
 
 
+def _child_preexec():  # pragma: no cover - runs in the forked child
+    """Child side of launch_local: die with the launcher.  PR_SET_PDEATHSIG makes the
+    kernel SIGTERM the rank if the launcher is SIGKILLed (no handler of ours runs then),
+    so no rank can outlive it holding a GPU."""
+    import ctypes
+    import signal
+
+    try:
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM))  # PR_SET_PDEATHSIG
+    except OSError:
+        pass
+
+
+def _pump_prefixed(stream, out, prefix: bytes):
+    """Copy a rank's stderr line by line, each line prefixed with its rank."""
+    try:
+        for line in iter(stream.readline, b""):
+            out.write(prefix + line)
+            out.flush()
+    except (OSError, ValueError):
+        pass
+    finally:
+        stream.close()
+
+
 def launch_local(nproc: int, argv: Sequence[str], env: Optional[dict] = None,
                  timeout_s: Optional[float] = None, node_rank: int = 0, nnodes: int = 1,
-                 master_addr: Optional[str] = None, master_port: Optional[int] = None) -> int:
+                 master_addr: Optional[str] = None, master_port: Optional[int] = None,
+                 grace_s: float = 10.0, prefix_stderr: bool = True) -> int:
     """Per-node launcher (the torchrun role, without its agent): start ``nproc``
     fresh child processes ``python <argv>`` with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set,
     one per GPU, wait for all, return the first non-zero exit code (0 if all passed).
@@ -52,12 +78,24 @@ def launch_local(nproc: int, argv: Sequence[str], env: Optional[dict] = None,
     and every node must be given the same master_addr/port (rank 0's node).
 
     The parent must not have touched the GPU (a process that initialised HIP must not
-    be replaced or fork GPU children); it only counts devices.  If one rank fails, the
-    others would block in their next collective, so the survivors are terminated.
+    be replaced or fork GPU children); it only counts devices.
+
+    Stop paths, all bounded:
+      * one rank exits non-zero -> its peers would block in their next collective until
+        the RCCL timeout, so they get SIGTERM, then SIGKILL after ``grace_s``;
+      * SIGTERM / SIGINT to the launcher (edgeAgent stop: the launcher is the module
+        container's PID 1) -> forwarded to every rank (the module turns it into a fleet
+        stop vote and writes its final report + state file), SIGKILL after ``grace_s``;
+      * ``timeout_s`` -> every rank is SIGTERMed, then SIGKILLed; exit code 124;
+      * the launcher itself SIGKILLed -> the kernel SIGTERMs the ranks (PDEATHSIG).
+    Each rank's stderr is prefixed ``[rank R] ``; stdout passes through unchanged (the
+    bench's one JSON line).
     """
+    import signal
     import socket
     import subprocess
     import sys
+    import threading
     import time
 
     if master_port is None:
@@ -70,36 +108,88 @@ def launch_local(nproc: int, argv: Sequence[str], env: Optional[dict] = None,
     addr = master_addr or "127.0.0.1"
     base = dict(os.environ if env is None else env)
     base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host
-    procs = []
-    for r in range(nproc):
-        e = dict(base, RANK=str(node_rank * nproc + r), LOCAL_RANK=str(r),
-                 WORLD_SIZE=str(nnodes * nproc), LOCAL_WORLD_SIZE=str(nproc),
-                 MASTER_ADDR=addr, MASTER_PORT=str(master_port))
-        procs.append(subprocess.Popen([sys.executable] + list(argv), env=e))
-    rc = 0
-    t_end = None if timeout_s is None else time.monotonic() + timeout_s
-    pending = list(procs)
-    while pending:
-        for p in list(pending):
-            code = p.poll()
-            if code is None:
-                continue
-            pending.remove(p)
-            if code != 0 and rc == 0:
-                rc = code
-                for q in pending:  # peers would hang in their next collective
-                    q.terminate()
-        if t_end is not None and time.monotonic() > t_end:
-            for q in pending:
-                q.kill()
-            rc = rc or 124
-            break
-        time.sleep(0.05)
-    for p in procs:
-        try:
-            p.wait(timeout=30)
-        except subprocess.TimeoutExpired:
-            p.kill()
+    base.setdefault("PYTHONUNBUFFERED", "1")  # prefixed stderr lines arrive as written
+    procs, pumps = [], []
+    got_signal = []
+
+    def _on_signal(signum, _frame):
+        got_signal.append(signum)
+
+    main_thread = threading.current_thread() is threading.main_thread()
+    old = {}
+    if main_thread:
+        for sig in (signal.SIGTERM, signal.SIGINT):
+            old[sig] = signal.signal(sig, _on_signal)
+    try:
+        for r in range(nproc):
+            grank = node_rank * nproc + r
+            e = dict(base, RANK=str(grank), LOCAL_RANK=str(r),
+                     WORLD_SIZE=str(nnodes * nproc), LOCAL_WORLD_SIZE=str(nproc),
+                     MASTER_ADDR=addr, MASTER_PORT=str(master_port))
+            p = subprocess.Popen([sys.executable] + list(argv), env=e,
+                                 stderr=subprocess.PIPE if prefix_stderr else None,
+                                 preexec_fn=_child_preexec)
+            procs.append(p)
+            if prefix_stderr:
+                t = threading.Thread(target=_pump_prefixed, daemon=True,
+                                     args=(p.stderr, sys.stderr.buffer, f"[rank {grank}] ".encode()))
+                t.start()
+                pumps.append(t)
+        rc = 0
+        t_end = None if timeout_s is None else time.monotonic() + timeout_s
+        kill_at = None  # SIGKILL deadline once the survivors were asked to stop
+        pending = list(procs)
+
+        def _stop_all(why: str):
+            nonlocal kill_at
+            if kill_at is None:
+                print(f"[launcher] {why}: stopping {len(pending)} rank(s) "
+                      f"(SIGTERM, SIGKILL after {grace_s:g} s)", file=sys.stderr, flush=True)
+                for q in pending:
+                    try:
+                        q.send_signal(signal.SIGTERM)
+                    except OSError:
+                        pass
+                kill_at = time.monotonic() + grace_s
+
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    if pending:
+                        _stop_all(f"rank {procs.index(p) + node_rank * nproc} exited {code}")
+            if got_signal and kill_at is None:  # rc stays the ranks' own exit codes
+                _stop_all(f"signal {got_signal[0]}")
+            if t_end is not None and time.monotonic() > t_end and kill_at is None:
+                rc = rc or 124
+                _stop_all(f"timeout after {timeout_s:g} s")
+            if kill_at is not None and time.monotonic() > kill_at:
+                for q in pending:
+                    q.kill()
+                for q in pending:
+                    q.wait()
+                pending = []
+                break
+            time.sleep(0.05)
+        for p in procs:
+            try:
+                p.wait(timeout=grace_s)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        for t in pumps:
+            t.join(timeout=2)
+    finally:
+        for p in procs:  # never leave a rank behind, whatever happened above
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        for sig, h in old.items():
+            signal.signal(sig, h)
     return rc if rc >= 0 else 128 - rc
 
 
@@ -213,13 +303,14 @@ def all_gather_vector(vals: Sequence[float]) -> List[List[float]]:
     return [o.cpu().tolist() for o in out]
 
 
-def all_gather_object(obj) -> list:
-    """Gather one small picklable control object per rank (module lockstep boundary:
-    queued twin patches / method calls, stop flags).  Identity at world size 1."""
+def all_gather_object(obj, group=None) -> list:
+    """Gather one small picklable control object per rank (build-time agreement: desired
+    config, build errors, the auto sync interval).  Identity at world size 1.  Pass
+    ``group=control_group()`` to keep it on the CPU gloo group (no HIP stream, no RCCL)."""
     if not is_dist():
         return [obj]
     out = [None] * dist.get_world_size()
-    dist.all_gather_object(out, obj)
+    dist.all_gather_object(out, obj, group=group)
     return out
 
 
@@ -261,3 +352,83 @@ def model_tensors(model) -> List[torch.Tensor]:
     for c in model.convs():
         ts += [c.w, c.b]
     return ts
+
+
+_CTL_GROUP = None
+
+
+def control_group():
+    """CPU (gloo) process group for the module's control plane: lockstep boundary
+    exchanges never touch RCCL or a HIP stream, so they cannot queue behind (or in
+    front of) inference work on the device.  Collective: every rank must call it the
+    first time.  None at world size 1."""
+    global _CTL_GROUP
+    if not is_dist():
+        return None
+    if _CTL_GROUP is None:
+        _CTL_GROUP = dist.new_group(backend="gloo")
+    return _CTL_GROUP
+
+
+class ObjectExchange:
+    """Asynchronous all-gather of one small picklable object per rank over the gloo
+    control group (module lockstep boundary, SURVEY §2.6: collectives off the hot path).
+
+    ``post(obj)`` serialises into a fixed ``capacity``-byte slot and starts a
+    non-blocking all_gather; ``wait()`` returns the per-rank objects.  The module posts
+    at boundary k and waits at boundary k+1, so the exchange overlaps a whole boundary
+    interval of inference instead of stalling the step that reaches the boundary.
+    """
+
+    HEADER = 8
+
+    def __init__(self, capacity: int = 64 << 10, group=None):
+        self.capacity = capacity
+        self.group = group if group is not None else control_group()
+        self.world = dist.get_world_size() if is_dist() else 1
+        self._work = None
+        self._out = None
+        self.posted = 0
+
+    @property
+    def pending(self) -> bool:
+        return self._work is not None or self._out is not None
+
+    def fits(self, obj) -> bool:
+        import pickle
+
+        return len(pickle.dumps(obj, protocol=4)) <= self.capacity - self.HEADER
+
+    def post(self, obj) -> None:
+        import pickle
+
+        if self.pending:
+            raise RuntimeError("ObjectExchange: previous exchange not collected")
+        raw = pickle.dumps(obj, protocol=4)
+        if len(raw) > self.capacity - self.HEADER:
+            raise ValueError(f"control payload {len(raw)} B exceeds {self.capacity} B")
+        buf = torch.zeros(self.capacity, dtype=torch.uint8)
+        buf[:self.HEADER] = torch.tensor(list(len(raw).to_bytes(self.HEADER, "little")),
+                                         dtype=torch.uint8)
+        buf[self.HEADER:self.HEADER + len(raw)] = torch.frombuffer(bytearray(raw),
+                                                                   dtype=torch.uint8)
+        self.posted += 1
+        if self.world == 1:
+            self._out = [buf]
+            return
+        self._out = [torch.empty_like(buf) for _ in range(self.world)]
+        self._work = dist.all_gather(self._out, buf, group=self.group, async_op=True)
+
+    def wait(self) -> list:
+        import pickle
+
+        if not self.pending:
+            raise RuntimeError("ObjectExchange: nothing posted")
+        if self._work is not None:
+            self._work.wait()
+        out, self._work, self._out = self._out, None, None
+        res = []
+        for b in out:
+            n = int.from_bytes(bytes(b[:self.HEADER].tolist()), "little")
+            res.append(pickle.loads(b[self.HEADER:self.HEADER + n].numpy().tobytes()))
+        return res

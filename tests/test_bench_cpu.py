@@ -87,3 +87,97 @@ def test_bench_rejects_bad_gpus():
 def test_bench_refuses_more_gpus_than_visible():
     r = _run_bench(["--gpus", "2"], timeout=300)  # no --cpu; this host sees 0 GPUs
     assert r.returncode == 2 and "GPU(s) visible" in r.stderr
+
+
+def _ranks_alive(marker: str):
+    import psutil
+
+    out = []
+    for p in psutil.process_iter(["pid", "cmdline"]):
+        cl = p.info.get("cmdline") or []
+        if any("bench.py" in c for c in cl) and marker in cl:
+            out.append(p)
+    return out
+
+
+def test_bench_launcher_timeout_kills_hung_rank():
+    """a rank that never arrives (hung RCCL init) must not hang the
+    job.  --launch-timeout bounds it: non-zero exit, every rank gone, stderr prefixed."""
+    import time
+
+    marker = "424242"  # unique --seed value to find our own ranks afterwards
+    t0 = time.monotonic()
+    r = _run_bench(["--cpu", "--gpus", "2", "--steps", "1", "--warmup", "0", "--seed", marker,
+                    "--hang-rank", "1", "--launch-timeout", "15"], timeout=120)
+    assert r.returncode == 124, r.stderr[-3000:]
+    assert time.monotonic() - t0 < 60
+    assert "[launcher] timeout" in r.stderr
+    assert not _ranks_alive(marker)
+
+
+def test_bench_launcher_forwards_sigterm():
+    """SIGTERM to the launcher (driver / edgeAgent stop) reaches every rank; nothing
+    survives the grace period."""
+    import signal
+    import time
+
+    marker = "434343"
+    env = dict(os.environ, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--gpus", "2",
+                          "--steps", "1", "--warmup", "0", "--seed", marker, "--hang-rank", "1"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, cwd=ROOT)
+    try:
+        deadline = time.monotonic() + 60
+        while len(_ranks_alive(marker)) < 3 and time.monotonic() < deadline:
+            time.sleep(0.2)  # launcher + 2 ranks
+        assert len(_ranks_alive(marker)) == 3
+        p.send_signal(signal.SIGTERM)
+        _, err = p.communicate(timeout=40)
+    finally:
+        if p.poll() is None:
+            p.kill()
+    assert p.returncode != 0
+    assert b"[launcher] signal 15" in err
+    time.sleep(0.5)
+    assert not _ranks_alive(marker)
+
+
+def test_launcher_peer_failure_is_bounded(tmp_path):
+    """One rank dies; its peer is stuck in a collective.  The launcher SIGTERMs it and
+    escalates to SIGKILL after the grace period instead of waiting for the gloo/RCCL
+    timeout; each rank's stderr carries its rank prefix."""
+    import time
+
+    from kvedge_amd import parallel
+
+    script = tmp_path / "rank.py"
+    script.write_text(
+        "import os, signal, sys, time\n"
+        "r = int(os.environ['RANK'])\n"
+        "print('hello from', r, file=sys.stderr, flush=True)\n"
+        "if r == 1:\n"
+        "    time.sleep(0.5); sys.exit(7)\n"
+        "signal.signal(signal.SIGTERM, signal.SIG_IGN)  # a rank that ignores SIGTERM\n"
+        "time.sleep(600)\n")
+    import io
+    import contextlib
+
+    buf = io.BytesIO()
+
+    class _Err:
+        buffer = buf
+
+        def write(self, s):
+            buf.write(s.encode())
+
+        def flush(self):
+            pass
+
+    t0 = time.monotonic()
+    with contextlib.redirect_stderr(_Err()):
+        rc = parallel.launch_local(2, [str(script)], grace_s=2.0)
+    assert rc == 7
+    assert time.monotonic() - t0 < 20
+    txt = buf.getvalue().decode()
+    assert "[rank 0] hello from 0" in txt and "[rank 1] hello from 1" in txt

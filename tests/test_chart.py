@@ -404,6 +404,40 @@ def test_multi_vm_dp_wiring():
     assert "NetworkMode" not in json.loads(mod["settings"]["createOptions"])["HostConfig"]
 
 
+def _module_envs(objs):
+    cm = [o for o in by_kind(objs, "ConfigMap") if o["metadata"]["name"].endswith("module-deployment")][0]
+    out = []
+    for k in sorted(cm["data"], key=lambda k: (k != "deployment.json", k)):  # replica order
+        man = json.loads(cm["data"][k])["modulesContent"]
+        mod = man["$edgeAgent"]["properties.desired"]["modules"]["kvedge"]
+        out.append(({k2: v["value"] for k2, v in mod["env"].items()},
+                    man["kvedge"]["properties.desired"]["world_size"]))
+    return out
+
+
+def test_dp_disabled_replicas_are_independent_jobs():
+    """with dp.enabled=false the replicas are independent devices.  No
+    VM may get cross-VM rank env (which would make each module rendezvous as rank i of a
+    world-N job on its own loopback and hang)."""
+    _, objs = render(sets=["replicas=2", "dp.enabled=false"])
+    assert not [o for o in by_kind(objs, "Service") if "rendezvous" in o["metadata"]["name"]]
+    envs = _module_envs(objs)
+    assert len(envs) == 2
+    for env, world in envs:
+        assert "KVEDGE_NODE_RANK" not in env and "KVEDGE_NNODES" not in env
+        assert "MASTER_ADDR" not in env and world == 1
+    # 2 VMs x 4 GPUs, DP off: each VM runs its own 4-rank job on loopback
+    _, objs = render(sets=["replicas=2", "dp.enabled=false", "gpu.count=4"])
+    for env, world in _module_envs(objs):
+        assert env["KVEDGE_NODE_RANK"] == "0" and env["KVEDGE_NNODES"] == "1"
+        assert env["KVEDGE_RANKS_PER_NODE"] == "4" and env["MASTER_ADDR"] == "127.0.0.1"
+        assert "NCCL_SOCKET_IFNAME" not in env and world == 4
+    # DP on with 2 x 4 GPUs: world 8 across VMs
+    _, objs = render(sets=["replicas=2", "gpu.count=4"])
+    for i, (env, world) in enumerate(_module_envs(objs)):
+        assert env["KVEDGE_NODE_RANK"] == str(i) and env["KVEDGE_NNODES"] == "2" and world == 8
+
+
 def test_config_toml_is_git_ignored():
     """Reference .gitignore:1-2 keeps config.toml (IoT Hub connection string) out of git."""
     pats = [ln.strip() for ln in open(os.path.join(ROOT, ".gitignore")) if ln.strip()]

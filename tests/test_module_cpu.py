@@ -149,3 +149,124 @@ def test_failed_rebuild_rolls_back_and_stamps(tmp_path):
     assert app.state["total_images"] == n0 + 4  # still serving
     assert stamps.read_text().count("module_first_inference") == 1
     app.stop()
+
+
+# ------------------------------------------------------------------ stub azure-iot-device
+class _StubSdk:
+    """Minimal stand-in for azure-iot-device's v2 sync API surface the module uses.
+    Records every call in order; a twin patch and a method request are "delivered by
+    edgeHub" DURING connect(), i.e. before the module has finished starting."""
+
+    def __init__(self, desired):
+        import types
+
+        sdk = self
+        self.calls, self.responses, self.sent, self.reported = [], [], [], []
+        self.desired = dict(desired, **{"$version": 7})
+
+        class MethodRequest:
+            def __init__(self, request_id, name, payload):
+                self.request_id, self.name, self.payload = request_id, name, payload
+
+        class Message:
+            def __init__(self, data):
+                self.data, self.content_type, self.content_encoding = data, None, None
+
+        class MethodResponse:
+            def __init__(self, request_id, status, payload):
+                self.request_id, self.status, self.payload = request_id, status, payload
+
+            @classmethod
+            def create_from_method_request(cls, req, status, payload):
+                return cls(req.request_id, status, payload)
+
+        class IoTHubModuleClient:
+            def __init__(self):
+                self.on_twin_desired_properties_patch_received = None
+                self.on_method_request_received = None
+
+            @classmethod
+            def create_from_edge_environment(cls):
+                sdk.calls.append("create_from_edge_environment")
+                sdk.client = cls()
+                return sdk.client
+
+            def connect(self):
+                sdk.calls.append(("connect",
+                                  self.on_twin_desired_properties_patch_received is not None,
+                                  self.on_method_request_received is not None))
+                # edgeHub pushes these while the connection is coming up
+                if self.on_twin_desired_properties_patch_received:
+                    self.on_twin_desired_properties_patch_received(
+                        {"report_interval_s": 0.5, "$version": 8})
+                if self.on_method_request_received:
+                    self.on_method_request_received(
+                        MethodRequest("r1", "benchmark", {"steps": 1, "warmup": 0}))
+
+            def shutdown(self):
+                sdk.calls.append("shutdown")
+
+            def get_twin(self):
+                sdk.calls.append("get_twin")
+                return {"desired": dict(sdk.desired), "reported": {}}
+
+            def patch_twin_reported_properties(self, props):
+                json.dumps(props)  # must be JSON-serialisable
+                sdk.reported.append(props)
+
+            def send_message_to_output(self, msg, output):
+                sdk.sent.append((output, msg))
+
+            def send_method_response(self, resp):
+                sdk.responses.append(resp)
+
+        self.MethodRequest = MethodRequest
+        dev = types.ModuleType("azure.iot.device")
+        dev.IoTHubModuleClient, dev.Message, dev.MethodResponse = \
+            IoTHubModuleClient, Message, MethodResponse
+        dev.MethodRequest = MethodRequest
+        self.modules = {"azure": types.ModuleType("azure"),
+                        "azure.iot": types.ModuleType("azure.iot"), "azure.iot.device": dev}
+
+
+def test_azure_transport_against_stub_sdk(tmp_path, monkeypatch):
+    """the production transport runs end to end through a
+    stub ``azure.iot.device``: handlers registered before connect (the patch and method
+    sent during connect are not lost), desired twin ($version stripped) -> config,
+    deferred ``benchmark`` reply via MethodResponse.create_from_method_request,
+    telemetry via send_message_to_output with a JSON content type.  Parity with the
+    real SDK is unpinned (the package is not installed in this image)."""
+    import sys
+
+    from kvedge_amd.module.transport import make_transport
+
+    sdk = _StubSdk({"model": "resnet50", "batch": 1, "image_size": 64,
+                    "report_interval_s": 1000})
+    for k, m in sdk.modules.items():
+        monkeypatch.setitem(sys.modules, k, m)
+    tr = make_transport("azure")
+    app = ModuleApp(tr, device="cpu", state_path=str(tmp_path / "s.json"), clock=Clock()).start()
+    assert sdk.calls[0] == "create_from_edge_environment"
+    assert sdk.calls[1] == ("connect", True, True)  # handlers were already installed
+    assert app.cfg.batch == 1 and app.cfg.image_size == 64
+    # the deferred method arrived during connect: answered at the first boundary
+    app.run(max_steps=3)
+    resp = {r.request_id: r for r in sdk.responses}
+    assert resp["r1"].status == 200 and resp["r1"].payload["images_per_s"] > 0
+    # the patch sent during connect was applied ($version never reaches the config)
+    assert app.cfg.report_interval_s == 0.5
+    tel = [(o, m) for o, m in sdk.sent if o == "telemetry"]
+    assert tel, "telemetry expected after the 0.5 s report interval"
+    out, msg = tel[-1]
+    assert msg.content_type == "application/json" and msg.content_encoding == "utf-8"
+    body = json.loads(msg.data)
+    assert body["model"] == "resnet50" and body["images_per_s"] > 0
+    assert any(r.get("status") == "running" for r in sdk.reported)
+    # a later method through the SDK's handler thread path; unknown -> 404
+    sdk.client.on_method_request_received(sdk.MethodRequest("r2", "nope", None))
+    sdk.client.on_method_request_received(sdk.MethodRequest("r3", "ping", {}))
+    app.run(max_steps=1)
+    resp = {r.request_id: r for r in sdk.responses}
+    assert resp["r2"].status == 404 and resp["r3"].status == 200
+    app.stop()
+    assert sdk.calls[-1] == "shutdown"

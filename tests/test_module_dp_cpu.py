@@ -63,10 +63,13 @@ def _worker(rank, world, port, q, tmp):
             return self.t
 
     script = {}
-    if rank == 2:
+    if rank == 0:  # VM 0's twin is the fleet control point
         script = {3: [("method", "benchmark", {"steps": 1, "warmup": 0}),
                       ("twin", {"batch": 2})],
                   7: [("method", "reconfigure", {"batch": 3})]}
+    if rank == 2:  # another device's twin / methods: rejected, never fleet-wide
+        script = {3: [("twin", {"batch": 5}), ("method", "reconfigure", {"batch": 6}),
+                      ("method", "ping", {})]}
     tr = Scripted({"model": "resnet50", "batch": 1, "image_size": 64,
                    "report_interval_s": 0.5}, script)
     cfg = ModuleConfig(world_size=world, sync_every=2, use_graph=False)
@@ -110,15 +113,21 @@ def test_module_lockstep_4_ranks(tmp_path):
     steps = {r[1] for r in res}
     assert len(steps) == 1, f"ranks left the loop at different steps: {res}"
     n = steps.pop()
-    assert n == 10  # rank 1 voted to stop at step 10: everyone left at that boundary
-    # every rank applied rank 2's batch patch, and rolled back the failing batch=3 together
+    # rank 1 voted to stop at step 10 (boundary 5); the exchange runs with a one-boundary
+    # lag, so the fleet applies the vote, and leaves, together at boundary 6
+    assert n == 12
+    # every rank applied rank 0's batch patch, and rolled back the failing batch=3 together
     assert [r[2] for r in res] == [2] * WORLD
     assert all(r[4] == 2 and r[5] == 1 for r in res)
     assert all(r[3] == n // 2 for r in res)
+    r0 = res[0][6]
+    assert r0["benchmark"][0] == 200 and r0["benchmark"][1]["world_size"] == WORLD
+    assert r0["reconfigure"][0] == 409 and "injected" in r0["reconfigure"][1]["error"]
+    assert all("rolled back" in r[7] for r in res if r[0] != 2)
+    # rank 2's own twin patch and reconfigure were refused (409), ping still answered
     r2 = res[2][6]
-    assert r2["benchmark"][0] == 200 and r2["benchmark"][1]["world_size"] == WORLD
-    assert r2["reconfigure"][0] == 409 and "injected" in r2["reconfigure"][1]["error"]
-    assert all("rolled back" in r[7] for r in res)
+    assert r2["reconfigure"][0] == 409 and "rank 0's twin" in r2["reconfigure"][1]["error"]
+    assert r2["ping"][0] == 200
     # only rank 0 emits telemetry (job totals)
     assert res[0][8] >= 1 and all(r[8] == 0 for r in res[1:])
 
@@ -171,3 +180,69 @@ def test_module_cli_topologies(tmp_path):
     assert tel0 and tel0[-1]["world_size"] == 2 and not tel1
     assert open(os.path.join(str(tmp_path), "stamps-b1")).read().startswith(
         "module_first_inference ")
+
+
+def _sync_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    torch.set_num_threads(1)
+    from kvedge_amd import parallel
+    from kvedge_amd.module.app import ModuleApp
+    from kvedge_amd.module.config import ModuleConfig
+    from kvedge_amd.module.transport import FakeTransport
+
+    parallel.init_from_env(prefer_gpu=False)
+    tr = FakeTransport({"model": "resnet50", "batch": 1, "image_size": 64,
+                        "report_interval_s": 1e9})
+    app = ModuleApp(tr, ModuleConfig(world_size=world, sync_every=0, use_graph=False),
+                    device="cpu")
+    # measured module-step time: 10 ms on rank 0, 50 ms on rank 1 -> rank 0's 20 wins
+    app._module_step_s = lambda: 0.010 if rank == 0 else 0.050
+    try:
+        app.start()
+        calls = []
+        real_ag = dist.all_gather
+
+        def spy_all_gather(out, t, group=None, async_op=False):
+            calls.append((group is parallel.control_group(), async_op, t.device.type))
+            return real_ag(out, t, group=group, async_op=async_op)
+
+        def forbidden(*a, **k):
+            raise AssertionError("blocking collective on the hot path")
+
+        dist.all_gather = spy_all_gather
+        dist.all_reduce = dist.broadcast = dist.all_gather_object = forbidden
+        try:
+            n = app.run(max_steps=100)
+        finally:
+            dist.all_gather = real_ag
+        q.put((rank, app.sync_every, app.boundaries, n, calls))
+    finally:
+        parallel.shutdown()
+
+
+@pytest.mark.timeout(300)
+def test_module_auto_sync_every_async_boundaries():
+    """boundaries are spaced by measured step time (>= 200 ms: 10 ms
+    steps -> every 20 steps, rank 0's measurement adopted by all), and the boundary
+    exchange is an ASYNC all_gather on the CPU gloo control group -- no blocking
+    collective, nothing on RCCL or a HIP stream, during the serving loop."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sync_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=250) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, sync_every, boundaries, n, calls in res:
+        assert sync_every == 20
+        # stop voted at step 100 (boundary 5), applied one boundary later
+        assert n == 120 and boundaries == 6
+        assert len(calls) == boundaries
+        assert all(c == (True, True, "cpu") for c in calls), calls
