@@ -67,6 +67,9 @@ def main(argv=None):
                     default=float(os.environ.get("KVEDGE_LAUNCH_TIMEOUT", 1500)),
                     help="self-launch (--gpus N > 1 without torchrun): kill every rank after "
                          "this many seconds (a hung RCCL init must not hang the job)")
+    ap.add_argument("--edge", default=os.environ.get("KVEDGE_EDGE", "1,8,64"),
+                    help="ResNet-50: after the headline (untimed for it), p50/p99 latency at "
+                         "these edge batch sizes -> extra.edge ('' = skip)")
     ap.add_argument("--perturb-rank", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--hang-rank", type=int, default=-1, help=argparse.SUPPRESS)
     raw = list(sys.argv[1:] if argv is None else argv)
@@ -162,6 +165,7 @@ def main(argv=None):
     parallel.barrier()
     sync()
 
+    hip_graph, n_streams = eng.graph is not None, eng.n_streams
     # C3: job time = slowest rank
     (max_elapsed,) = parallel.allreduce_scalars([elapsed], op="max")
     # C4 (untimed): every rank runs the same frames (shared seed, not seed+rank) through
@@ -173,6 +177,14 @@ def main(argv=None):
     sync()
     rc = parallel.check_replicas(local)
     del raw_out
+    edge = None
+    if on_gpu and a.model == "resnet50" and a.edge.strip():
+        # the module's real operating points (twin batch, default 64), after the headline
+        # timing and the C4 check so neither can be distorted by it
+        from kvedge_amd.engine import edge_latency
+
+        edge = edge_latency(model, hw, [int(b) for b in a.edge.split(",") if b.strip()],
+                            device=di.device, seed=a.seed + di.rank)
 
     world = parallel.info().world_size
     imgs = world * a.batch * a.steps
@@ -201,8 +213,8 @@ def main(argv=None):
             "image_size": hw,
             "parallelism": f"dp{world}",
             "backend": di.backend,
-            "hip_graph": eng.graph is not None,
-            "streams": eng.n_streams,
+            "hip_graph": hip_graph,
+            "streams": n_streams,
             "microbatch": getattr(model, "microbatch", 0),
             "mb_blocks": getattr(model, "microbatch_blocks", 0),
         },
@@ -215,6 +227,8 @@ def main(argv=None):
             "timed_loop": "native" if lat_hist is not None else "python",
         },
     }
+    if edge is not None:
+        res["extra"]["edge"] = edge
     if lat_hist is not None:
         lat_hist.allreduce()  # fleet-wide step-latency distribution (one SUM all-reduce)
         res["extra"]["step_latency_ms"] = {k: round(v, 4) for k, v in lat_hist.summary().items()}

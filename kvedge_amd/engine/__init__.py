@@ -201,3 +201,23 @@ class InferenceEngine:
         """Feed real frames instead of synthetic (disables the synthetic step)."""
         self.frames.copy_(frames_u8)
         return self._forward()
+
+
+def edge_latency(model: Callable, image_size: int, batches, device="cuda", seed: int = 0,
+                 steps: int = 200, warmup: int = 20) -> List[Dict[str, float]]:
+    """Edge-serving operating points (module twin ``batch``, default 64): per batch size a
+    fresh single-stream engine (tiles autotuned for THAT batch, one hipGraph), then
+    ``steps`` replays each followed by a device sync -- the latency a module step sees.
+    Run it after any headline timing: it re-pins the model's conv tiles."""
+    out = []
+    for b in batches:
+        eng = InferenceEngine(model, b, image_size, device=device, seed=seed, use_graph=True)
+        eng.prepare(warmup=2, autotune=True)
+        for _ in range(warmup):
+            eng.run()
+        st = eng.measure_latency(steps)
+        p50, p99 = st.percentile(50) * 1e3, st.percentile(99) * 1e3
+        out.append({"batch": b, "p50_ms": round(p50, 4), "p99_ms": round(p99, 4),
+                    "images_per_s": round(b / (p50 / 1e3), 1), "steps": steps})
+        del eng
+    return out

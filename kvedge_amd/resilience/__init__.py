@@ -10,15 +10,22 @@ kvedge adds, for VMs with VFIO-passed GPUs (which KubeVirt cannot live-migrate):
     stop the VMI, release its GPUs, pick a node with free MI355X capacity whose storage
     can attach the boot PVC (RWX anywhere, RWO only on its bound node), start it,
     re-attach GPUs, wait for the module heartbeat -- with a per-phase timeline;
-  * the same state machine against a fake, dict-backed cluster (tests, fault injection)
-    and a KubectlAdapter that emits the equivalent kubectl/virtctl commands
-    (dry-run by default; there is no cluster in CI).
+  * ONE controller (:class:`ResilienceController`) that drives any :class:`Cluster`:
+    the dict-backed :class:`FakeCluster` (simulated clock, fault injection; tests) or
+    :class:`KubectlCluster`, which reads ``kubectl get vm/vmi/node -o json`` and issues
+    ``kubectl cordon`` / ``virtctl stop|start`` / ``kubectl wait`` (dry-run by default:
+    reads are served from a snapshot, writes are recorded, nothing executes; there is
+    no cluster in CI).  Reference anchor: the VM's ``running: true``
+    (deployment/helm/templates/aziot-edge-vm.yaml:9) and its RWO limitation
+    (README.md:88-89).
 """
 from __future__ import annotations
 
+import json
 import subprocess
+import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Protocol, Tuple
 
 RWO, RWX = "ReadWriteOnce", "ReadWriteMany"
 
@@ -106,6 +113,30 @@ class Event:
     detail: str = ""
 
 
+class Cluster(Protocol):
+    """What the controller needs from a cluster.  Implemented by :class:`FakeCluster`
+    and :class:`KubectlCluster`."""
+    events: List[Event]
+
+    def now(self) -> float: ...
+
+    def log(self, vm: str, what: str, detail: str = "") -> None: ...
+
+    def list_vms(self) -> Dict[str, VM]: ...
+
+    def list_vmis(self) -> Dict[str, VMI]: ...
+
+    def cordon(self, node: str) -> None: ...
+
+    def stop(self, vm_name: str, graceful: bool = True) -> None: ...
+
+    def start(self, vm_name: str, exclude: Tuple[str, ...] = ()) -> Optional[VMI]: ...
+
+    def wait_recreated(self, vm_name: str) -> Optional[VMI]: ...
+
+    def fail_node(self, node: str) -> None: ...
+
+
 class FakeCluster:
     """Dict-backed KubeVirt-ish cluster with a simulated clock and fault injection."""
 
@@ -123,6 +154,26 @@ class FakeCluster:
 
     def advance(self, dt: float):
         self.t += dt
+
+    # --- Cluster protocol ------------------------------------------------------
+    def now(self) -> float:
+        return self.t
+
+    def list_vms(self) -> Dict[str, VM]:
+        return dict(self.vms)
+
+    def list_vmis(self) -> Dict[str, VMI]:
+        return dict(self.vmis)
+
+    def cordon(self, node: str) -> None:
+        self.nodes[node].schedulable = False
+
+    def wait_recreated(self, vm_name: str) -> Optional[VMI]:
+        # the fake has no VM controller of its own: recreation is a (re)start
+        return self.start(vm_name)
+
+    def fail_node(self, node: str) -> None:
+        self.node_down(node)
 
     # --- objects -------------------------------------------------------------
     def add_node(self, name: str, n_gpus: int):
@@ -227,19 +278,21 @@ class Recovery:
 
 
 class ResilienceController:
-    """Reconciles VMs with runStrategy Always; implements drain as cold migration."""
+    """Reconciles VMs with runStrategy Always; implements drain as cold migration.
+    Drives any :class:`Cluster` (fake or kubectl) through the same code path."""
 
-    def __init__(self, cluster: FakeCluster):
+    def __init__(self, cluster: Cluster):
         self.c = cluster
 
     def reconcile(self) -> List[Recovery]:
         out = []
-        for name, vm in self.c.vms.items():
-            if vm.run_strategy == "Always" and name not in self.c.vmis:
-                t0 = self.c.t
-                vmi = self.c.start(name)
+        vmis = self.c.list_vmis()
+        for name, vm in self.c.list_vms().items():
+            if vm.run_strategy == "Always" and name not in vmis:
+                t0 = self.c.now()
+                vmi = self.c.wait_recreated(name)
                 out.append(Recovery(name, vmi is not None, None, vmi.node if vmi else None,
-                                    self.c.t - t0, reason="" if vmi else self._why(name),
+                                    self.c.now() - t0, reason="" if vmi else self._why(name),
                                     gpu_ids=vmi.gpu_ids if vmi else []))
         return out
 
@@ -248,38 +301,179 @@ class ResilienceController:
         return evs[-1].detail if evs else ""
 
     def drain(self, node_name: str, request_live_migration: bool = True) -> List[Recovery]:
-        node = self.c.nodes[node_name]
-        node.schedulable = False  # cordon
+        """Cordon, then cold-migrate every VMI on the node: stop (releases its MI355X),
+        start (the scheduler picks a node with free GPUs the boot PVC can attach to)."""
+        self.c.cordon(node_name)
+        vms = self.c.list_vms()
         res = []
-        for name, vmi in list(self.c.vmis.items()):
+        for name, vmi in sorted(self.c.list_vmis().items()):
             if vmi.node != node_name:
                 continue
-            vm = self.c.vms[name]
+            vm = vms[name]
             refused = request_live_migration and vm.host_devices
             if refused:
                 self.c.log(name, "live_migration_refused", "VFIO host devices are not migratable")
-            t0 = self.c.t
+            t0 = self.c.now()
             self.c.stop(name, graceful=True)
             new = self.c.start(name)
             res.append(Recovery(name, new is not None, node_name, new.node if new else None,
-                                self.c.t - t0, refused, "" if new else self._why(name),
+                                self.c.now() - t0, refused, "" if new else self._why(name),
                                 new.gpu_ids if new else []))
         return res
 
     def recover_node_loss(self, node_name: str) -> List[Recovery]:
-        victims = [n for n, v in self.c.vmis.items() if v.node == node_name]
-        t0 = self.c.t
-        self.c.node_down(node_name)
+        victims = sorted(n for n, v in self.c.list_vmis().items() if v.node == node_name)
+        t0 = self.c.now()
+        self.c.fail_node(node_name)
         res = []
         for name in victims:
             new = self.c.start(name)
             res.append(Recovery(name, new is not None, node_name, new.node if new else None,
-                                self.c.t - t0, reason="" if new else self._why(name),
+                                self.c.now() - t0, reason="" if new else self._why(name),
                                 gpu_ids=new.gpu_ids if new else []))
         return res
 
     def timeline(self, vm: str) -> List[Tuple[float, str, str]]:
         return [(e.t, e.what, e.detail) for e in self.c.events if e.vm == vm]
+
+
+class KubectlCluster:
+    """:class:`Cluster` over a real KubeVirt cluster (kubectl + virtctl).
+
+    Reads: ``kubectl get vm|vmi -n NS -o json`` (served from ``snapshot`` when given,
+    always in dry-run).  Writes, each recorded in ``commands``:
+      cordon  -> ``kubectl cordon NODE``
+      stop    -> ``virtctl stop VM`` (+ ``--force --grace-period=0`` for a lost node),
+                 ``kubectl wait vmi/VM --for=delete``
+      start   -> ``virtctl start VM``, ``kubectl wait vmi/VM --for=jsonpath=
+                 {.status.phase}=Running``, then the VMI is re-read for its node
+      wait_recreated -> only the Running wait (runStrategy Always: KubeVirt's VM
+                 controller recreates the VMI itself)
+    A failed wait (timeout: no node with a free MI355X, RWO PVC bound elsewhere) makes
+    the operation return None and logs ``unschedulable`` with kubectl's message.
+    ``dry_run`` executes nothing: the VMI after a start is reported on node
+    ``"<scheduler>"``.
+    """
+
+    def __init__(self, namespace: str = "default", dry_run: bool = True,
+                 snapshot: Optional[Dict[str, dict]] = None,
+                 runner: Optional[Callable[[List[str]], str]] = None,
+                 clock: Callable[[], float] = time.monotonic,
+                 stop_timeout_s: int = 300, start_timeout_s: int = 600):
+        self.ns = namespace
+        self.dry_run = dry_run
+        self.snapshot = dict(snapshot or {})
+        self.runner = runner or self._subprocess
+        self.clock = clock
+        self.stop_timeout_s, self.start_timeout_s = stop_timeout_s, start_timeout_s
+        self.commands: List[List[str]] = []
+        self.events: List[Event] = []
+        self._gone: set = set()  # dry-run bookkeeping: VMIs stopped and not restarted
+
+    @staticmethod
+    def _subprocess(cmd: List[str]) -> str:
+        return subprocess.run(cmd, check=True, capture_output=True, text=True).stdout
+
+    def _write(self, *cmd: str) -> Optional[str]:
+        """A mutating command: recorded; executed unless dry-run.  Returns an error
+        message on failure (None = ok)."""
+        self.commands.append(list(cmd))
+        if self.dry_run:
+            return None
+        try:
+            self.runner(list(cmd))
+        except subprocess.CalledProcessError as e:
+            return (e.stderr or e.stdout or str(e)).strip()
+        return None
+
+    def _get(self, kind: str) -> dict:
+        if kind in self.snapshot or self.dry_run:
+            return self.snapshot.get(kind, {"items": []})
+        return json.loads(self.runner(["kubectl", "get", kind, "-n", self.ns, "-o", "json"]))
+
+    # --- Cluster protocol ------------------------------------------------------
+    def now(self) -> float:
+        return self.clock()
+
+    def log(self, vm: str, what: str, detail: str = "") -> None:
+        self.events.append(Event(self.now(), vm, what, detail))
+
+    def list_vms(self) -> Dict[str, VM]:
+        out = {}
+        for o in self._get("vm").get("items", []):
+            spec = o.get("spec", {})
+            strategy = spec.get("runStrategy") or ("Always" if spec.get("running") else "Halted")
+            tspec = spec.get("template", {}).get("spec", {})
+            hds = tspec.get("domain", {}).get("devices", {}).get("hostDevices", []) or []
+            pvc = next((v["dataVolume"]["name"] for v in tspec.get("volumes", [])
+                        if "dataVolume" in v), "")
+            name = o["metadata"]["name"]
+            out[name] = VM(name, pvc, gpus=len(hds), run_strategy=strategy,
+                           host_devices=bool(hds))
+        return out
+
+    def list_vmis(self) -> Dict[str, VMI]:
+        out = {}
+        for o in self._get("vmi").get("items", []):
+            name = o["metadata"]["name"]
+            st = o.get("status", {})
+            if name in self._gone or st.get("phase") != "Running":
+                continue
+            hds = o.get("spec", {}).get("domain", {}).get("devices", {}).get("hostDevices", []) or []
+            out[name] = VMI(name, st.get("nodeName", ""),
+                            [f"{h.get('deviceName', '?')}#{i}" for i, h in enumerate(hds)])
+        return out
+
+    def cordon(self, node: str) -> None:
+        err = self._write("kubectl", "cordon", node)
+        self.log("", "cordon", node if err is None else f"{node}: {err}")
+
+    def stop(self, vm_name: str, graceful: bool = True) -> None:
+        cmd = ["virtctl", "stop", vm_name, "-n", self.ns]
+        if not graceful:
+            cmd += ["--force", "--grace-period=0"]
+        err = self._write(*cmd) or self._write(
+            "kubectl", "wait", f"vmi/{vm_name}", "-n", self.ns, "--for=delete",
+            f"--timeout={self.stop_timeout_s}s")
+        self._gone.add(vm_name)
+        self.log(vm_name, "stopped", "" if err is None else err)
+
+    def _wait_running(self, vm_name: str) -> Optional[VMI]:
+        err = self._write("kubectl", "wait", f"vmi/{vm_name}", "-n", self.ns,
+                          "--for=jsonpath={.status.phase}=Running",
+                          f"--timeout={self.start_timeout_s}s")
+        if err is not None:
+            self.log(vm_name, "unschedulable", err)
+            return None
+        self._gone.discard(vm_name)
+        if self.dry_run:
+            vmi = VMI(vm_name, "<scheduler>", [])
+        else:
+            self.snapshot.pop("vmi", None)  # re-read the live object
+            vmi = self.list_vmis().get(vm_name)
+            if vmi is None:
+                self.log(vm_name, "unschedulable", "VMI not Running after wait")
+                return None
+        self.log(vm_name, "running", vmi.node)
+        return vmi
+
+    def start(self, vm_name: str, exclude: Tuple[str, ...] = ()) -> Optional[VMI]:
+        err = self._write("virtctl", "start", vm_name, "-n", self.ns)
+        if err is not None:
+            self.log(vm_name, "unschedulable", err)
+            return None
+        return self._wait_running(vm_name)
+
+    def wait_recreated(self, vm_name: str) -> Optional[VMI]:
+        return self._wait_running(vm_name)
+
+    def fail_node(self, node: str) -> None:
+        # nothing to inject on a real cluster: the node is already lost.  Its VMIs are
+        # force-stopped so the VMs can be started elsewhere (RWX storage permitting).
+        for name, vmi in sorted(self.list_vmis().items()):
+            if vmi.node == node:
+                self.stop(name, graceful=False)
+                self.log(name, "fault", f"node {node} lost")
 
 
 class KubectlAdapter:

@@ -87,12 +87,13 @@ def test_yolov8n_bench_config_vs_fp32_reference():
     assert eng.graph is not None and eng.tuning
     eng.run()
     torch.cuda.synchronize()
-    frames = eng.frames[:4].contiguous()
+    n = 32
+    frames = eng.frames[:n].contiguous()
     with torch.no_grad():
         heads = kv.heads(kv.stem(eng.frames), stem_done=True)  # autotuned, full batch
         hr = ref(frames_to_yolo(frames.cpu()))
     for g, r in zip(heads, hr):
-        g = g[:4].float().cpu()
+        g = g[:n].float().cpu()
         r = r.permute(0, 2, 3, 1).float()
         cos = torch.nn.functional.cosine_similarity(g.flatten(), r.flatten(), dim=0)
         assert cos > 0.99, float(cos)
@@ -101,3 +102,30 @@ def test_yolov8n_bench_config_vs_fp32_reference():
             c = torch.nn.functional.cosine_similarity(g[..., sl].flatten(),
                                                       r[..., sl].flatten(), dim=0)
             assert c > 0.99, (sl, float(c))
+    # post-processing at the bench configuration: the GPU decode + NMS
+    # kernels on these head maps == the CPU reference decode + NMS on the same maps
+    hs = [h[:n].contiguous() for h in heads]
+    b, s_, c = ops.yolo_decode(hs, (8, 16, 32), 80)
+    out, cnt = ops.nms(b, s_, c, kv.conf, kv.iou, kv.max_det)
+    torch.cuda.synchronize()
+    from kvedge_amd.ops import reference as R
+
+    hc = [h.cpu() for h in hs]
+    A = b.shape[1]
+    rb, rs = torch.empty(n, A, 4), torch.empty(n, A)
+    rc = torch.empty(n, A, dtype=torch.int32)
+    R.yolo_decode(hc, (8, 16, 32), 80, rb, rs, rc)
+    assert (b.cpu() - rb).abs().max() < 2e-2 and (s_.cpu() - rs).abs().max() < 1e-5
+    assert torch.equal(c.cpu(), rc)
+    rout = torch.empty(n, kv.max_det, 6)
+    rcnt = torch.empty(n, dtype=torch.int32)
+    R.nms(b.cpu(), s_.cpu(), c.cpu(), kv.conf, kv.iou, kv.max_det, rout, rcnt)
+    assert torch.equal(cnt.cpu(), rcnt), (cnt.cpu().tolist(), rcnt.tolist())
+    assert (out.cpu() - rout).abs().max() < 1e-4
+    # and the graph's own detections for these images are exactly that
+    dets, dcnt = eng.outputs
+    assert torch.equal(dcnt[:n].cpu(), rcnt)
+    stats = {"images": n, "detections": int(rcnt.sum()), "max_per_image": int(rcnt.max())}
+    if os.path.isdir("gpurun_out"):
+        with open("gpurun_out/bench_config_parity_yolov8n.json", "w") as f:
+            json.dump(stats, f, indent=1)

@@ -30,9 +30,11 @@ def _inputs(N, H, W, nt, dual, seed):
 
 
 def _close(got, ref, what):
-    err = (got.float() - ref.float()).abs().max().item()
-    scale = ref.float().abs().max().item()
-    assert err <= 0.02 * scale + 0.02, (what, err, scale)
+    got, ref = got.float(), ref.float()
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    rr = ((got - ref).pow(2).mean().sqrt() / ref.pow(2).mean().sqrt().clamp_min(1e-12)).item()
+    assert err <= 0.02 * scale and rr <= 4e-3, (what, err, scale, rr)
 
 
 @pytest.mark.parametrize("dual", [False, True])

@@ -18,6 +18,24 @@ def _native():
     assert ops.load(), "native kvedge library must be loaded on the GPU box"
 
 
+RRMS_TOL = 4e-3  # rms(err) / rms(ref): ~2-3x the two sides' independent bf16 output rounding
+
+
+def _rrms(got, ref) -> float:
+    """Relative RMS error: a dropped K chunk or a wrong tap moves every element, which
+    this sees even when one large output makes the max bound loose (VERDICT r2 weak #9)."""
+    got, ref = got.float(), ref.float()
+    return ((got - ref).pow(2).mean().sqrt() / ref.pow(2).mean().sqrt().clamp_min(1e-12)).item()
+
+
+def _assert_close(got, ref, ctx=None):
+    got, ref = got.float(), ref.float()
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    rr = _rrms(got, ref)
+    assert err <= 0.02 * scale and rr <= RRMS_TOL, (ctx, err, scale, rr)
+
+
 def _rand(shape, seed, scale=1.0):
     g = torch.Generator().manual_seed(seed)
     return (torch.randn(shape, generator=g) * scale).to(torch.bfloat16)
@@ -48,6 +66,9 @@ def _conv_case(N, H, W, cin, cout, k, stride, pad, act, res=False, ldx_extra=0, 
     orf = out_ref.float()
     err = (og - orf).abs().max().item()
     scale = orf.abs().max().item() + 1e-6
+    sl = slice(y_coff, y_coff + cout)
+    rr = _rrms(og[..., sl], orf[..., sl])
+    assert rr <= RRMS_TOL, ("relative rms", rr)
     # untouched channels outside the output slice must stay zero
     if ldy_extra:
         mask = torch.ones(ldy, dtype=torch.bool)
@@ -73,13 +94,13 @@ def _conv_case(N, H, W, cin, cout, k, stride, pad, act, res=False, ldx_extra=0, 
 ])
 def test_conv_vs_reference(case):
     err, scale = _conv_case(*case)
-    assert err <= 0.02 * scale + 0.02, (case, err, scale)
+    assert err <= 0.02 * scale, (case, err, scale)
 
 
 def test_conv_residual_and_slices():
     err, scale = _conv_case(2, 28, 28, 64, 128, 3, 1, 1, ops.ACT_RELU, res=True, ldx_extra=64,
                             x_coff=32, ldy_extra=64, y_coff=32)
-    assert err <= 0.02 * scale + 0.02
+    assert err <= 0.02 * scale
 
 
 N_TILES = 68  # v1 register-staged (0-5) + v2 LDS-DMA (6-31) + v3 streaming (32-53) + v4 direct (54-57)
@@ -134,7 +155,7 @@ def test_conv_every_tile(tile, case):
                                     x_coff=xc, tile=tile)
         except RuntimeError:
             return
-        assert err <= 0.02 * scale + 0.02, (tile, case, err, scale)
+        assert err <= 0.02 * scale, (tile, case, err, scale)
         return
     if tile >= STREAM0 and (k != 1 or s != 1 or not _stream_fits(tile, (cin * k * k + 63) // 64 * 64, res)):
         with pytest.raises(RuntimeError):
@@ -143,7 +164,7 @@ def test_conv_every_tile(tile, case):
         return
     err, scale = _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
                             tile=tile)
-    assert err <= 0.02 * scale + 0.02, (tile, case, err, scale)
+    assert err <= 0.02 * scale, (tile, case, err, scale)
 
 
 @pytest.mark.parametrize("tile", [-1] + list(range(STREAM0, DIRECT0)))
@@ -166,7 +187,7 @@ def test_conv_stream_gemm(tile, case):
         return
     err, scale = _conv_case(N, H, W, cin, cout, 1, 1, 0, act, res=res, ldx_extra=lx, x_coff=xc,
                             ldy_extra=ly, y_coff=yc, tile=tile)
-    assert err <= 0.02 * scale + 0.02, (tile, case, err, scale)
+    assert err <= 0.02 * scale, (tile, case, err, scale)
 
 
 @pytest.mark.parametrize("tile", list(range(NLOOP0, N_TILES)))
@@ -192,7 +213,7 @@ def test_conv_nloop_gemm(tile, case):
         return
     err, scale = _conv_case(N, H, W, cin, cout, 1, 1, 0, act, res=res, ldx_extra=lx, x_coff=xc,
                             ldy_extra=ly, y_coff=yc, tile=tile)
-    assert err <= 0.02 * scale + 0.02, (tile, case, err, scale)
+    assert err <= 0.02 * scale, (tile, case, err, scale)
 
 
 def test_conv_identity_asymmetric():
@@ -333,8 +354,7 @@ def test_conv_dual_fused_downsample(tile, geom):
         return
     got = ops.conv_dual(x1.cuda(), x2.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, s, tile=tile)
     torch.cuda.synchronize()
-    err = (got.cpu().float() - ref.float()).abs().max().item()
-    assert err <= 0.02 * ref.float().abs().max().item() + 0.02
+    _assert_close(got.cpu(), ref, ("dual", tile, geom))
 
 
 def test_conv_dual_rejects_v1_tiles():
@@ -379,7 +399,7 @@ def test_conv_poisoned_canary(tile, k):
     assert torch.isnan(o[..., mask]).all()
     assert torch.isnan(flat[n_out:].cpu().float()).all()
     ref = ops.conv2d(x.cpu(), spec, w.cpu(), b.cpu())
-    assert (inside - ref.float()).abs().max().item() <= 0.02 * ref.float().abs().max().item() + 0.02
+    _assert_close(inside, ref, ("canary", tile, k))
 
 
 @pytest.mark.parametrize("case", [
@@ -412,7 +432,7 @@ def test_conv_direct3x3(case, dtile):
     a = act | (ops.RES_AFTER_ACT if res and act != ops.ACT_NONE else 0)
     err, scale = _conv_case(N, H, W, cin, cout, 3, s, 1, a, res=res, ldx_extra=lx, x_coff=xc,
                             ldy_extra=ly, y_coff=yc, tile=DIRECT0 + dtile)
-    assert err <= 0.02 * scale + 0.02, (case, err, scale)
+    assert err <= 0.02 * scale, (case, err, scale)
 
 
 @pytest.mark.parametrize("case", [
@@ -435,7 +455,7 @@ def test_conv_direct1x1(case, dtile):
     N, H, W, cin, cout, act, lx, xc, ly, yc = case
     err, scale = _conv_case(N, H, W, cin, cout, 1, 1, 0, act, ldx_extra=lx, x_coff=xc,
                             ldy_extra=ly, y_coff=yc, tile=DIRECT0 + dtile)
-    assert err <= 0.02 * scale + 0.02, (case, err, scale)
+    assert err <= 0.02 * scale, (case, err, scale)
 
 
 @pytest.mark.parametrize("shape", [(2, 40, 40), (1, 13, 7)])
@@ -452,8 +472,7 @@ def test_conv_direct_s2d_stem(shape):
     got = ops.conv2d(x.cuda(), spec, wp.cuda(), b.cuda(), tile=DIRECT0)
     torch.cuda.synchronize()
     assert got.shape == ref.shape == (N, H, W, 16)
-    err = (got.cpu().float() - ref.float()).abs().max().item()
-    assert err <= 0.02 * ref.float().abs().max().item() + 0.02, err
+    _assert_close(got.cpu(), ref, ("s2d stem", shape))
 
 
 def test_conv_direct3x3_rejects():
@@ -489,8 +508,7 @@ def test_stem_pool_fused(shape):
     torch.cuda.synchronize()
     got = out.cpu().float()
     assert torch.isnan(got[..., :8]).all()
-    err = (got[..., 8:] - ref.float()).abs().max().item()
-    assert err <= 0.02 * ref.float().abs().max().item() + 0.02, err
+    _assert_close(got[..., 8:], ref, ("stem_pool", shape))
 
 
 @pytest.mark.parametrize("case", [
@@ -527,5 +545,4 @@ def test_conv_tail_fused(case, mf):
                              res=r.cuda(), tile=tile)
     torch.cuda.synchronize()
     for got, ref in ((y, y_ref), (z, z_ref)):
-        err = (got.cpu().float() - ref.float()).abs().max().item()
-        assert err <= 0.02 * ref.float().abs().max().item() + 0.02, (case, err)
+        _assert_close(got.cpu(), ref, ("tail", case, mf))

@@ -11,6 +11,15 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
+
+
+def _close(got, ref):
+    """max |err| <= 2% of max |ref| AND relative RMS <= 4e-3 (VERDICT r2 weak #9)."""
+    got, ref = got.float(), ref.float()
+    err = (got - ref).abs().max().item()
+    rr = ((got - ref).pow(2).mean().sqrt() / ref.pow(2).mean().sqrt().clamp_min(1e-12)).item()
+    assert err <= 0.02 * ref.abs().max().item() and rr <= 4e-3, (err, rr)
+
 def resnet():
     assert ops.load()
     ref = init_resnet50(seed=0)
@@ -32,7 +41,7 @@ def test_resnet50_parity(resnet):
     cos_dep = torch.nn.functional.cosine_similarity(lg_gpu.flatten(), lg_cpu.flatten(), dim=0)
     cos_ref = torch.nn.functional.cosine_similarity(lg_gpu.flatten(), lg_ref.flatten(), dim=0)
     assert cos_dep > 0.995, float(cos_dep)
-    assert cos_ref > 0.98, float(cos_ref)
+    assert cos_ref > 0.99, float(cos_ref)
 
 
 def test_resnet50_engine_graph(resnet):
@@ -108,8 +117,7 @@ def test_stem_from_frames_kernel(hw):
     ref = ops.stem_from_frames(fr, b.spec, b.w, b.b).float()
     got = ops.stem_from_frames(fr.cuda(), b.spec, b.w.cuda(), b.b.cuda())
     torch.cuda.synchronize()
-    err = (got.cpu().float() - ref).abs().max().item()
-    assert err <= 0.02 * ref.abs().max().item() + 0.02, err
+    _close(got.cpu(), ref)
 
 
 def test_yolov8n_fused_stem_parity(yolo):
@@ -139,8 +147,7 @@ def test_stem_pool_frames_kernel(resnet, hw, n):
     two = ops.stem_pool(ops.preprocess(fr.cuda(), s2d=True), kv.stem.spec, kv.stem.w, kv.stem.b)
     torch.cuda.synchronize()
     assert got.shape == ref.shape
-    err = (got.cpu().float() - ref).abs().max().item()
-    assert err <= 0.02 * ref.abs().max().item() + 0.02, err
+    _close(got.cpu(), ref)
     err2 = (got.float() - two.float()).abs().max().item()
     assert err2 <= 0.01 * ref.abs().max().item() + 0.01, err2
 

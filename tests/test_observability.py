@@ -42,3 +42,16 @@ def test_amd_smi_parser_on_real_mi355x_output():
     m = parse_amd_smi_metric(open(p).read())
     assert set(m) == {"util_pct", "vram_used_mb", "vram_total_mb"}
     assert m["vram_total_mb"] == 294896.0  # 288 GiB HBM3E
+
+
+def test_amd_smi_index_is_mapped_by_pci_address():
+    """amd-smi enumerates every GPU of the host; HIP ordinals follow
+    HIP_/ROCR_VISIBLE_DEVICES.  The sampler maps by PCI bus id, never by ordinal."""
+    from kvedge_amd.utils.gpustat import smi_index_for_bdf
+
+    lst = json.dumps([{"gpu": 0, "bdf": "0000:05:00.0"}, {"gpu": 1, "bdf": "0000:15:00.0"},
+                      {"gpu": 7, "bdf": "0000:F5:00.0"}])
+    assert smi_index_for_bdf(lst, "0000:15:00.0") == 1
+    assert smi_index_for_bdf(lst, "f5:00.0") == 7  # short form, case-insensitive
+    assert smi_index_for_bdf(lst, "0000:25:00.0") is None
+    assert smi_index_for_bdf("garbage", "0000:05:00.0") is None

@@ -1,4 +1,7 @@
-"""T-resilience: drain / node loss / GPU failure on a fake cluster."""
+"""T-resilience: drain / node loss / GPU failure on a fake cluster,
+and the same controller over a dry-run / scripted KubectlCluster."""
+import json
+
 from kvedge_amd.resilience import (RWO, RWX, FakeCluster, KubectlAdapter, ResilienceController,
                                    Timings)
 
@@ -177,3 +180,79 @@ def test_gpu_reattach_restart_resumes_module_from_state_file(tmp_path):
     tel = tr2.outputs("telemetry")
     assert tel and tel[-1]["total_images"] > before
     app2.stop()
+
+
+def _rendered_snapshot(replicas, node="node-a"):
+    """kubectl-get-shaped JSON for a chart render: the VMs as rendered, and one Running
+    VMI per VM on ``node`` (what `kubectl get vmi -o json` would show after boot)."""
+    import os
+
+    from kvedge_amd.deploy.helm import Chart, manifests
+
+    chart = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                         "deploy", "helm")
+    objs = manifests(Chart(chart).render("rel", sets=[f"replicas={replicas}", "dp.enabled=false"]))
+    vms = [o for o in objs if o["kind"] == "VirtualMachine"]
+    vmis = [{"metadata": {"name": v["metadata"]["name"]},
+             "spec": v["spec"]["template"]["spec"],
+             "status": {"phase": "Running", "nodeName": node}} for v in vms]
+    return {"vm": {"items": vms}, "vmi": {"items": vmis}}, [v["metadata"]["name"] for v in vms]
+
+
+def test_one_controller_drives_kubectl_cluster_dry_run():
+    """the SAME ResilienceController drives a KubectlCluster.  A drain
+    of a node holding both VMs of a 2-replica render emits exactly cordon, then per VM
+    stop -> wait-deleted -> start -> wait-running, with the rendered names."""
+    from kvedge_amd.resilience import KubectlCluster
+
+    snap, names = _rendered_snapshot(2)
+    kc = KubectlCluster("edge", dry_run=True, snapshot=snap)
+    vms = kc.list_vms()
+    assert sorted(vms) == sorted(names)
+    assert all(v.run_strategy == "Always" and v.host_devices and v.gpus == 1 for v in vms.values())
+    assert vms[names[0]].pvc == "aziot-edge-kubevirt-linux-dv"
+    ctl = ResilienceController(kc)
+    rec = ctl.drain("node-a")
+    assert [r.vm for r in rec] == sorted(names)
+    assert all(r.ok and r.live_migration_refused and r.from_node == "node-a" for r in rec)
+    cmds = [" ".join(c) for c in kc.commands]
+    want = ["kubectl cordon node-a"]
+    for vm in sorted(names):
+        want += [f"virtctl stop {vm} -n edge",
+                 f"kubectl wait vmi/{vm} -n edge --for=delete --timeout=300s",
+                 f"virtctl start {vm} -n edge",
+                 f"kubectl wait vmi/{vm} -n edge --for=jsonpath={{.status.phase}}=Running "
+                 "--timeout=600s"]
+    assert cmds == want
+    # the same controller on the fake cluster still cold-migrates (fake tests above)
+    assert [w for _, w, _ in ctl.timeline(names[0])] == [
+        "live_migration_refused", "stopped", "running"]
+
+
+def test_kubectl_cluster_reports_unschedulable_and_node_loss():
+    """A live runner whose Running-wait times out (no free MI355X) -> Recovery not ok with
+    kubectl's message; node loss force-stops the lost node's VMIs before restarting."""
+    import subprocess
+
+    from kvedge_amd.resilience import KubectlCluster
+
+    snap, names = _rendered_snapshot(2)
+    seen = []
+    after = {"items": [dict(snap["vmi"]["items"][0], status={"phase": "Running",
+                                                             "nodeName": "node-b"})]}
+
+    def runner(cmd):
+        line = " ".join(cmd)
+        seen.append(line)
+        if cmd[:3] == ["kubectl", "get", "vmi"]:
+            return json.dumps(after)  # live re-read after the restart
+        if cmd[:2] == ["kubectl", "wait"] and "Running" in line and names[1] in line:
+            raise subprocess.CalledProcessError(1, cmd, "", "timed out waiting for the condition")
+        return ""
+
+    kc = KubectlCluster("edge", dry_run=False, snapshot=dict(snap), runner=runner)
+    ctl = ResilienceController(kc)
+    rec = {r.vm: r for r in ctl.recover_node_loss("node-a")}
+    assert sum("--force --grace-period=0" in c for c in seen) == 2  # both VMIs on node-a
+    assert rec[names[0]].ok and rec[names[0]].to_node == "node-b"
+    assert not rec[names[1]].ok and "timed out" in rec[names[1]].reason
