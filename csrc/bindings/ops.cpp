@@ -409,6 +409,36 @@ void synth_frames_dev(at::Tensor& y, at::Tensor& step, int64_t seed) {
 }
 
 // Frames-in ResNet stem + pool: preprocess (normalise + s2d) fused into stem_pool's fetch
+// Frames-in ResNet stem + pool, 12-channel s2d formulation (stem12.hip: K = 192, not 256)
+void stem12_pool_frames(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias,
+                        at::Tensor& y, at::ArrayRef<double> mean, at::ArrayRef<double> stdv,
+                        int64_t y_coff) {
+  check_dev(x, "x");
+  check_bf16(w, "w");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.scalar_type() == at::kByte && x.dim() == 4 && x.size(3) == 3 && x.is_contiguous(),
+              "kvedge: stem12_pool_frames x must be contiguous u8 [N,H,W,3]");
+  TORCH_CHECK(x.size(1) % 2 == 0 && x.size(2) % 4 == 0, "kvedge: stem12_pool_frames H even, W % 4");
+  TORCH_CHECK(w.numel() == 64 * 192 && w.is_contiguous(), "kvedge: stem12 w must be [64][192]");
+  TORCH_CHECK(bias.is_cuda() && bias.scalar_type() == at::kFloat && bias.numel() == 64 &&
+                  bias.is_contiguous(), "kvedge: stem12 bias");
+  TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "kvedge: mean/std of 3");
+  const int64_t N = x.size(0), H = x.size(1) / 2, W = x.size(2) / 2;
+  TORCH_CHECK(y.dim() == 4 && y.size(0) == N && y.size(1) == (H - 1) / 2 + 1 &&
+                  y.size(2) == (W - 1) / 2 + 1 && y.size(3) >= y_coff + 64 && y.is_contiguous(),
+              "kvedge: stem12_pool_frames y shape");
+  float m[3], is[3];
+  for (int i = 0; i < 3; ++i) {
+    m[i] = (float)mean[i];
+    is[i] = (float)(1.0 / stdv[i]);
+  }
+  const c10::DeviceGuard g(x.device());
+  const int rc = kv_stem12_pool_frames(x.data_ptr(), w.data_ptr(), bias.data_ptr<float>(),
+                                       y.data_ptr(), (int)N, (int)x.size(1), (int)x.size(2), m, is,
+                                       (int)y.size(3), (int)y_coff, cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: stem12_pool_frames failed rc=", rc);
+}
+
 void stem_pool_frames(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias,
                       at::Tensor& y, at::ArrayRef<double> mean, at::ArrayRef<double> stdv,
                       int64_t y_coff) {
@@ -516,6 +546,7 @@ TORCH_LIBRARY(kvedge, m) {
   m.def("synth_frames(Tensor(a!) y, int seed, int step) -> ()");
   m.def("synth_frames_dev(Tensor(a!) y, Tensor(b!) step, int seed) -> ()");
   m.def("stem_pool_frames(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, float[] mean, float[] std, int y_coff) -> ()");
+  m.def("stem12_pool_frames(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, float[] mean, float[] std, int y_coff) -> ()");
   m.def("preprocess(Tensor x, Tensor(a!) y, float[] mean, float[] std) -> ()");
   m.def("batchnorm_nhwc(Tensor x, Tensor(a!) y, Tensor scale, Tensor shift, bool relu) -> ()");
   m.def("conv_num_tiles() -> int", conv_num_tiles);
@@ -541,6 +572,7 @@ TORCH_LIBRARY_IMPL(kvedge, CUDA, m) {
   m.impl("synth_frames_dev", synth_frames_dev);
   m.impl("preprocess", preprocess);
   m.impl("stem_pool_frames", stem_pool_frames);
+  m.impl("stem12_pool_frames", stem12_pool_frames);
   m.impl("batchnorm_nhwc", batchnorm_nhwc);
 }
 

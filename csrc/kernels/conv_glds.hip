@@ -73,7 +73,10 @@ __device__ __forceinline__ void wait_vm() {
 // image and the same fragment bytes per FLOP (a 16x16x32 fragment is 16 rows x 32 k, a
 // 32x32x16 one 32 rows x 16 k: both one ds_read_b128); the 16x16x32 loop holds a higher
 // clock under load (MI355X_MICROARCH.md, DVFS item 7) at twice the MFMA count.
-template <int BM, int BN, int WM, int WN, int MODE, int D, int BKT = 64, int MF = 32>
+//
+// XP = true: the cross-stage pipelined main loop (v7 tiles, below the ring description).
+template <int BM, int BN, int WM, int WN, int MODE, int D, int BKT = 64, int MF = 32,
+          bool XP = false>
 __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_kernel(
     const KvConvParams p) {
   constexpr int NW = WM * WN;     // waves per workgroup
@@ -327,7 +330,89 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
   };
 
   const int nk = p.Kpad / BK;
-  if (D == 2) {
+  if constexpr (XP) {
+    // v7 cross-stage pipeline.  The ring loop above opens every stage with its own
+    // fragment reads AFTER the stage barrier, so each stage starts with an LDS-latency
+    // bubble in which no wave of the workgroup has an MFMA to issue (8 waves x 12 reads
+    // = 96 KB queue at 256 B/clk).  Here a phase (one stage = one MFMA k-step) issues
+    // the fragment reads of the NEXT stage into the other register set before its own
+    // MFMAs, so the MFMA stream never waits for LDS:
+    //   phase kt:  DMA stage kt+D-1 -> slot of stage kt-1      (WAR: its reads fed the
+    //              MFMAs of phase kt-1, which every wave issued before the last barrier)
+    //              ds_read stage kt+1 -> register set (kt+1)&1  (RAW: stage kt+1 was
+    //              waited for (own vmcnt) and published (barrier) at the end of kt-1)
+    //              MFMAs of stage kt from register set kt&1
+    //              vmcnt: stage kt+2 landed (D-3 younger stages in flight); s_barrier
+    // One raw barrier per stage, never a vmcnt(0) inside the loop.
+    static_assert(KS == 1 && D >= 4, "XP: one MFMA k-step per stage and >= 4 ring slots");
+    constexpr int OPS = A_INS + B_INS;
+    bf16x8 af0[TM], bg0[TN], af1[TM], bg1[TN];
+    auto ld = [&](bf16x8 (&af)[TM], bf16x8 (&bg)[TN], int slot) __attribute__((always_inline)) {
+      const bf16* As = smem + slot * STAGE;
+      const bf16* Bs = As + BM * BK;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int row = wm * WTM + tm * MF + fr;
+        af[tm] = *reinterpret_cast<const bf16x8*>(As + row * BK + ((fh ^ sw(row)) << 3));
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int row = wn * WTN + tn * MF + fr;
+        bg[tn] = *reinterpret_cast<const bf16x8*>(Bs + row * BK + ((fh ^ sw(row)) << 3));
+      }
+    };
+    auto mm = [&](bf16x8 (&af)[TM], bf16x8 (&bg)[TN]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          if constexpr (MF == 32)
+            acc[tn][tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bg[tn], af[tm], acc[tn][tm], 0, 0, 0);
+          else
+            acc[tn][tm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bg[tn], af[tm], acc[tn][tm], 0, 0, 0);
+        }
+    };
+    // interleave: this phase's DMA issue and next-stage reads between the first MFMAs
+    auto order = [&]() __attribute__((always_inline)) {
+      constexpr int NR = TM + TN, NM = TM * TN;
+      static_assert(NM >= 2 * NR, "enough MFMAs to cover the reads");
+#pragma unroll
+      for (int i = 0; i < OPS; ++i) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NM - 2 * NR, 0);
+    };
+#pragma unroll
+    for (int s = 0; s < D - 1; ++s) issue(s, s);
+    wait_vm<(D - 2) * OPS>();  // stage 0 landed (this wave's part)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    ld(af0, bg0, 0);
+    wait_vm<(D - 3) * OPS>();  // stage 1
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    auto phase = [&](int kt, bf16x8 (&ca)[TM], bf16x8 (&cb)[TN], bf16x8 (&na)[TM],
+                     bf16x8 (&nb)[TN]) __attribute__((always_inline)) {
+      issue((kt + D - 1) % D, kt + D - 1);
+      if (kt + 1 < nk) ld(na, nb, (kt + 1) % D);
+      mm(ca, cb);
+      order();
+      wait_vm<(D - 3) * OPS>();  // stage kt+2 landed
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      phase(kt, af0, bg0, af1, bg1);
+      phase(kt + 1, af1, bg1, af0, bg0);
+    }
+    if (kt < nk) phase(kt, af0, bg0, af1, bg1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land on the C tile
+  } else if (D == 2) {
     issue(0, 0);
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
@@ -412,13 +497,13 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
 
 typedef void (*ConvKernelFn)(const KvConvParams);
 
-template <int BM, int BN, int WM, int WN, int D = 2, int BKT = 64, int MF = 32>
+template <int BM, int BN, int WM, int WN, int D = 2, int BKT = 64, int MF = 32, bool XP = false>
 ConvKernelFn glds_get(int mode) {
   switch (mode) {
-    case 0: return conv_glds_kernel<BM, BN, WM, WN, 0, D, BKT, MF>;
-    case 1: return conv_glds_kernel<BM, BN, WM, WN, 1, D, BKT, MF>;
-    case 4: return conv_glds_kernel<BM, BN, WM, WN, 4, D, BKT, MF>;
-    default: return conv_glds_kernel<BM, BN, WM, WN, 3, D, BKT, MF>;
+    case 0: return conv_glds_kernel<BM, BN, WM, WN, 0, D, BKT, MF, XP>;
+    case 1: return conv_glds_kernel<BM, BN, WM, WN, 1, D, BKT, MF, XP>;
+    case 4: return conv_glds_kernel<BM, BN, WM, WN, 4, D, BKT, MF, XP>;
+    default: return conv_glds_kernel<BM, BN, WM, WN, 3, D, BKT, MF, XP>;
   }
 }
 
@@ -473,9 +558,33 @@ static const GldsTile kGldsTiles[] = {
 
 int glds_num_tiles() { return (int)(sizeof(kGldsTiles) / sizeof(kGldsTiles[0])); }
 
+// v7: the XP (cross-stage pipelined) main loop on BK = 32 rings, v_mfma_f32_16x16x32.
+// Own index range after v6 so the older families keep their indices.
+static const GldsTile kXpTiles[] = {
+    {256, 256, &glds_get<256, 256, 2, 4, 4, 32, 16, true>, 512},  // 128 px x 64 ch per wave
+    {256, 256, &glds_get<256, 256, 4, 2, 4, 32, 16, true>, 512},  // 64 px x 128 ch per wave
+    {256, 256, &glds_get<256, 256, 2, 4, 5, 32, 16, true>, 512},  // 4 stages in flight
+    {256, 256, &glds_get<256, 256, 4, 2, 5, 32, 16, true>, 512},
+    {256, 128, &glds_get<256, 128, 4, 2, 6, 32, 16, true>, 512},  // N = 128 layers, 64 x 64
+    {128, 256, &glds_get<128, 256, 2, 4, 6, 32, 16, true>, 512},
+};
+
+int xp_num_tiles() { return (int)(sizeof(kXpTiles) / sizeof(kXpTiles[0])); }
+
 // mode here is the caller's (0 general, 1 gemm); picks MODE 0 vs 3 by Cin and taps.
+static int glds_launch_entry(const KvConvParams* p, const struct GldsTile& e, hipStream_t stream);
+
 int glds_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   if (tile < 0 || tile >= glds_num_tiles()) return -6;
+  return glds_launch_entry(p, kGldsTiles[tile], stream);
+}
+
+int xp_launch(const KvConvParams* p, int tile, hipStream_t stream) {
+  if (tile < 0 || tile >= xp_num_tiles()) return -6;
+  return glds_launch_entry(p, kXpTiles[tile], stream);
+}
+
+static int glds_launch_entry(const KvConvParams* p, const GldsTile& e, hipStream_t stream) {
   int mode = p->mode;
   if (mode == 2) return -8;  // legacy stem layout: v1 only
   if (mode == 0 && (p->Cin % 64 != 0 || p->KH * p->KW > 32)) mode = 3;
@@ -486,7 +595,6 @@ int glds_launch(const KvConvParams* p, int tile, hipStream_t stream) {
     const long long x2b = (long long)p->N * p->H2 * p->W2 * p->ldx2 * 2;
     if (!p->x2 || x2b >= kOOB || p->K1 % BK || (p->Kpad - p->K1) % BK || p->ldx2 % 8) return -10;
   }
-  const GldsTile& e = kGldsTiles[tile];
   const long long nwg = (long long)((p->M + e.bm - 1) / e.bm) * ((p->Cout + e.bn - 1) / e.bn);
   if (nwg <= 0) return 0;
   hipLaunchKernelGGL(e.get(mode), dim3((unsigned)nwg), dim3(e.nt), 0, stream, *p);

@@ -316,13 +316,16 @@ int direct_launch(const KvConvParams* p, int tile, hipStream_t stream);
 int nloop_num_tiles();
 int nloop_launch(const KvConvParams* p, int tile, hipStream_t stream);
 int nloop_sched_check();
+// v7 cross-stage pipelined LDS-DMA GEMM (conv_glds.hip XP loop): indices after v6
+int xp_num_tiles();
+int xp_launch(const KvConvParams* p, int tile, hipStream_t stream);
 }  // namespace kvedge
 
 extern "C" int kv_nloop_sched_check(void) { return kvedge::nloop_sched_check(); }
 
 extern "C" int kv_conv_num_tiles(void) {
   return kNumTiles + glds_num_tiles() + stream_num_tiles() + direct_num_tiles() +
-         nloop_num_tiles();
+         nloop_num_tiles() + xp_num_tiles();
 }
 
 extern "C" int kv_conv_pick_tile(const KvConvParams* p) {
@@ -461,7 +464,9 @@ static int kv_conv2d_one(const KvConvParams* p, int tile, hipStream_t stream) {
   const int v3 = kNumTiles + glds_num_tiles();
   const int v4 = v3 + stream_num_tiles();
   const int v6 = v4 + direct_num_tiles();
-  if (tile >= v6 + nloop_num_tiles()) return -6;
+  const int v7 = v6 + nloop_num_tiles();
+  if (tile >= v7 + xp_num_tiles()) return -6;
+  if (tile >= v7) return xp_launch(p, tile - v7, stream);
   if (tile >= v6) return nloop_launch(p, tile - v6, stream);
   if (tile >= v4) return direct_launch(p, tile - v4, stream);
   if (tile >= v3) return stream_launch(p, tile - v3, stream);

@@ -93,6 +93,11 @@ int kv_stem_pool_lds_bytes(int W);
 int kv_stem_pool_frames(const void* frames, const void* w, const float* bias, void* y, int N,
                         int H0, int W0, const float* mean3, const float* inv_std3, int ldy,
                         int y_coff, hipStream_t s);
+// second-generation frames-in stem + pool (stem12.hip): 12-channel s2d, K = 192, w [64][192]
+int kv_stem12_pool_frames(const void* frames, const void* w, const float* bias, void* y, int N,
+                          int H0, int W0, const float* mean3, const float* inv_std3, int ldy,
+                          int y_coff, hipStream_t s);
+int kv_stem12_lds_bytes(int Ws);
 
 int kv_maxpool2d(const void* x, void* y, int N, int H, int W, int C, int ldx, int x_coff,
                  int ldy, int y_coff, int k, int stride, int pad, int Ho, int Wo, hipStream_t s);

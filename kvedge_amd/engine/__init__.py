@@ -216,7 +216,7 @@ def edge_latency(model: Callable, image_size: int, batches, device="cuda", seed:
         for _ in range(warmup):
             eng.run()
         st = eng.measure_latency(steps)
-        p50, p99 = st.percentile(50) * 1e3, st.percentile(99) * 1e3
+        p50, p99 = st.percentile(50), st.percentile(99)  # ms
         out.append({"batch": b, "p50_ms": round(p50, 4), "p99_ms": round(p99, 4),
                     "images_per_s": round(b / (p50 / 1e3), 1), "steps": steps})
         del eng

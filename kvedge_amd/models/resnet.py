@@ -21,7 +21,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .layers import DeployedConv, DeployedDualConv, calibrate_bn, count_flops, frames_to_nchw
+from .layers import (DeployedConv, DeployedDualConv, calibrate_bn, count_flops, fold_bn,
+                     frames_to_nchw)
 
 ACT_NONE, ACT_RELU = ops.ACT_NONE, ops.ACT_RELU
 
@@ -201,6 +202,9 @@ class KvResNet50:
         self.num_classes = ref.num_classes
         # stride-2 7x7 stem as a stride-1 4x4 conv over space-to-depth input (K12b)
         self.stem = DeployedConv.stem_s2d(ref.conv1, ref.bn1, ACT_RELU, self.device)
+        # the same folded stem as a 12-channel s2d 4x4 conv (K = 192): the frames-in GPU path
+        wf, _ = fold_bn(ref.conv1, ref.bn1)
+        self.stem12_w = ops.pack_stem12(wf).to(self.device)
         self._flops = {}
         self._ref = ref
         self.blocks = [DeployedBottleneck(b, self.device) for b in ref.blocks]
@@ -247,8 +251,14 @@ class KvResNet50:
     # level with or slower than direct + tail (docs/kernels.md, profiles/r2_v8_block_probe.md)
     fuse_block: bool = False
 
+    # frames-in stem: the 12-channel s2d kernel (stem12.hip, K 192, two workgroups per CU)
+    # instead of the 16-channel one (stem_pool.hip, K 256)
+    stem12: bool = True
+
     def stem_and_pool(self, x: torch.Tensor, frames_in: bool = False) -> torch.Tensor:
         if frames_in:
+            if self.stem12:
+                return ops.stem12_pool_frames(x, self.stem12_w, self.stem.b)
             return ops.stem_pool_frames(x, self.stem.spec, self.stem.w, self.stem.b)
         if self.fuse_stem_pool:
             return ops.stem_pool(x, self.stem.spec, self.stem.w, self.stem.b)

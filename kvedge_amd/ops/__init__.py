@@ -344,6 +344,71 @@ def stem_pool_frames(frames: torch.Tensor, spec: "ConvSpec", w: torch.Tensor,
     return out
 
 
+def pack_stem12(wf: torch.Tensor) -> torch.Tensor:
+    """Folded 7x7/2 stem weights [Cout, 3, 7, 7] -> the 12-channel s2d 4x4 form [Cout, 192]
+    bf16 that csrc/kernels/stem12.hip reads.  K index = r*48 + s*12 + dy*6 + dx*3 + c for
+    s2d tap (r, s) in 4x4 and s2d channel (dy, dx, c); its weight is
+    wf[:, c, 2r-1+dy, 2s-1+dx] (zero where that leaves 0..6)."""
+    cout, cin, k, _ = wf.shape
+    assert cin == 3 and k == 7
+    w = torch.zeros(cout, 4, 4, 2, 2, 3)
+    for r in range(4):
+        for dy in range(2):
+            ky = 2 * r - 1 + dy
+            if not 0 <= ky < 7:
+                continue
+            for s_ in range(4):
+                for dx in range(2):
+                    kx = 2 * s_ - 1 + dx
+                    if 0 <= kx < 7:
+                        w[:, r, s_, dy, dx, :] = wf[:, :, ky, kx].float()
+    return w.reshape(cout, 192).to(torch.bfloat16).contiguous()
+
+
+def stem12_reference(frames: torch.Tensor, w12: torch.Tensor, bias: torch.Tensor,
+                     mean=None, std=None) -> torch.Tensor:
+    """CPU reference of :func:`stem12_pool_frames`, step for step: normalise (fp32) -> bf16,
+    12-channel space-to-depth, 4x4 stride-1 conv (pads 2 / 1) in fp32, bf16, ReLU, 3x3/2
+    max pool (pad 1)."""
+    mean = IMAGENET_MEAN if mean is None else mean
+    std = IMAGENET_STD if std is None else std
+    N, H0, W0, _ = frames.shape
+    Hs, Ws = H0 // 2, W0 // 2
+    m = torch.tensor(mean, dtype=torch.float32)
+    inv = 1.0 / torch.tensor(std, dtype=torch.float32)
+    x = (frames.float() * (inv / 255.0) + (-m * inv)).to(torch.bfloat16).float()
+    x = x.view(N, Hs, 2, Ws, 2, 3).permute(0, 1, 3, 2, 4, 5).reshape(N, Hs, Ws, 12)
+    xp = torch.nn.functional.pad(x, (0, 0, 2, 1, 2, 1))  # X: 2 left 1 right, Y: 2 top 1 bottom
+    cols = xp.unfold(1, 4, 1).unfold(2, 4, 1)            # [N, Hs, Ws, 12, 4(r), 4(s)]
+    cols = cols.permute(0, 1, 2, 4, 5, 3).reshape(N, Hs, Ws, 192)
+    y = cols @ w12.float().t() + bias.float()
+    y = y.to(torch.bfloat16).float().relu()
+    y = torch.nn.functional.max_pool2d(y.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    return y.to(torch.bfloat16).contiguous()
+
+
+def stem12_pool_frames(frames: torch.Tensor, w12: torch.Tensor, bias: torch.Tensor,
+                       out: Optional[torch.Tensor] = None, y_coff: int = 0,
+                       mean=None, std=None) -> torch.Tensor:
+    """Frames-in ResNet stem + ReLU + 3x3/2 max pool over a 12-channel space-to-depth image
+    (K = 192 instead of the 16-channel form's 256; csrc/kernels/stem12.hip).
+    frames: uint8 [N, H, W, 3] (H even, W % 4 == 0); w12: :func:`pack_stem12`.
+    -> [N, H/4, W/4, 64] (224 -> 56).  CPU: :func:`stem12_reference`."""
+    assert frames.dtype == torch.uint8 and frames.dim() == 4 and frames.shape[3] == 3
+    mean = IMAGENET_MEAN if mean is None else mean
+    std = IMAGENET_STD if std is None else std
+    N, H0, W0, _ = frames.shape
+    Hs, Ws = H0 // 2, W0 // 2
+    if out is None:
+        out = empty(N, (Hs - 1) // 2 + 1, (Ws - 1) // 2 + 1, 64, dtype=torch.bfloat16,
+                    device=frames.device)
+    if not frames.is_cuda:
+        out[..., y_coff:y_coff + 64] = stem12_reference(frames, w12, bias, mean, std)
+        return out
+    _native().stem12_pool_frames(frames, w12, bias, out, list(mean), list(std), y_coff)
+    return out
+
+
 def stem_from_frames(frames: torch.Tensor, spec: "ConvSpec", w: torch.Tensor,
                      bias: Optional[torch.Tensor], out: Optional[torch.Tensor] = None,
                      tile: int = -1) -> torch.Tensor:

@@ -103,10 +103,11 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale
 
 
-N_TILES = 68  # v1 register-staged (0-5) + v2 LDS-DMA (6-31) + v3 streaming (32-53) + v4 direct (54-57)
+N_TILES = 74  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 XP (68-73)
 # + v6 A-resident N-loop 1x1 GEMM (58-67, conv_nloop.hip kNlTiles: one Kpad per tile;
 # 63-65 are the fused-downsample (dual) forms, 66-67 step 128 K at a time)
 NLOOP0 = 58
+XP0 = 68  # v7: the v2 kernel's cross-stage pipelined loop (BK 32 rings, 8 waves)
 NLOOP_KPAD = [128, 256, 256, 256, 256, 384, 384, 768, 256, 256]
 NLOOP_DUAL = {63, 64, 65}
 STREAM0 = 32  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
@@ -147,7 +148,7 @@ def test_tile_count():
 ])
 def test_conv_every_tile(tile, case):
     N, H, W, cin, cout, k, s, p, act, res, lx, xc = case
-    if tile >= DIRECT0:
+    if DIRECT0 <= tile < XP0:
         # the direct family takes only its instantiated shapes (a 1x1 64 -> 128 runs as two
         # Cout slices of the 64 -> 64 form); anything else must be refused, never run wrong
         try:
@@ -190,7 +191,7 @@ def test_conv_stream_gemm(tile, case):
     assert err <= 0.02 * scale, (tile, case, err, scale)
 
 
-@pytest.mark.parametrize("tile", list(range(NLOOP0, N_TILES)))
+@pytest.mark.parametrize("tile", list(range(NLOOP0, XP0)))
 @pytest.mark.parametrize("case", [
     # (N, H, W, cin, cout, act, res, ldx_extra, x_coff, ldy_extra, y_coff)
     (4, 14, 14, 256, 1024, ops.ACT_RELU, True, 0, 0, 0, 0),     # ResNet stage-3 expand + res
@@ -330,7 +331,8 @@ def test_nms_dense_overlaps():
     assert (o.cpu() - o_ref).abs().max() < 1e-4
 
 
-@pytest.mark.parametrize("tile", [-1] + list(range(6, DIRECT0)) + sorted(NLOOP_DUAL) + [NLOOP0 + 8])
+@pytest.mark.parametrize("tile", [-1] + list(range(6, DIRECT0)) + sorted(NLOOP_DUAL) + [NLOOP0 + 8]
+                         + list(range(XP0, N_TILES)))
 @pytest.mark.parametrize("geom", [(2, 14, 14, 64, 128, 256, 2), (2, 7, 7, 128, 256, 512, 1),
                                   (1, 5, 5, 64, 64, 128, 2),
                                   # the v6 dual tiles' K: 128 + 256 and 256 + 512, tails
@@ -344,7 +346,7 @@ def test_conv_dual_fused_downsample(tile, geom):
     w = (torch.randn(cout, K1 + K2, generator=g) * 0.05).to(torch.bfloat16)
     b = torch.randn(cout, generator=g)
     ref = ops.conv_dual(x1, x2, w, b, ops.ACT_RELU, s)
-    if tile >= NLOOP0 and (tile not in NLOOP_DUAL or K1 + K2 != NLOOP_KPAD[tile - NLOOP0]):
+    if NLOOP0 <= tile < XP0 and (tile not in NLOOP_DUAL or K1 + K2 != NLOOP_KPAD[tile - NLOOP0]):
         with pytest.raises(RuntimeError):  # each v6 dual tile is compiled for one K
             ops.conv_dual(x1.cuda(), x2.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, s, tile=tile)
         return
@@ -366,7 +368,7 @@ def test_conv_dual_rejects_v1_tiles():
 
 
 @pytest.mark.parametrize("tile", [-1, 1, 6, 7, 12, 13, STREAM0, STREAM0 + 1, STREAM0 + 5, DIRECT0,
-                                  DIRECT0 + 1])
+                                  DIRECT0 + 1, XP0, XP0 + 4])
 @pytest.mark.parametrize("k", [1, 3])
 def test_conv_poisoned_canary(tile, k):
     """SURVEY §5.2 poisoned-buffer check: the output buffer is NaN-filled, with a NaN
@@ -375,10 +377,10 @@ def test_conv_poisoned_canary(tile, k):
     (a kernel that writes past M/N tails or outside [y_coff, y_coff+cout) fails here)."""
     if STREAM0 <= tile < DIRECT0 and k != 1:
         pytest.skip("v3 tiles take 1x1 GEMMs only")
-    if tile >= DIRECT0 and k != 3:
+    if DIRECT0 <= tile < XP0 and k != 3:
         pytest.skip("v4 takes 3x3 only")
     N, H, W, cin, cout, ldy, y_coff = 3, 13, 11, 64, 72, 104, 16
-    if tile >= DIRECT0:
+    if DIRECT0 <= tile < XP0:
         cout = 64  # an instantiated direct shape (64 -> 64 ReLU)
     spec = ConvSpec.auto(cin, cout, k, 1, k // 2, ops.ACT_RELU)
     g = torch.Generator().manual_seed(3)

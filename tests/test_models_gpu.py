@@ -184,3 +184,30 @@ def test_resnet50_microbatch_fused_tail(resnet, mb, nb):
             kv.microbatch, kv.microbatch_blocks = 0, 3
     torch.cuda.synchronize()
     assert torch.allclose(lg_full, lg_mb, atol=1e-2, rtol=1e-2), (lg_full - lg_mb).abs().max()
+
+
+@pytest.mark.parametrize("hw,n", [((224, 224), 3), ((64, 96), 5), ((38, 20), 5), ((224, 224), 40),
+                                  ((36, 20), 300), ((22, 28), 7)])
+def test_stem12_pool_frames_kernel(resnet, hw, n):
+    """12-channel s2d stem (csrc/kernels/stem12.hip, K 192) vs its CPU reference step for
+    step, and vs the fp32 nn.Conv2d stem: odd stem heights (38 -> 19 rows), image-start
+    bands inside a workgroup's range (n = 300: more bands than workgroups), a channel-slice
+    output with a NaN canary outside it."""
+    ref, kv, kv_cpu = resnet
+    fr = torch.randint(0, 256, (n, hw[0], hw[1], 3), dtype=torch.uint8,
+                       generator=torch.Generator().manual_seed(13))
+    want = ops.stem12_reference(fr, kv_cpu.stem12_w, kv_cpu.stem.b)
+    Hp, Wp = want.shape[1], want.shape[2]
+    out = torch.full((n, Hp, Wp, 80), float("nan"), dtype=torch.bfloat16, device="cuda")
+    ops.stem12_pool_frames(fr.cuda(), kv.stem12_w, kv.stem.b, out=out, y_coff=8)
+    torch.cuda.synchronize()
+    got = out.cpu()
+    assert torch.isnan(got[..., :8].float()).all() and torch.isnan(got[..., 72:].float()).all()
+    _close(got[..., 8:72], want)
+    # and the model's own stem (fp32 nn.Module conv + BN + ReLU + pool)
+    with torch.no_grad():
+        x = frames_to_nchw(fr)
+        r = torch.nn.functional.max_pool2d(torch.relu(ref.bn1(ref.conv1(x))), 3, 2, 1)
+    r = r.permute(0, 2, 3, 1)
+    cos = torch.nn.functional.cosine_similarity(got[..., 8:72].float().flatten(), r.flatten(), dim=0)
+    assert cos > 0.999, float(cos)

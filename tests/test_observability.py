@@ -55,3 +55,16 @@ def test_amd_smi_index_is_mapped_by_pci_address():
     assert smi_index_for_bdf(lst, "f5:00.0") == 7  # short form, case-insensitive
     assert smi_index_for_bdf(lst, "0000:25:00.0") is None
     assert smi_index_for_bdf("garbage", "0000:05:00.0") is None
+
+
+def test_amd_smi_list_fixture_from_the_pool():
+    """`amd-smi list --json` captured on the MI355X pool (r3 baseline run)."""
+    import os
+
+    from kvedge_amd.utils.gpustat import smi_index_for_bdf
+
+    p = os.path.join(os.path.dirname(__file__), "fixtures", "amdsmi_list_mi355x.json")
+    txt = open(p).read()
+    bdf = json.loads(txt)[0]["bdf"]
+    assert smi_index_for_bdf(txt, bdf) == 0
+    assert smi_index_for_bdf(txt, bdf.upper()) == 0

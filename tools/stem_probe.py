@@ -22,9 +22,18 @@ def main():
     fr = torch.randint(0, 256, (a.batch, 224, 224, 3), dtype=torch.uint8, device="cuda")
     x = m.preprocess(fr)
     flops = 2 * a.batch * 112 * 112 * 64 * 147
+    def frames16():
+        m.stem12 = False
+        return m.stem_and_pool(fr, frames_in=True)
+
+    def frames12():
+        m.stem12 = True
+        return m.stem_and_pool(fr, frames_in=True)
+
     for name, fn in (("preprocess+stem_pool", lambda: m.stem_and_pool(m.preprocess(fr))),
                      ("stem_pool", lambda: m.stem_and_pool(x)),
-                     ("stem_pool_frames", lambda: m.stem_and_pool(fr, frames_in=True))):
+                     ("stem_pool_frames (16-ch s2d, K 256)", frames16),
+                     ("stem12_pool_frames (12-ch s2d, K 192)", frames12)):
         out = fn()
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -31,7 +31,10 @@ def main():
               ("s3.c1a", 28, 512, 256, False), ("s4.c1a", 14, 1024, 512, False), ("s1.c3-nores", 56, 64, 256, False),
               ("s2.c3-nores", 28, 128, 512, False), ("s3.c3-nores", 14, 256, 1024, False), ("s1.c1a-wide", 56, 64, 512, False),
               ("s1.c2", 56, 64, 64, False, 3), ("s2.c2", 28, 128, 128, False, 3),
-              ("s3.c2", 14, 256, 256, False, 3), ("s4.c2", 7, 512, 512, False, 3)]
+              ("s3.c2", 14, 256, 256, False, 3), ("s4.c2", 7, 512, 512, False, 3),
+              # stride-2 3x3 (block 0 of stages 2-4): input hw, output hw / 2
+              ("s2.c2s", 56, 128, 128, False, 3, 2), ("s3.c2s", 28, 256, 256, False, 3, 2),
+              ("s4.c2s", 14, 512, 512, False, 3, 2)]
     if a.only:
         layers = [l for l in layers if l[0] in a.only.split(",")]
     ntiles = int(torch.ops.kvedge.conv_num_tiles())
@@ -53,14 +56,16 @@ def main():
     print("|---" * (len(tiles) + 2) + "|")
     for name, hw, cin, cout, res, *kk in layers:
         k = kk[0] if kk else 1
-        spec = ConvSpec.auto(cin, cout, k, 1, k // 2, ops.ACT_RELU)
+        st = kk[1] if len(kk) > 1 else 1
+        spec = ConvSpec.auto(cin, cout, k, st, k // 2, ops.ACT_RELU)
         x = torch.randn(B, hw, hw, cin, device="cuda").to(torch.bfloat16)
         w = (torch.randn(cout, spec.Kpad, device="cuda") * 0.05).to(torch.bfloat16)
         b = torch.randn(cout, device="cuda")
-        out = torch.empty(B, hw, hw, cout, device="cuda", dtype=torch.bfloat16)
-        r = torch.randn(B, hw, hw, cout, device="cuda").to(torch.bfloat16) if res else None
-        byts = 2.0 * B * hw * hw * (cin + cout * (2 if res else 1)) + 2.0 * cout * spec.Kpad
-        flops = 2.0 * B * hw * hw * cout * cin * k * k
+        ho = hw // st
+        out = torch.empty(B, ho, ho, cout, device="cuda", dtype=torch.bfloat16)
+        r = torch.randn(B, ho, ho, cout, device="cuda").to(torch.bfloat16) if res else None
+        byts = 2.0 * B * (hw * hw * cin + ho * ho * cout * (2 if res else 1)) + 2.0 * cout * spec.Kpad
+        flops = 2.0 * B * ho * ho * cout * cin * k * k
         cells, best = [], 1e30
         for t in tiles:
             try:
