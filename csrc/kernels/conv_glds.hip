@@ -97,8 +97,13 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
   static_assert(A_INS >= 1 && B_INS >= 1, "tile too small for BK");
   static_assert((NW == 4 || NW == 8) && TM >= 1 && TN >= 1 && D >= 2 && D <= 6, "tile");
   // chunk swizzle of row r: ds_read_b128 of 16 rows x one logical chunk is conflict-free
+  // BK = 32 rows are 64 B (4 chunks): MF = 16 reads take rows 0-15 with chunk quarter
+  // lane >> 4, so a ds_read_b128 lane group mixes rows {0-3, 12-15} of one quarter with
+  // rows {4-11} of the next; XOR (row >> 2) & 2 makes the 16 (row & 3, chunk) slots of
+  // every group distinct (the (row >> 2) & 3 form is 2-way conflicted there: PMC
+  // SQ_LDS_BANK_CONFLICT 19x, profiles/r3_v2_pmc_s3c2_b256)
   auto sw = [](int r) __attribute__((always_inline)) {
-    return BK == 64 ? ((r >> 1) & 7) : ((r >> 2) & 3);
+    return BK == 64 ? ((r >> 1) & 7) : (MF == 16 ? ((r >> 2) & 2) : ((r >> 2) & 3));
   };
   __shared__ __attribute__((aligned(16))) bf16 smem[D * STAGE];
 
@@ -567,6 +572,16 @@ static const GldsTile kXpTiles[] = {
     {256, 256, &glds_get<256, 256, 4, 2, 5, 32, 16, true>, 512},
     {256, 128, &glds_get<256, 128, 4, 2, 6, 32, 16, true>, 512},  // N = 128 layers, 64 x 64
     {128, 256, &glds_get<128, 256, 2, 4, 6, 32, 16, true>, 512},
+    // the plain ring loop on BK = 32 with the MF = 16 conflict-free swizzle (the round-1/2
+    // BK = 32 rings were measured with a 2-way conflicted one); 4-wave forms fit <= 80 KB of
+    // LDS, so two workgroups -- of this launch or of the other stream's -- share a CU and
+    // one's epilogue overlaps the other's main loop
+    {256, 256, &glds_get<256, 256, 4, 2, 4, 32, 16>, 512},        // 128 KB
+    {256, 128, &glds_get<256, 128, 2, 2, 3, 32, 16>},             // 72 KB, 128 x 64 per wave
+    {128, 256, &glds_get<128, 256, 2, 2, 3, 32, 16>},             // 72 KB, 64 x 128 per wave
+    {128, 128, &glds_get<128, 128, 2, 2, 4, 32, 16>},             // 64 KB
+    {128, 128, &glds_get<128, 128, 2, 2, 5, 32, 16>},             // 80 KB
+    {256, 128, &glds_get<256, 128, 4, 2, 4, 32, 16>, 512},        // 96 KB
 };
 
 int xp_num_tiles() { return (int)(sizeof(kXpTiles) / sizeof(kXpTiles[0])); }

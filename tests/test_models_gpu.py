@@ -10,9 +10,6 @@ from kvedge_amd.models.resnet import KvResNet50, init_resnet50
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-
-
 def _close(got, ref):
     """max |err| <= 2% of max |ref| AND relative RMS <= 4e-3 (VERDICT r2 weak #9)."""
     got, ref = got.float(), ref.float()
@@ -20,6 +17,8 @@ def _close(got, ref):
     rr = ((got - ref).pow(2).mean().sqrt() / ref.pow(2).mean().sqrt().clamp_min(1e-12)).item()
     assert err <= 0.02 * ref.abs().max().item() and rr <= 4e-3, (err, rr)
 
+
+@pytest.fixture(scope="module")
 def resnet():
     assert ops.load()
     ref = init_resnet50(seed=0)

@@ -11,7 +11,7 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/p$i -o p$i -- \
-    python3 tools/tile_probe.py --only $L --tiles $T --iters 3 > $OUT/p$i.log 2>&1 || exit $?
+    python3 tools/tile_probe.py --only $L --tiles $T --iters 3 --batch ${PMC_BATCH:-256} > $OUT/p$i.log 2>&1 || exit $?
 done
 python3 tools/pmc_summary.py $OUT > $OUT/summary.txt 2>&1 || true
 echo done

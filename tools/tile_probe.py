@@ -15,6 +15,9 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tiles", default="")
     ap.add_argument("--only", default="")
+    ap.add_argument("--concurrent", type=int, default=1,
+                    help="launch each call on this many streams at once (the multi-stream "
+                         "engine's situation) and report time per call")
     a = ap.parse_args()
     import torch
     from kvedge_amd import ops
@@ -40,17 +43,28 @@ def main():
     ntiles = int(torch.ops.kvedge.conv_num_tiles())
     tiles = [int(t) for t in a.tiles.split(",")] if a.tiles else list(range(ntiles))
 
+    side = [torch.cuda.Stream() for _ in range(a.concurrent)]
+
     def timeit(fn):
         for _ in range(3):
             fn()
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
+        cur = torch.cuda.current_stream()
         st.record()
         for _ in range(a.iters):
-            fn()
+            if a.concurrent == 1:
+                fn()
+                continue
+            for s_ in side:
+                s_.wait_stream(cur)
+                with torch.cuda.stream(s_):
+                    fn()
+            for s_ in side:
+                cur.wait_stream(s_)
         en.record()
         torch.cuda.synchronize()
-        return st.elapsed_time(en) / a.iters * 1e3
+        return st.elapsed_time(en) / a.iters / a.concurrent * 1e3
 
     print("| layer | " + " | ".join(str(t) for t in tiles) + " | best |")
     print("|---" * (len(tiles) + 2) + "|")
