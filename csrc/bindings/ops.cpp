@@ -132,7 +132,12 @@ void conv_tail(const at::Tensor& x, const c10::optional<at::Tensor>& x2, const a
   TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && z.dim() == 4, "kvedge: NHWC tensors");
   const int64_t N = x.size(0), H = x.size(1), W = x.size(2), K1 = x.size(3);
   const int64_t Cout = y.size(3), Nt = w1.size(0);
-  TORCH_CHECK(y.size(0) == N && y.size(1) == H && y.size(2) == W, "kvedge: y shape");
+  // y [N, H, W, Cout], or [N, H/2, W/2, Cout]: only the even pixels, compacted (y_s2)
+  const bool y_s2 = y.size(1) != H;
+  TORCH_CHECK(y.size(0) == N && (y_s2 ? (H % 2 == 0 && W % 2 == 0 && y.size(1) == H / 2 &&
+                                         y.size(2) == W / 2)
+                                      : (y.size(1) == H && y.size(2) == W)),
+              "kvedge: y shape ([N,H,W,C], or [N,H/2,W/2,C] for the even-pixel form)");
   TORCH_CHECK(z.size(0) == N && z.size(1) == H && z.size(2) == W && z.size(3) == Nt,
               "kvedge: z shape");
   TORCH_CHECK(w1.dim() == 2 && w1.size(1) == Cout, "kvedge: w1 must be [n_t, Cout]");
@@ -154,6 +159,7 @@ void conv_tail(const at::Tensor& x, const c10::optional<at::Tensor>& x2, const a
   p.M = (int)(N * H * W);
   p.ldy = (int)Cout; p.y_coff = 0; p.r_coff = 0;
   p.act = (int)act;
+  p.y_s2 = y_s2 ? 1 : 0;
   if (x2.has_value() && x2->defined()) {
     check_bf16(*x2, "x2");
     TORCH_CHECK(!(res.has_value() && res->defined()), "kvedge: conv_tail dual form takes no res");
@@ -169,7 +175,8 @@ void conv_tail(const at::Tensor& x, const c10::optional<at::Tensor>& x2, const a
   } else {
     TORCH_CHECK(res.has_value() && res->defined(), "kvedge: conv_tail plain form needs res");
     check_bf16(*res, "res");
-    TORCH_CHECK(res->sizes() == y.sizes(), "kvedge: res shape");
+    TORCH_CHECK(res->dim() == 4 && res->size(0) == N && res->size(1) == H && res->size(2) == W &&
+                    res->size(3) == Cout, "kvedge: res shape");
     TORCH_CHECK(w.dim() == 2 && w.size(0) == Cout && w.size(1) == K1, "kvedge: w [Cout, K1]");
     p.mode = 1; p.K = (int)K1; p.Kpad = (int)K1;
     p.res = res->data_ptr(); p.ldr = (int)Cout;

@@ -234,27 +234,35 @@ def conv_tail(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], ac
               w1: torch.Tensor, b1: Optional[torch.Tensor], res: Optional[torch.Tensor] = None,
               x2: Optional[torch.Tensor] = None, stride2: int = 1,
               out: Optional[torch.Tensor] = None, z: Optional[torch.Tensor] = None,
-              tile: int = -1):
+              tile: int = -1, y_s2: bool = False):
     """Fused bottleneck tail: y = act(x . W^T + bias + res) -- or, with ``x2``, the dual
     conv3 + downsample GEMM of :func:`conv_dual` -- AND z = ReLU(y . w1^T + b1), the next
     block's 1x1 reduce conv, in one pass: y is written once and never re-read from HBM.
-    w: packed [Cout, K] (1x1); w1: packed [n_t, Cout].  Returns (y, z)."""
+    w: packed [Cout, K] (1x1); w1: packed [n_t, Cout].  Returns (y, z).
+
+    ``y_s2``: y is returned as y[:, ::2, ::2] only ([N, H/2, W/2, Cout]; z stays full): the
+    form for a y whose only other reader is a stride-2 downsample -- 3/4 of its HBM
+    writes disappear (ResNet-50's stage-1 -> stage-2 boundary)."""
     N, H, W, _ = x.shape
     cout, nt = w.shape[0], w1.shape[0]
     if out is None:
-        out = empty(N, H, W, cout, dtype=torch.bfloat16, device=x.device)
+        out = (empty(N, H // 2, W // 2, cout, dtype=torch.bfloat16, device=x.device) if y_s2
+               else empty(N, H, W, cout, dtype=torch.bfloat16, device=x.device))
     if z is None:
         z = empty(N, H, W, nt, dtype=torch.bfloat16, device=x.device)
     if x.is_cuda:
         _native().conv_tail(x, x2, w, bias, res, out, w1, b1, z, stride2, act, tile)
         return out, z
+    full = empty(N, H, W, cout, dtype=torch.bfloat16, device=x.device) if y_s2 else out
     if x2 is not None:
-        _ref.conv_dual(x, x2, w, bias, act, stride2, out)
+        _ref.conv_dual(x, x2, w, bias, act, stride2, full)
     else:
         spec = ConvSpec.auto(x.shape[3], cout, 1, 1, 0, act)
-        _ref.conv2d(x, spec, w, bias, res, out, 0, 0, 0)
+        _ref.conv2d(x, spec, w, bias, res, full, 0, 0, 0)
     spec1 = ConvSpec.auto(cout, nt, 1, 1, 0, ACT_RELU)
-    _ref.conv2d(out, spec1, w1, b1, None, z, 0, 0, 0)
+    _ref.conv2d(full, spec1, w1, b1, None, z, 0, 0, 0)
+    if y_s2:
+        out.copy_(full[:, ::2, ::2])
     return out, z
 
 

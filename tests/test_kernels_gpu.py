@@ -548,3 +548,38 @@ def test_conv_tail_fused(case, mf):
     torch.cuda.synchronize()
     for got, ref in ((y, y_ref), (z, z_ref)):
         _assert_close(got.cpu(), ref, ("tail", case, mf))
+
+
+@pytest.mark.parametrize("case", [
+    # (N, H, W, k1, k2, stride2, n_t)
+    (2, 56, 56, 64, 0, 1, 128),    # layer1 block 2 -> layer2 (the deployed y_s2 site)
+    (3, 14, 10, 64, 0, 1, 64),     # M tail, odd tile splits
+    (2, 28, 28, 64, 64, 1, 64),    # dual form
+])
+def test_conv_tail_even_pixels_only(case):
+    """y_s2 tail: y written only at even (h, w), compacted to [N, H/2, W/2, C]; z full.
+    The destination is NaN-filled with a canary tail: nothing past it may be written."""
+    N, H, W, k1, k2, s2, nt = case
+    cout = 256
+    g = torch.Generator().manual_seed(H + nt)
+    t = _rand((N, H, W, k1), 4)
+    w = (torch.randn(cout, k1 + k2, generator=g) * (2.0 / (k1 + k2)) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(cout, generator=g) * 0.1
+    w1 = (torch.randn(nt, cout, generator=g) * (2.0 / cout) ** 0.5).to(torch.bfloat16)
+    b1 = torch.randn(nt, generator=g) * 0.1
+    kw = {}
+    if k2:
+        kw = {"x2": _rand((N, H * s2, W * s2, k2), 5), "stride2": s2}
+    else:
+        kw = {"res": _rand((N, H, W, cout), 6)}
+    y_ref, z_ref = ops.conv_tail(t, w, b, ops.ACT_RELU, w1, b1, **kw)
+    n_y = N * (H // 2) * (W // 2) * cout
+    flat = torch.full((n_y + 4096,), float("nan"), dtype=torch.bfloat16, device="cuda")
+    y = flat[:n_y].view(N, H // 2, W // 2, cout)
+    gkw = {k: (v.cuda() if torch.is_tensor(v) else v) for k, v in kw.items()}
+    y, z = ops.conv_tail(t.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, w1.cuda(), b1.cuda(),
+                         out=y, y_s2=True, **gkw)
+    torch.cuda.synchronize()
+    assert torch.isnan(flat[n_y:].cpu().float()).all()
+    _assert_close(y.cpu(), y_ref[:, ::2, ::2], ("y_s2", case))
+    _assert_close(z.cpu(), z_ref, ("z", case))
