@@ -33,12 +33,18 @@ void conv(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
           int64_t Cin, int64_t ldx, int64_t x_coff, int64_t Ho, int64_t Wo, int64_t Cout,
           int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t K, int64_t ldy,
           int64_t y_coff, int64_t ldr, int64_t r_coff, int64_t act, int64_t mode,
-          int64_t tile) {
+          int64_t tile, const c10::optional<at::Tensor>& ws) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_bf16(y, "y");
   const c10::DeviceGuard g(x.device());
   KvConvParams p{};
+  if (ws.has_value() && ws->defined()) {  // split-K workspace (v8 tiles): fp32, zero, >= M*Cout
+    check_dev(*ws, "ws");
+    TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= N * Ho * Wo * Cout,
+                "kvedge: split-K workspace fp32[M*Cout]");
+    p.ws = ws->data_ptr<float>();
+  }
   p.x = x.data_ptr();
   p.w = w.data_ptr();
   p.bias = nullptr;
@@ -79,7 +85,7 @@ void conv(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
 //   y = act( x1 (1x1) . W[:, :K1]  +  x2 (1x1, stride s2) . W[:, K1:]  + bias )
 void conv_dual(const at::Tensor& x1, const at::Tensor& x2, const at::Tensor& w,
                const c10::optional<at::Tensor>& bias, at::Tensor& y, int64_t stride2,
-               int64_t act, int64_t tile) {
+               int64_t act, int64_t tile, const c10::optional<at::Tensor>& ws) {
   check_bf16(x1, "x1");
   check_bf16(x2, "x2");
   check_bf16(w, "w");
@@ -113,6 +119,12 @@ void conv_dual(const at::Tensor& x1, const at::Tensor& x2, const at::Tensor& w,
   p.act = (int)act; p.mode = 4;
   p.x2 = x2.data_ptr(); p.K1 = (int)K1; p.H2 = (int)x2.size(1); p.W2 = (int)x2.size(2);
   p.ldx2 = (int)K2; p.stride2 = (int)stride2;
+  if (ws.has_value() && ws->defined()) {
+    check_dev(*ws, "ws");
+    TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= (int64_t)p.M * Cout,
+                "kvedge: split-K workspace fp32[M*Cout]");
+    p.ws = ws->data_ptr<float>();
+  }
   const int rc = kv_conv2d(&p, (int)tile, cur_stream(x1));
   TORCH_CHECK(rc == 0, "kvedge: conv_dual failed rc=", rc);
 }
@@ -132,12 +144,7 @@ void conv_tail(const at::Tensor& x, const c10::optional<at::Tensor>& x2, const a
   TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && z.dim() == 4, "kvedge: NHWC tensors");
   const int64_t N = x.size(0), H = x.size(1), W = x.size(2), K1 = x.size(3);
   const int64_t Cout = y.size(3), Nt = w1.size(0);
-  // y [N, H, W, Cout], or [N, H/2, W/2, Cout]: only the even pixels, compacted (y_s2)
-  const bool y_s2 = y.size(1) != H;
-  TORCH_CHECK(y.size(0) == N && (y_s2 ? (H % 2 == 0 && W % 2 == 0 && y.size(1) == H / 2 &&
-                                         y.size(2) == W / 2)
-                                      : (y.size(1) == H && y.size(2) == W)),
-              "kvedge: y shape ([N,H,W,C], or [N,H/2,W/2,C] for the even-pixel form)");
+  TORCH_CHECK(y.size(0) == N && y.size(1) == H && y.size(2) == W, "kvedge: y shape");
   TORCH_CHECK(z.size(0) == N && z.size(1) == H && z.size(2) == W && z.size(3) == Nt,
               "kvedge: z shape");
   TORCH_CHECK(w1.dim() == 2 && w1.size(1) == Cout, "kvedge: w1 must be [n_t, Cout]");
@@ -159,7 +166,6 @@ void conv_tail(const at::Tensor& x, const c10::optional<at::Tensor>& x2, const a
   p.M = (int)(N * H * W);
   p.ldy = (int)Cout; p.y_coff = 0; p.r_coff = 0;
   p.act = (int)act;
-  p.y_s2 = y_s2 ? 1 : 0;
   if (x2.has_value() && x2->defined()) {
     check_bf16(*x2, "x2");
     TORCH_CHECK(!(res.has_value() && res->defined()), "kvedge: conv_tail dual form takes no res");
@@ -175,8 +181,7 @@ void conv_tail(const at::Tensor& x, const c10::optional<at::Tensor>& x2, const a
   } else {
     TORCH_CHECK(res.has_value() && res->defined(), "kvedge: conv_tail plain form needs res");
     check_bf16(*res, "res");
-    TORCH_CHECK(res->dim() == 4 && res->size(0) == N && res->size(1) == H && res->size(2) == W &&
-                    res->size(3) == Cout, "kvedge: res shape");
+    TORCH_CHECK(res->sizes() == y.sizes(), "kvedge: res shape");
     TORCH_CHECK(w.dim() == 2 && w.size(0) == Cout && w.size(1) == K1, "kvedge: w [Cout, K1]");
     p.mode = 1; p.K = (int)K1; p.Kpad = (int)K1;
     p.res = res->data_ptr(); p.ldr = (int)Cout;
@@ -528,9 +533,10 @@ int64_t set_conv_chunk_bytes(int64_t b) { return kv_set_conv_chunk_bytes(b); }
 TORCH_LIBRARY(kvedge, m) {
   m.def("conv(Tensor x, Tensor w, Tensor? bias, Tensor? res, Tensor(a!) y, int N, int H, int W, "
         "int Cin, int ldx, int x_coff, int Ho, int Wo, int Cout, int KH, int KW, int stride, "
-        "int pad, int K, int ldy, int y_coff, int ldr, int r_coff, int act, int mode, int tile) -> ()");
+        "int pad, int K, int ldy, int y_coff, int ldr, int r_coff, int act, int mode, int tile, "
+        "Tensor(b!)? ws=None) -> ()");
   m.def("conv_dual(Tensor x1, Tensor x2, Tensor w, Tensor? bias, Tensor(a!) y, int stride2, int act, "
-        "int tile) -> ()");
+        "int tile, Tensor(b!)? ws=None) -> ()");
   m.def("conv_tail(Tensor x, Tensor? x2, Tensor w, Tensor? bias, Tensor? res, Tensor(a!) y, "
         "Tensor w1, Tensor? b1, Tensor(b!) z, int stride2, int act, int tile) -> ()");
   m.def("conv_block(Tensor t, Tensor w2, Tensor b2, Tensor w3, Tensor b3, Tensor? x2, Tensor? res, "

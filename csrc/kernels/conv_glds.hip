@@ -76,7 +76,7 @@ __device__ __forceinline__ void wait_vm() {
 //
 // XP = true: the cross-stage pipelined main loop (v7 tiles, below the ring description).
 template <int BM, int BN, int WM, int WN, int MODE, int D, int BKT = 64, int MF = 32,
-          bool XP = false>
+          bool XP = false, bool DE = false, bool SK = false>
 __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_kernel(
     const KvConvParams p) {
   constexpr int NW = WM * WN;     // waves per workgroup
@@ -111,8 +111,13 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wv / WN, wn = wv % WN;
   const int nbm = (p.M + BM - 1) / BM, nbn = (p.Cout + BN - 1) / BN;
-  const int t = xcd_remap(blockIdx.x, nbm * nbn);
+  // split-K (SK): the p.ksplit consecutive blocks of a tile take equal shares of its K steps
+  const int kz = SK ? (int)(blockIdx.x % p.ksplit) : 0;
+  const int t = SK ? (int)(blockIdx.x / p.ksplit) : xcd_remap(blockIdx.x, nbm * nbn);
   const int m0 = (t / nbn) * BM, n0 = (t % nbn) * BN;
+  const int nk_all = p.Kpad / BKT;
+  const int kb = SK ? kz * nk_all / p.ksplit : 0;                  // first K step (absolute)
+  const int ke = SK ? (kz + 1) * nk_all / p.ksplit : nk_all;      // one past the last
 
   const __amdgpu_buffer_rsrc_t rx = make_rsrc(p.x, p.N * p.H * p.W * p.ldx * 2);
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.w, p.Cout * p.Kpad * 2);
@@ -130,7 +135,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
   constexpr int CPR = BNH / 8;
   constexpr int PERH = BM * CPR / NT;
   constexpr int PER = PERH * NSPLIT;
-  constexpr bool kPrefetchRes = PER <= 8;
+  constexpr bool kPrefetchRes = !DE && PER <= 8;
   bf16x8 rpre[kPrefetchRes ? PER : 1];
   if (kPrefetchRes && p.res) {
     const bf16* R = reinterpret_cast<const bf16*>(p.res);
@@ -205,7 +210,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
   if (MODE == 3) {
 #pragma unroll
     for (int i = 0; i < A_INS; ++i) {
-      int c = a_lc[i] * 8, tap = 0;
+      int c = a_lc[i] * 8 + kb * BK, tap = 0;
       while (c >= p.Cin) { c -= p.Cin; ++tap; }
       g_tap[i] = tap;
       g_c[i] = c;
@@ -217,7 +222,14 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
   // k0 / Cin and tap / KW divisions (a ~20-instruction VALU expansion each: there is no
   // scalar divide) become a compare-and-bump on wave-uniform values
   int k_c0 = 0, k_r = 0, k_s = 0;
-  auto issue = [&](int stage, int kt) {
+  if (SK && MODE == 0 && kb > 0) {  // split-K: start the tap walk at this slice's first step
+    const int kbase = kb * BK, tap = kbase / p.Cin;
+    k_c0 = kbase - tap * p.Cin;
+    k_r = tap / p.KW;
+    k_s = tap - k_r * p.KW;
+  }
+  auto issue = [&](int stage, int kt_rel) {
+    const int kt = kt_rel + kb;  // absolute K step
     bf16* As = smem + stage * STAGE;
     bf16* Bs = As + BM * BK;
     if (MODE == 1) {
@@ -334,7 +346,7 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
     }
   };
 
-  const int nk = p.Kpad / BK;
+  const int nk = ke - kb;
   if constexpr (XP) {
     // v7 cross-stage pipeline.  The ring loop above opens every stage with its own
     // fragment reads AFTER the stage barrier, so each stage starts with an LDS-latency
@@ -443,6 +455,87 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land on the C tile
   }
+  if constexpr (SK) {
+    // ---- split-K: fp32 partial sums of this K slice into ws (no bias / act / residual:
+    // the finalize kernel applies them once).  A lane holds, per MFMA block, channels
+    // (MF 32) 8g + 4fh + j / (MF 16) 4fh + j of pixel fr.
+    float* __restrict__ ws = p.ws;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const int m = m0 + wm * WTM + tm * MF + fr;
+#pragma unroll
+        for (int e = 0; e < NACC; ++e) {
+          const int n = n0 + wn * WTN + tn * MF + (MF == 32 ? (e >> 2) * 8 : 0) + fh * 4 + (e & 3);
+          if (m < p.M && n < p.Cout) unsafeAtomicAdd(ws + (size_t)m * p.Cout + n, acc[tn][tm][e]);
+        }
+      }
+    return;
+  }
+  if constexpr (DE) {
+    // ---- direct epilogue (no LDS C tile, no barrier): each lane holds 4 consecutive
+    // channels of one pixel per 16x16 block; v_permlane16_swap between the blocks tn and
+    // tn+1 (row 1 of one register <-> row 0 of the other, rows 3 <-> 2) leaves every lane
+    // with 8 consecutive channels of its pixel -> one 16-B store per block pair (64 B per
+    // pixel per wave instruction).  Rows 0..3 of the wave (lane >> 4) end up holding
+    // channels [16 tn, +8), [16 (tn+1), +8), [16 tn + 8, +8), [16 (tn+1) + 8, +8).
+    static_assert(MF == 16 && TN % 2 == 0, "DE: 16x16x32 accumulators, block pairs");
+    const bool has_res = p.res != nullptr;
+    const __amdgpu_buffer_rsrc_t ry = make_rsrc(p.y, p.M * p.ldy * 2);
+    const __amdgpu_buffer_rsrc_t rr = make_rsrc(p.res, has_res ? p.M * p.ldr * 2 : 0);
+    const int rho = lane >> 4;
+    const int csel = 16 * (rho & 1) + 8 * (rho >> 1);  // channel offset within a block pair
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    dispatch_act(p.act, has_res, [&](auto A1, auto A2) __attribute__((always_inline)) {
+      constexpr int act1 = decltype(A1)::value, act2 = decltype(A2)::value;
+#pragma unroll
+      for (int tn = 0; tn < TN; tn += 2) {
+        const int nb = n0 + wn * WTN + tn * 16;  // first channel of the block pair
+        float4 bv0 = make_float4(0.f, 0.f, 0.f, 0.f), bv1 = bv0;
+        if (p.bias) {
+          if (nb + fh * 4 < p.Cout) bv0 = *reinterpret_cast<const float4*>(p.bias + nb + fh * 4);
+          if (nb + 16 + fh * 4 < p.Cout) bv1 = *reinterpret_cast<const float4*>(p.bias + nb + 16 + fh * 4);
+        }
+        const int n = nb + csel;
+        u32x4 rv[TM];
+        if (has_res) {
+#pragma unroll
+          for (int tm = 0; tm < TM; ++tm) {
+            const int m = m0 + wm * WTM + tm * 16 + fr;
+            const int off = (m < p.M && n < p.Cout) ? (m * p.ldr + p.r_coff + n) * 2 : kOOB;
+            rv[tm] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          bf16x4 a, b;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            a[j] = f2bf(act_c<act1>(acc[tn][tm][j] + (&bv0.x)[j]));
+            b[j] = f2bf(act_c<act1>(acc[tn + 1][tm][j] + (&bv1.x)[j]));
+          }
+          uint2 ua = __builtin_bit_cast(uint2, a), ub = __builtin_bit_cast(uint2, b);
+          {
+            const auto r0 = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
+            const auto r1 = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
+            ua.x = r0[0]; ub.x = r0[1];
+            ua.y = r1[0]; ub.y = r1[1];
+          }
+          bf16x8 v = __builtin_bit_cast(bf16x8, make_uint4(ua.x, ua.y, ub.x, ub.y));
+          if (has_res) {
+            const bf16x8 r = __builtin_bit_cast(bf16x8, rv[tm]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = f2bf(act_c<act2>((float)v[e] + (float)r[e]));
+          }
+          const int m = m0 + wm * WTM + tm * 16 + fr;
+          const int off = (m < p.M && n < p.Cout) ? (m * p.ldy + p.y_coff + n) * 2 : kOOB;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ry, off, 0, 0);
+        }
+      }
+    });
+    return;
+  }
   __syncthreads();
 
   // ---- fused epilogue through LDS (see conv_igemm.hip) ----------------------
@@ -502,14 +595,49 @@ __global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? 2 : 1) void conv_glds_
 
 typedef void (*ConvKernelFn)(const KvConvParams);
 
-template <int BM, int BN, int WM, int WN, int D = 2, int BKT = 64, int MF = 32, bool XP = false>
+template <int BM, int BN, int WM, int WN, int D = 2, int BKT = 64, int MF = 32, bool XP = false,
+          bool DE = false, bool SK = false>
 ConvKernelFn glds_get(int mode) {
   switch (mode) {
-    case 0: return conv_glds_kernel<BM, BN, WM, WN, 0, D, BKT, MF, XP>;
-    case 1: return conv_glds_kernel<BM, BN, WM, WN, 1, D, BKT, MF, XP>;
-    case 4: return conv_glds_kernel<BM, BN, WM, WN, 4, D, BKT, MF, XP>;
-    default: return conv_glds_kernel<BM, BN, WM, WN, 3, D, BKT, MF, XP>;
+    case 0: return conv_glds_kernel<BM, BN, WM, WN, 0, D, BKT, MF, XP, DE, SK>;
+    case 1: return conv_glds_kernel<BM, BN, WM, WN, 1, D, BKT, MF, XP, DE, SK>;
+    case 4: return conv_glds_kernel<BM, BN, WM, WN, 4, D, BKT, MF, XP, DE, SK>;
+    default: return conv_glds_kernel<BM, BN, WM, WN, 3, D, BKT, MF, XP, DE, SK>;
   }
+}
+
+// split-K finalize: y = act2(act1(ws + bias) (+ res)) -> bf16, and ws = 0 for the next layer
+__global__ __launch_bounds__(256) void splitk_finalize_kernel(
+    float* __restrict__ ws, const float* __restrict__ bias, const bf16* __restrict__ res,
+    bf16* __restrict__ y, int M, int Cout, int ldy, int y_coff, int ldr, int r_coff, int act) {
+  const int cpr = Cout >> 3;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)M * cpr) return;
+  const int m = (int)(idx / cpr), c = (int)(idx - (long long)m * cpr) * 8;
+  float4* src = reinterpret_cast<float4*>(ws + (size_t)m * Cout + c);
+  const float4 a0 = src[0], a1 = src[1];
+  src[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+  src[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+  float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  if (bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(bias + c);
+    const float4 b1 = *reinterpret_cast<const float4*>(bias + c + 4);
+    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+    v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+  }
+  bf16x8 o;
+  dispatch_act(act, res != nullptr, [&](auto A1, auto A2) __attribute__((always_inline)) {
+    constexpr int act1 = decltype(A1)::value, act2 = decltype(A2)::value;
+    bf16x8 r;
+    if (res) r = *reinterpret_cast<const bf16x8*>(res + (size_t)m * ldr + r_coff + c);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float u = act_c<act1>(v[e]);
+      if (res) u = act_c<act2>((float)f2bf(u) + (float)r[e]);
+      o[e] = f2bf(u);
+    }
+  });
+  *reinterpret_cast<bf16x8*>(y + (size_t)m * ldy + y_coff + c) = o;
 }
 
 struct GldsTile {
@@ -582,12 +710,42 @@ static const GldsTile kXpTiles[] = {
     {128, 128, &glds_get<128, 128, 2, 2, 4, 32, 16>},             // 64 KB
     {128, 128, &glds_get<128, 128, 2, 2, 5, 32, 16>},             // 80 KB
     {256, 128, &glds_get<256, 128, 4, 2, 4, 32, 16>, 512},        // 96 KB
+    // direct register epilogue (DE: v_permlane16_swap -> 16-B stores, no LDS C tile, no
+    // epilogue barrier) on the best 8-wave forms and the 2-per-CU 256 x 128
+    {256, 256, &glds_get<256, 256, 4, 2, 2, 64, 16, false, true>, 512},
+    {256, 256, &glds_get<256, 256, 2, 4, 5, 32, 16, true, true>, 512},
+    {256, 128, &glds_get<256, 128, 2, 2, 3, 32, 16, false, true>},
+    {128, 128, &glds_get<128, 128, 2, 2, 2, 64, 16, false, true>},
 };
 
 int xp_num_tiles() { return (int)(sizeof(kXpTiles) / sizeof(kXpTiles[0])); }
 
+// v8: split-K (edge batches: few output tiles, long K).  (instantiation, K slices)
+struct SkTile {
+  GldsTile t;
+  int split;
+};
+static const SkTile kSkTiles[] = {
+    {{64, 64, &glds_get<64, 64, 2, 2, 2, 64, 32, false, false, true>}, 4},
+    {{64, 64, &glds_get<64, 64, 2, 2, 2, 64, 32, false, false, true>}, 8},
+    {{64, 64, &glds_get<64, 64, 2, 2, 2, 64, 32, false, false, true>}, 16},
+    {{128, 64, &glds_get<128, 64, 2, 2, 2, 64, 32, false, false, true>}, 4},
+    {{128, 64, &glds_get<128, 64, 2, 2, 2, 64, 32, false, false, true>}, 8},
+    {{64, 128, &glds_get<64, 128, 2, 2, 2, 64, 32, false, false, true>}, 4},
+    {{64, 128, &glds_get<64, 128, 2, 2, 2, 64, 32, false, false, true>}, 8},
+    {{128, 128, &glds_get<128, 128, 2, 2, 2, 64, 16, false, false, true>}, 2},
+    {{128, 128, &glds_get<128, 128, 2, 2, 2, 64, 16, false, false, true>}, 4},
+    {{128, 128, &glds_get<128, 128, 2, 2, 2, 64, 16, false, false, true>}, 8},
+    {{256, 256, &glds_get<256, 256, 4, 2, 2, 64, 16, false, false, true>, 512}, 2},
+    {{256, 256, &glds_get<256, 256, 4, 2, 2, 64, 16, false, false, true>, 512}, 4},
+    {{256, 256, &glds_get<256, 256, 4, 2, 2, 64, 16, false, false, true>, 512}, 8},
+};
+
+int sk_num_tiles() { return (int)(sizeof(kSkTiles) / sizeof(kSkTiles[0])); }
+
 // mode here is the caller's (0 general, 1 gemm); picks MODE 0 vs 3 by Cin and taps.
-static int glds_launch_entry(const KvConvParams* p, const struct GldsTile& e, hipStream_t stream);
+static int glds_launch_entry(const KvConvParams* p, const struct GldsTile& e, hipStream_t stream,
+                             int split = 1);
 
 int glds_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   if (tile < 0 || tile >= glds_num_tiles()) return -6;
@@ -599,7 +757,24 @@ int xp_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   return glds_launch_entry(p, kXpTiles[tile], stream);
 }
 
-static int glds_launch_entry(const KvConvParams* p, const GldsTile& e, hipStream_t stream) {
+int sk_launch(const KvConvParams* p, int tile, hipStream_t stream) {
+  if (tile < 0 || tile >= sk_num_tiles()) return -6;
+  const SkTile& e = kSkTiles[tile];
+  const int nk = p->Kpad / BK;
+  if (!p->ws || e.split > nk) return -11;  // no workspace, or more slices than K steps
+  KvConvParams q = *p;
+  q.ksplit = e.split;
+  if (const int rc = glds_launch_entry(&q, e.t, stream, e.split)) return rc;
+  const long long thr = (long long)p->M * (p->Cout / 8);
+  if (thr <= 0) return 0;
+  hipLaunchKernelGGL(splitk_finalize_kernel, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0,
+                     stream, p->ws, p->bias, (const bf16*)p->res, (bf16*)p->y, p->M, p->Cout,
+                     p->ldy, p->y_coff, p->ldr, p->r_coff, p->act);
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
+static int glds_launch_entry(const KvConvParams* p, const GldsTile& e, hipStream_t stream,
+                             int split) {
   int mode = p->mode;
   if (mode == 2) return -8;  // legacy stem layout: v1 only
   if (mode == 0 && (p->Cin % 64 != 0 || p->KH * p->KW > 32)) mode = 3;
@@ -610,7 +785,8 @@ static int glds_launch_entry(const KvConvParams* p, const GldsTile& e, hipStream
     const long long x2b = (long long)p->N * p->H2 * p->W2 * p->ldx2 * 2;
     if (!p->x2 || x2b >= kOOB || p->K1 % BK || (p->Kpad - p->K1) % BK || p->ldx2 % 8) return -10;
   }
-  const long long nwg = (long long)((p->M + e.bm - 1) / e.bm) * ((p->Cout + e.bn - 1) / e.bn);
+  const long long nwg =
+      (long long)((p->M + e.bm - 1) / e.bm) * ((p->Cout + e.bn - 1) / e.bn) * split;
   if (nwg <= 0) return 0;
   hipLaunchKernelGGL(e.get(mode), dim3((unsigned)nwg), dim3(e.nt), 0, stream, *p);
   return hipGetLastError() == hipSuccess ? 0 : -7;

@@ -319,13 +319,16 @@ int nloop_sched_check();
 // v7 cross-stage pipelined LDS-DMA GEMM (conv_glds.hip XP loop): indices after v6
 int xp_num_tiles();
 int xp_launch(const KvConvParams* p, int tile, hipStream_t stream);
+// v8 split-K (conv_glds.hip SK kernels + finalize): indices after v7
+int sk_num_tiles();
+int sk_launch(const KvConvParams* p, int tile, hipStream_t stream);
 }  // namespace kvedge
 
 extern "C" int kv_nloop_sched_check(void) { return kvedge::nloop_sched_check(); }
 
 extern "C" int kv_conv_num_tiles(void) {
   return kNumTiles + glds_num_tiles() + stream_num_tiles() + direct_num_tiles() +
-         nloop_num_tiles() + xp_num_tiles();
+         nloop_num_tiles() + xp_num_tiles() + sk_num_tiles();
 }
 
 extern "C" int kv_conv_pick_tile(const KvConvParams* p) {
@@ -368,7 +371,7 @@ static int kv_conv_check_extents(const KvConvParams* p) {
                                     : (long long)p->N * p->H * p->W * p->ldx * 2)) return -20;
   if (!kv_in_alloc(p->w, (long long)p->Cout * p->Kpad * 2)) return -21;
   if (!kv_in_alloc(p->bias, (long long)p->Cout * 4)) return -22;
-  if (!kv_in_alloc(p->y, (p->y_s2 ? M / 4 : M) * p->ldy * 2)) return -23;
+  if (!kv_in_alloc(p->y, M * p->ldy * 2)) return -23;
   if (p->res && !kv_in_alloc(p->res, M * p->ldr * 2)) return -24;
   if (p->n_t && (!kv_in_alloc(p->z, M * p->ldz * 2) ||
                  !kv_in_alloc(p->w_t, (long long)p->n_t * p->Cout * 2) ||
@@ -389,7 +392,7 @@ static int kv_conv2d_one(const KvConvParams* p, int tile, hipStream_t stream);
 static long long kv_conv_max_image_bytes(const KvConvParams* p) {
   const long long hw = (long long)p->H * p->W, ohw = (long long)p->Ho * p->Wo;
   long long m = p->in_u8 ? hw * 12 : hw * p->ldx * 2;
-  m = std::max(m, (p->y_s2 ? ohw / 4 : ohw) * p->ldy * 2);
+  m = std::max(m, ohw * p->ldy * 2);
   if (p->res) m = std::max(m, ohw * p->ldr * 2);
   if (p->mode == 4) m = std::max(m, (long long)p->H2 * p->W2 * p->ldx2 * 2);
   if (p->n_t) m = std::max(m, ohw * p->ldz * 2);
@@ -427,7 +430,7 @@ extern "C" int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream) {
       return b ? static_cast<const char*>(b) + (long long)n0 * bytes_per_image : nullptr;
     };
     q.x = adv(p->x, p->in_u8 ? hw * 12 : hw * p->ldx * 2);
-    q.y = const_cast<char*>(adv(p->y, (p->y_s2 ? ohw / 4 : ohw) * p->ldy * 2));
+    q.y = const_cast<char*>(adv(p->y, ohw * p->ldy * 2));
     if (p->res) q.res = adv(p->res, ohw * p->ldr * 2);
     if (p->mode == 4) q.x2 = adv(p->x2, (long long)p->H2 * p->W2 * p->ldx2 * 2);
     if (p->n_t) q.z = const_cast<char*>(adv(p->z, ohw * p->ldz * 2));
@@ -438,7 +441,6 @@ extern "C" int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream) {
 
 static int kv_conv2d_one(const KvConvParams* p, int tile, hipStream_t stream) {
   if (p->Kpad % BK != 0 || p->Cout % 8 != 0) return -1;
-  if (p->y_s2 && (!p->n_t || p->Ho % 2 || p->Wo % 2)) return -8;  // compact y: tails only
   if (p->n_t) {  // fused bottleneck tail: the v3 tail tile only
     const int v3 = kNumTiles + glds_num_tiles();
     if (tile < 0) tile = v3 + stream_tail_tile(p->n_t);
@@ -466,7 +468,9 @@ static int kv_conv2d_one(const KvConvParams* p, int tile, hipStream_t stream) {
   const int v4 = v3 + stream_num_tiles();
   const int v6 = v4 + direct_num_tiles();
   const int v7 = v6 + nloop_num_tiles();
-  if (tile >= v7 + xp_num_tiles()) return -6;
+  const int v8 = v7 + xp_num_tiles();
+  if (tile >= v8 + sk_num_tiles()) return -6;
+  if (tile >= v8) return sk_launch(p, tile - v8, stream);
   if (tile >= v7) return xp_launch(p, tile - v7, stream);
   if (tile >= v6) return nloop_launch(p, tile - v6, stream);
   if (tile >= v4) return direct_launch(p, tile - v4, stream);

@@ -340,21 +340,9 @@ void conv_stream_kernel(const KvConvParams p) {
   };
 
   // act1/act2 compile-time: instantiated per activation pair by dispatch_act() below
-  // y_s2 (tails): pixel -> (image, ho, wo) without a per-store integer divide (a runtime
-  // divide is ~40 VALU; per store it made the stage-1 tail 19 % slower): the tile base is
-  // split once per tile, rows inside the tile advance by exact 16-bit FastDivs
-  const FastDiv fWo = make_fastdiv(p.Wo > 0 ? p.Wo : 1), fHo = make_fastdiv(p.Ho > 0 ? p.Ho : 1);
   auto epilogue = [&](int ti, const ResRegs& rres, auto A1, auto A2) __attribute__((always_inline)) {
     constexpr int act1 = decltype(A1)::value, act2 = decltype(A2)::value;
     const int m0 = (mfirst + ti * mstep) * BM;
-    int img0 = 0, ho0 = 0, wo0 = 0;
-    if (NT1 > 0 && p.y_s2) {
-      const int hw = p.Ho * p.Wo;
-      img0 = __builtin_amdgcn_readfirstlane(m0 / hw);
-      const int r0 = m0 - img0 * hw;
-      ho0 = __builtin_amdgcn_readfirstlane(r0 / p.Wo);
-      wo0 = r0 - ho0 * p.Wo;
-    }
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
 #pragma unroll
@@ -389,18 +377,7 @@ void conv_stream_kernel(const KvConvParams p) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = f2bf(act_c<act2>((float)v[e] + (float)rv[e]));
       }
-      int off = (m < p.M && n < p.Cout) ? (m * p.ldy + p.y_coff + n) * 2 : kOOB;
-      if (NT1 > 0 && p.y_s2) {  // even (ho, wo) only, compacted: [N, Ho/2, Wo/2, ldy]
-        const int t = wo0 + ml;                   // < Wo + BM < 2^16: exact FastDiv
-        const int dh = fdiv(t, fWo);
-        const int wo = t - dh * p.Wo;
-        int ho = ho0 + dh;
-        const int di = fdiv(ho, fHo);
-        ho -= di * p.Ho;
-        const int img = img0 + di;
-        const int m2 = (img * (p.Ho >> 1) + (ho >> 1)) * (p.Wo >> 1) + (wo >> 1);
-        off = ((ho | wo) & 1) ? kOOB : (off == kOOB ? kOOB : (m2 * p.ldy + p.y_coff + n) * 2);
-      }
+      const int off = (m < p.M && n < p.Cout) ? (m * p.ldy + p.y_coff + n) * 2 : kOOB;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ry, off, 0, SP);
       if constexpr (NT1 > 0) *reinterpret_cast<bf16x8*>(Cs + ml * CS + ch * 8) = v;
     }

@@ -49,11 +49,11 @@ typedef struct KvConvParams {
   const float* bias_t;
   void* z;
   int n_t, ldz, z_coff, act_t;
-  // y_s2 = 1 (fused tail only, Ho and Wo even): y is written ONLY at pixels with even
-  // (ho, wo), compacted to [N, Ho/2, Wo/2, ldy] -- for a y whose only other consumer is
-  // the next stage's stride-2 downsample (ResNet-50 stage 1 -> 2: the next conv1 runs in
-  // the tail, the stride-2 1x1 reads 1/4 of the pixels), 3/4 of its bytes are never written.
-  int y_s2;
+  // Split-K (v8 tiles, small-M layers: edge batches): the launch adds fp32 partial sums
+  // of its K slice into ws [M][Cout] (zero on entry) and a finalize kernel applies bias,
+  // residual and activation, writes y and zeroes ws again.  ws = NULL: v8 tiles refuse.
+  float* ws;
+  int ksplit;
 } KvConvParams;
 
 // tile: -1 = heuristic; otherwise an index into the tile table (kv_conv_num_tiles()).

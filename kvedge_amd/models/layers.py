@@ -148,15 +148,14 @@ class DeployedDualConv:
                                 (b3 + bd).contiguous().to(device), w3.shape[1],
                                 down_conv.stride[0], act)
 
-    def __call__(self, y, x, out=None, tile=None, stride2=None):
-        """``stride2``: override (1 when ``x`` is an already-subsampled, compact tensor)."""
-        s2 = self.stride2 if stride2 is None else stride2
-        out = ops.conv_dual(y, x, self.w, self.b, self.act, s2, out=out,
+    def __call__(self, y, x, out=None, tile=None):
+        out = ops.conv_dual(y, x, self.w, self.b, self.act, self.stride2, out=out,
                             tile=self.tile if tile is None else tile)
         if _RECORDER is not None:
-            key = ("dual", tuple(y.shape), tuple(x.shape), tuple(self.w.shape), s2, self.act)
+            key = ("dual", tuple(y.shape), tuple(x.shape), tuple(self.w.shape), self.stride2,
+                   self.act)
             fn = lambda t, o=out: ops.conv_dual(y, x, self.w, self.b, self.act,  # noqa: E731
-                                                s2, out=o, tile=t)
+                                                self.stride2, out=o, tile=t)
             _RECORDER.append((self, key, fn))
         return out
 

@@ -127,14 +127,12 @@ class DeployedBottleneck:
                 self.dual = DeployedDualConv.from_modules(b.conv3, b.bn3, b.downsample[0],
                                                           b.downsample[1], ACT_RELU, device)
 
-    def __call__(self, x, out=None, t1=None, x_s2=False):
-        """t1: this block's conv1 output when a previous fused tail already computed it.
-        x_s2: ``x`` holds only the even pixels of the block input (the previous tail's
-        ``y_s2`` form, valid when t1 is given): the fused downsample reads it at stride 1."""
+    def __call__(self, x, out=None, t1=None):
+        """t1: this block's conv1 output when a previous fused tail already computed it."""
         y = self.c1(x) if t1 is None else t1
         y = self.c2(y)
         if self.dual is not None:
-            return self.dual(y, x, out=out, stride2=1 if x_s2 else None)
+            return self.dual(y, x, out=out)
         idt = x if self.down is None else self.down(x)
         return self.c3(y, res=idt, out=out)
 
@@ -149,28 +147,18 @@ class DeployedBottleneck:
                 self.c3.spec.act == ACT_RELU and (self.dual is not None or self.down is None) and
                 (self.dual is None or c1.cout == 64) and k <= 128)
 
-    def call_tail(self, x, nxt: "DeployedBottleneck", t1=None, out=None, z=None,
-                  y_s2: bool = False):
+    def call_tail(self, x, nxt: "DeployedBottleneck", t1=None, out=None, z=None):
         """-> (this block's output y, the next block's conv1 output z) in one fused pass.
-        ``out``/``z``: preallocated destinations (micro-batch slices of full-batch tensors).
-        ``y_s2``: return only y's even pixels (see :meth:`tail_y_s2`)."""
+        ``out``/``z``: preallocated destinations (micro-batch slices of full-batch tensors)."""
         y = self.c1(x) if t1 is None else t1
         y = self.c2(y)
         c1 = nxt.c1
         if self.dual is not None:
             d = self.dual
             return ops.conv_tail(y, d.w, d.b, d.act, c1.w, c1.b, x2=x, stride2=d.stride2,
-                                 out=out, z=z, y_s2=y_s2)
+                                 out=out, z=z)
         return ops.conv_tail(y, self.c3.w, self.c3.b, self.c3.spec.act, c1.w, c1.b, res=x,
-                             out=out, z=z, y_s2=y_s2)
-
-    @staticmethod
-    def tail_y_s2(nxt: "DeployedBottleneck", after: Optional["DeployedBottleneck"]) -> bool:
-        """Whether a tail into ``nxt`` may write y at even pixels only: nxt's conv1 runs in
-        the tail (z), nxt's only other use of y is its fused stride-2 downsample, and nxt
-        itself is not tailed into ``after`` (a tail would read y as a full residual)."""
-        return (nxt.dual is not None and nxt.dual.stride2 == 2 and nxt.c2.spec.stride == 2 and
-                (after is None or not nxt.can_tail(after)))
+                             out=out, z=z)
 
     def can_block(self, nxt: "DeployedBottleneck") -> bool:
         """conv2 (3x3, 64 -> 64, stride 1) + the fused tail as ONE kernel (ops.conv_block):
@@ -262,9 +250,6 @@ class KvResNet50:
     # one workgroup per CU, cannot overlap its 3x3 phase with its memory phase, and measures
     # level with or slower than direct + tail (docs/kernels.md, profiles/r2_v8_block_probe.md)
     fuse_block: bool = False
-    # a tail whose y feeds only the next block's stride-2 downsample (stage 1 -> 2) writes
-    # y at even pixels only: 0.77 GB less HBM write traffic per 640 images
-    tail_s2: bool = True
 
     # frames-in stem: the 12-channel s2d kernel (stem12.hip, K 192, two workgroups per CU)
     # instead of the 16-channel one (stem_pool.hip, K 256)
@@ -314,21 +299,15 @@ class KvResNet50:
         else:
             x = self.stem_and_pool(x, frames_in)
             rest = self.blocks
-        x_s2 = False  # x holds only the even pixels (a y_s2 tail's output)
         for i, b in enumerate(rest):
             nxt = rest[i + 1] if i + 1 < len(rest) else None
-            after = rest[i + 2] if i + 2 < len(rest) else None
             if (self.fuse_block and x.is_cuda and nxt is not None and b.can_block(nxt) and
                     ops.conv_block_fits(x)):
                 x, t1 = b.call_block(x, nxt, t1=t1)
             elif self.fuse_tail and x.is_cuda and nxt is not None and b.can_tail(nxt):
-                ys2 = self.tail_s2 and DeployedBottleneck.tail_y_s2(nxt, after)
-                x, t1 = b.call_tail(x, nxt, t1=t1, y_s2=ys2)
-                x_s2 = ys2
-                continue
+                x, t1 = b.call_tail(x, nxt, t1=t1)
             else:
-                x, t1 = b(x, t1=t1, x_s2=x_s2), None
-            x_s2 = False
+                x, t1 = b(x, t1=t1), None
         return x
 
     def logits(self, x: torch.Tensor, frames_in: bool = False) -> torch.Tensor:

@@ -60,6 +60,8 @@ def load(build_if_missing: bool = False) -> bool:
         _load_error = f"failed to load {_LIB_PATH}: {e}"
         return False
     _check_single_hip_runtime()
+    global SPLITK0
+    SPLITK0 = int(torch.ops.kvedge.conv_num_tiles()) - N_SPLITK_TILES
     _loaded = True
     return True
 
@@ -193,6 +195,27 @@ def unpack_conv_weight(wp: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
 # ---------------------------------------------------------------------------
 # ops
 # ---------------------------------------------------------------------------
+# Split-K workspaces (v8 tiles): fp32, all zero between uses -- the finalize kernel of every
+# split-K layer zeroes what it read -- one per (device, stream), since layers on one stream
+# run in order while the multi-stream engine's slices run concurrently.  Sized on first use
+# (warm-up, before hipGraph capture), grown when a larger layer needs it.
+_WS: dict = {}
+SPLITK_MAX_ELEMS = 16 << 20  # layers with M*Cout above this never split (64 MB of fp32)
+N_SPLITK_TILES = 13          # conv_glds.hip kSkTiles: the LAST tile indices
+SPLITK0 = 1 << 30            # first split-K tile index, set by load()
+
+
+def splitk_workspace(device: torch.device, elems: int) -> Optional[torch.Tensor]:
+    if elems > SPLITK_MAX_ELEMS:
+        return None
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < elems:
+        ws = torch.zeros(max(elems, 1 << 16), dtype=torch.float32, device=device)
+        _WS[key] = ws
+    return ws
+
+
 def conv2d(x: torch.Tensor, spec: ConvSpec, w: torch.Tensor, bias: Optional[torch.Tensor],
            res: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
            x_coff: int = 0, y_coff: int = 0, r_coff: int = 0, tile: int = -1) -> torch.Tensor:
@@ -205,9 +228,10 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, w: torch.Tensor, bias: Optional[torc
     ldy = out.shape[3]
     ldr = res.shape[-1] if res is not None else 0
     if x.is_cuda:
+        ws = splitk_workspace(x.device, N * Ho * Wo * spec.cout) if tile >= SPLITK0 else None
         _native().conv(x, w, bias, res, out, N, H, W, spec.cin_eff, ldx, x_coff, Ho, Wo,
                        spec.cout, spec.kh, spec.kw, spec.stride, spec.pad, spec.K, ldy, y_coff,
-                       ldr, r_coff, spec.act, spec.mode, tile)
+                       ldr, r_coff, spec.act, spec.mode, tile, ws)
     else:
         _ref.conv2d(x, spec, w, bias, res, out, x_coff, y_coff, r_coff)
     return out
@@ -224,7 +248,8 @@ def conv_dual(x1: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, bias: Optiona
     if out is None:
         out = empty(N, Ho, Wo, cout, dtype=torch.bfloat16, device=x1.device)
     if x1.is_cuda:
-        _native().conv_dual(x1, x2, w, bias, out, stride2, act, tile)
+        ws = splitk_workspace(x1.device, N * Ho * Wo * cout) if tile >= SPLITK0 else None
+        _native().conv_dual(x1, x2, w, bias, out, stride2, act, tile, ws)
     else:
         _ref.conv_dual(x1, x2, w, bias, act, stride2, out)
     return out
@@ -234,35 +259,27 @@ def conv_tail(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], ac
               w1: torch.Tensor, b1: Optional[torch.Tensor], res: Optional[torch.Tensor] = None,
               x2: Optional[torch.Tensor] = None, stride2: int = 1,
               out: Optional[torch.Tensor] = None, z: Optional[torch.Tensor] = None,
-              tile: int = -1, y_s2: bool = False):
+              tile: int = -1):
     """Fused bottleneck tail: y = act(x . W^T + bias + res) -- or, with ``x2``, the dual
     conv3 + downsample GEMM of :func:`conv_dual` -- AND z = ReLU(y . w1^T + b1), the next
     block's 1x1 reduce conv, in one pass: y is written once and never re-read from HBM.
-    w: packed [Cout, K] (1x1); w1: packed [n_t, Cout].  Returns (y, z).
-
-    ``y_s2``: y is returned as y[:, ::2, ::2] only ([N, H/2, W/2, Cout]; z stays full): the
-    form for a y whose only other reader is a stride-2 downsample -- 3/4 of its HBM
-    writes disappear (ResNet-50's stage-1 -> stage-2 boundary)."""
+    w: packed [Cout, K] (1x1); w1: packed [n_t, Cout].  Returns (y, z)."""
     N, H, W, _ = x.shape
     cout, nt = w.shape[0], w1.shape[0]
     if out is None:
-        out = (empty(N, H // 2, W // 2, cout, dtype=torch.bfloat16, device=x.device) if y_s2
-               else empty(N, H, W, cout, dtype=torch.bfloat16, device=x.device))
+        out = empty(N, H, W, cout, dtype=torch.bfloat16, device=x.device)
     if z is None:
         z = empty(N, H, W, nt, dtype=torch.bfloat16, device=x.device)
     if x.is_cuda:
         _native().conv_tail(x, x2, w, bias, res, out, w1, b1, z, stride2, act, tile)
         return out, z
-    full = empty(N, H, W, cout, dtype=torch.bfloat16, device=x.device) if y_s2 else out
     if x2 is not None:
-        _ref.conv_dual(x, x2, w, bias, act, stride2, full)
+        _ref.conv_dual(x, x2, w, bias, act, stride2, out)
     else:
         spec = ConvSpec.auto(x.shape[3], cout, 1, 1, 0, act)
-        _ref.conv2d(x, spec, w, bias, res, full, 0, 0, 0)
+        _ref.conv2d(x, spec, w, bias, res, out, 0, 0, 0)
     spec1 = ConvSpec.auto(cout, nt, 1, 1, 0, ACT_RELU)
-    _ref.conv2d(full, spec1, w1, b1, None, z, 0, 0, 0)
-    if y_s2:
-        out.copy_(full[:, ::2, ::2])
+    _ref.conv2d(out, spec1, w1, b1, None, z, 0, 0, 0)
     return out, z
 
 

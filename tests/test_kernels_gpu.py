@@ -103,11 +103,13 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale
 
 
-N_TILES = 80  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 (68-79)
+N_TILES = 97  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue (68-83) + v8 split-K (84-96)
 # + v6 A-resident N-loop 1x1 GEMM (58-67, conv_nloop.hip kNlTiles: one Kpad per tile;
 # 63-65 are the fused-downsample (dual) forms, 66-67 step 128 K at a time)
 NLOOP0 = 58
 XP0 = 68  # v7: the v2 kernel's cross-stage pipelined loop (BK 32 rings, 8 waves)
+SK0 = 84  # v8: split-K (conv_glds.hip kSkTiles): K slices per tile
+SK_SPLITS = [4, 8, 16, 4, 8, 4, 8, 2, 4, 8, 2, 4, 8]
 NLOOP_KPAD = [128, 256, 256, 256, 256, 384, 384, 768, 256, 256]
 NLOOP_DUAL = {63, 64, 65}
 STREAM0 = 32  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
@@ -157,6 +159,11 @@ def test_conv_every_tile(tile, case):
         except RuntimeError:
             return
         assert err <= 0.02 * scale, (tile, case, err, scale)
+        return
+    if tile >= SK0 and SK_SPLITS[tile - SK0] > (cin * k * k + 63) // 64:
+        with pytest.raises(RuntimeError):  # more K slices than K steps
+            _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
+                       tile=tile)
         return
     if STREAM0 <= tile < DIRECT0 and (k != 1 or s != 1 or not _stream_fits(tile, (cin * k * k + 63) // 64 * 64, res)):
         with pytest.raises(RuntimeError):
@@ -346,6 +353,10 @@ def test_conv_dual_fused_downsample(tile, geom):
     w = (torch.randn(cout, K1 + K2, generator=g) * 0.05).to(torch.bfloat16)
     b = torch.randn(cout, generator=g)
     ref = ops.conv_dual(x1, x2, w, b, ops.ACT_RELU, s)
+    if tile >= SK0 and SK_SPLITS[tile - SK0] > (K1 + K2) // 64:
+        with pytest.raises(RuntimeError):
+            ops.conv_dual(x1.cuda(), x2.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, s, tile=tile)
+        return
     if NLOOP0 <= tile < XP0 and (tile not in NLOOP_DUAL or K1 + K2 != NLOOP_KPAD[tile - NLOOP0]):
         with pytest.raises(RuntimeError):  # each v6 dual tile is compiled for one K
             ops.conv_dual(x1.cuda(), x2.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, s, tile=tile)
@@ -368,7 +379,7 @@ def test_conv_dual_rejects_v1_tiles():
 
 
 @pytest.mark.parametrize("tile", [-1, 1, 6, 7, 12, 13, STREAM0, STREAM0 + 1, STREAM0 + 5, DIRECT0,
-                                  DIRECT0 + 1, XP0, XP0 + 4])
+                                  DIRECT0 + 1, XP0, XP0 + 4, SK0, SK0 + 9])
 @pytest.mark.parametrize("k", [1, 3])
 def test_conv_poisoned_canary(tile, k):
     """SURVEY §5.2 poisoned-buffer check: the output buffer is NaN-filled, with a NaN
@@ -550,36 +561,25 @@ def test_conv_tail_fused(case, mf):
         _assert_close(got.cpu(), ref, ("tail", case, mf))
 
 
+
+@pytest.mark.parametrize("tile", list(range(SK0, N_TILES)))
 @pytest.mark.parametrize("case", [
-    # (N, H, W, k1, k2, stride2, n_t)
-    (2, 56, 56, 64, 0, 1, 128),    # layer1 block 2 -> layer2 (the deployed y_s2 site)
-    (3, 14, 10, 64, 0, 1, 64),     # M tail, odd tile splits
-    (2, 28, 28, 64, 64, 1, 64),    # dual form
+    # (N, H, W, cin, cout, k, stride, act, res) -- ResNet-50 edge-batch shapes
+    (1, 14, 14, 256, 256, 3, 1, ops.ACT_RELU, False),     # s3 3x3 at batch 1: M 196
+    (1, 7, 7, 512, 512, 3, 1, ops.ACT_RELU, False),       # s4 3x3: M 49, K 4608
+    (1, 7, 7, 512, 2048, 1, 1, ops.ACT_RELU, True),       # s4 conv3 + residual
+    (2, 14, 14, 1024, 256, 1, 1, ops.ACT_RELU, False),    # s3 conv1, M tail
+    (1, 14, 14, 512, 512, 3, 2, ops.ACT_RELU, False),     # s4 block-0 3x3 / 2
 ])
-def test_conv_tail_even_pixels_only(case):
-    """y_s2 tail: y written only at even (h, w), compacted to [N, H/2, W/2, C]; z full.
-    The destination is NaN-filled with a canary tail: nothing past it may be written."""
-    N, H, W, k1, k2, s2, nt = case
-    cout = 256
-    g = torch.Generator().manual_seed(H + nt)
-    t = _rand((N, H, W, k1), 4)
-    w = (torch.randn(cout, k1 + k2, generator=g) * (2.0 / (k1 + k2)) ** 0.5).to(torch.bfloat16)
-    b = torch.randn(cout, generator=g) * 0.1
-    w1 = (torch.randn(nt, cout, generator=g) * (2.0 / cout) ** 0.5).to(torch.bfloat16)
-    b1 = torch.randn(nt, generator=g) * 0.1
-    kw = {}
-    if k2:
-        kw = {"x2": _rand((N, H * s2, W * s2, k2), 5), "stride2": s2}
-    else:
-        kw = {"res": _rand((N, H, W, cout), 6)}
-    y_ref, z_ref = ops.conv_tail(t, w, b, ops.ACT_RELU, w1, b1, **kw)
-    n_y = N * (H // 2) * (W // 2) * cout
-    flat = torch.full((n_y + 4096,), float("nan"), dtype=torch.bfloat16, device="cuda")
-    y = flat[:n_y].view(N, H // 2, W // 2, cout)
-    gkw = {k: (v.cuda() if torch.is_tensor(v) else v) for k, v in kw.items()}
-    y, z = ops.conv_tail(t.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, w1.cuda(), b1.cuda(),
-                         out=y, y_s2=True, **gkw)
+def test_conv_splitk(tile, case):
+    """v8 split-K: K slices add fp32 partials into the stream's workspace, the finalize
+    kernel applies bias / residual / activation, writes bf16 and re-zeroes the workspace
+    (checked: the next split-K layer on the stream relies on it)."""
+    N, H, W, cin, cout, k, s, act, res = case
+    if SK_SPLITS[tile - SK0] > (cin * k * k + 63) // 64:
+        return
+    err, scale = _conv_case(N, H, W, cin, cout, k, s, k // 2, act, res=res, tile=tile)
+    assert err <= 0.02 * scale, (tile, case, err, scale)
+    ws = ops.splitk_workspace(torch.device("cuda", torch.cuda.current_device()), 1)
     torch.cuda.synchronize()
-    assert torch.isnan(flat[n_y:].cpu().float()).all()
-    _assert_close(y.cpu(), y_ref[:, ::2, ::2], ("y_s2", case))
-    _assert_close(z.cpu(), z_ref, ("z", case))
+    assert int((ws != 0).sum()) == 0

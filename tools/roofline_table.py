@@ -38,12 +38,8 @@ def layers(B):
     for b, (dual, nt) in enumerate(((True, 64), (False, 64), (False, 128))):
         L.append((f"s1.b{b} conv2 3x3 64>64", "conv", 2 * t(B, 56, 64), gemm(m1, 576, 64)))
         src = t(B, 56, 64) if dual else t(B, 56, 256)
-        # block 2's y feeds only s2.b0's stride-2 downsample (its conv1 runs in this tail):
-        # it is written at even pixels only (KvResNet50.tail_s2)
-        yb = t(B, 28, 256) if b == 2 else t(B, 56, 256)
-        L.append((f"s1.b{b} tail conv3{'+down' if dual else '+res'} -> next conv1 ({nt})"
-                  + (" [y even px]" if b == 2 else ""), "conv",
-                  t(B, 56, 64) + src + yb + t(B, 56, nt),
+        L.append((f"s1.b{b} tail conv3{'+down' if dual else '+res'} -> next conv1 ({nt})", "conv",
+                  t(B, 56, 64) + src + t(B, 56, 256) + t(B, 56, nt),
                   gemm(m1, 64 + (64 if dual else 0), 256) + gemm(m1, 256, nt)))
     m2 = B * 28 * 28
     L.append(("s2.b0 conv2 3x3/2 128>128", "conv", t(B, 56, 128) + t(B, 28, 128), gemm(m2, 1152, 128)))
