@@ -163,3 +163,26 @@ def test_engine_streams_cpu_and_split_check():
     assert torch.equal(_cat_outputs([a, b]), torch.arange(12).view(4, 3))
     t = _cat_outputs([(a, a[:, 0]), (b, b[:, 0])])
     assert torch.equal(t[0], torch.arange(12).view(4, 3)) and t[1].tolist() == [0, 3, 6, 9]
+
+
+def test_op_roofline_flops_match_model():
+    """tools/op_roofline.py's per-op FLOPs (derived from each op call's own arguments) sum to
+    the reference architecture's FLOPs exactly, so its floors price the real model."""
+    import importlib.util
+    import os
+
+    from kvedge_amd import ops
+    from kvedge_amd.models.yolov8 import KvYoloV8n, init_yolov8n
+
+    path = os.path.join(os.path.dirname(__file__), "..", "tools", "op_roofline.py")
+    spec = importlib.util.spec_from_file_location("op_roofline", path)
+    R = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(R)
+    m = KvYoloV8n(init_yolov8n(seed=0, calibrate=False), "cpu")
+    fr = torch.randint(0, 256, (1, 96, 96, 3), dtype=torch.uint8)
+    with torch.no_grad():
+        rows = R.costs_only(m, fr, ops)
+    assert sum(r[2] for r in rows) == m.flops_per_image(96)
+    assert rows[0][0].startswith("stem") and rows[-1][0] == "nms"
+    assert all(r[1] > 0 for r in rows)
+    assert ops.conv2d.__name__ == "conv2d"  # wrappers removed
