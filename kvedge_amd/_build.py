@@ -53,6 +53,18 @@ def _headers():
     return glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
 
 
+def _incs(src: str):
+    """``#include "*.inc"`` files of a source (shared kernel bodies split over several
+    translation units, e.g. conv_glds_kernel.inc): dependencies of that source only."""
+    d = os.path.dirname(src)
+    out = []
+    with open(src) as f:
+        for line in f:
+            if line.startswith('#include "') and line.rstrip().endswith('.inc"'):
+                out.append(os.path.join(d, line.split('"')[1]))
+    return out
+
+
 def _stale(target: str, deps) -> bool:
     if not os.path.exists(target):
         return True
@@ -99,7 +111,7 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = False, asan: bool 
     for src in kernel_srcs:
         o = os.path.join(OBJ, os.path.basename(src) + ".o")
         objs.append(o)
-        if force or _stale(o, [src] + headers):
+        if force or _stale(o, [src] + headers + _incs(src)):
             tasks.append([hipcc(), *COMMON, f"-I{CSRC}/kernels", "-c", src, "-o", o])
     for src in runtime_srcs:
         o = os.path.join(OBJ, os.path.basename(src) + ".o")

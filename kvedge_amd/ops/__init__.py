@@ -201,7 +201,7 @@ def unpack_conv_weight(wp: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
 # (warm-up, before hipGraph capture), grown when a larger layer needs it.
 _WS: dict = {}
 SPLITK_MAX_ELEMS = 16 << 20  # layers with M*Cout above this never split (64 MB of fp32)
-N_SPLITK_TILES = 13          # conv_glds.hip kSkTiles: the LAST tile indices
+N_SPLITK_TILES = 13          # conv_sk.hip kSkTiles: the LAST tile indices
 SPLITK0 = 1 << 30            # first split-K tile index, set by load()
 
 
