@@ -137,6 +137,17 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
       const_cast<void*>(p.x), (short)0, U8 ? p.N * H * W * 12 : p.N * H * W * p.ldx * 2,
       0x00020000);
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  // Stride 2: patch row positions hold the EVEN input columns first, then the odd ones
+  // (column pc at pc / 2, or HALF + pc / 2).  Neighbouring output pixels then read
+  // neighbouring positions for every tap, at a pitch of PB = 16 x odd bytes: a ds_read_b128
+  // lane group's 16 reads hit 16 distinct 16-B bank slots.  In column order the pitch was
+  // 2 x PB (an even number of slots): every MFMA operand read 2-way conflicted
+  // (SQ_LDS_BANK_CONFLICT 17-33 M per stride-2 launch, profiles/r2_v2_yolov8n_b384_pmc.md).
+  const int HALF = (PW + 1) >> 1;
+  auto col_of = [&](int pos) __attribute__((always_inline)) {
+    if constexpr (S == 2) return pos < HALF ? 2 * pos : 2 * (pos - HALF) + 1;
+    return pos;
+  };
   // chunk q -> (patch pixel pp, 16-B chunk c).  U8: q = (pr*2 + c)*PW + pc, so consecutive
   // lanes walk one raw frame row (coalesced 6-B groups); otherwise pixel-major.
   auto chunk_of = [&](int q, int& pp, int& c) __attribute__((always_inline)) {
@@ -189,7 +200,7 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
       const int q = tid + NT * i;
       int pp, c;
       chunk_of(q, pp, c);
-      const int pr = fdiv(pp, fPW), pc = pp - pr * PW;
+      const int pr = fdiv(pp, fPW), pc = col_of(pp - pr * PW);
       const int iy = iy0 + pr, ix = pc - PADK;
       const bool ok = live && q < nchunks && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
       if constexpr (U8) {
@@ -248,14 +259,23 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
   constexpr int SL = C::PB / 16;  // 16-B slots per patch pixel (CPP data + 1 padding)
   const int nslots = patch_rows * PW * SL;
   const kv_i32x4 rx4 = kv_rsrc4(p.x, U8 ? 0 : p.N * H * W * p.ldx * 2);
+  // DMA forms without a residual split the waves by role: the first half issues every patch
+  // DMA, the second half every output store.  On gfx9 vmcnt counts stores too, so a wave
+  // that stored the band and then waited for its next-patch DMA (vmcnt(0)) also waited for
+  // its stores to be acknowledged -- one HBM write latency per band on every CU.  Split, the
+  // DMA waves have no stores outstanding and the store waves never wait on vmcnt.
+  constexpr int NWV = NT / 64;
+  constexpr bool SPLIT = DMA && !RES && NWV >= 4;
+  constexpr int NWD = SPLIT ? NWV / 2 : NWV;  // waves issuing the patch DMA
   auto dma_fetch = [&](int item, unsigned char* dst) __attribute__((always_inline)) {
     const int n = item / nbands, band = item - n * nbands;
     const int iy0 = band * kR * S - PADK;
     const bool live = item < total;
-    for (int j = wv; j * 64 < nslots; j += NT / 64) {  // one 1-KB DMA per wave per j
+    if (SPLIT && wv >= NWD) return;
+    for (int j = wv; j * 64 < nslots; j += NWD) {  // one 1-KB DMA per wave per j
       const int q = j * 64 + lane;
       const int pp = q / SL, c = q - pp * SL;
-      const int pr = fdiv(pp, fPW), pc = pp - pr * PW;
+      const int pr = fdiv(pp, fPW), pc = col_of(pp - pr * PW);
       const int iy = iy0 + pr, ix = pc - PADK;
       const bool ok = live && q < nslots && c < C::CPP && (unsigned)iy < (unsigned)H &&
                       (unsigned)ix < (unsigned)W;
@@ -323,10 +343,16 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
     for (int b = ph < NPH ? ph : nblk; b < nblk; b += NPH) {
       const int j = min(b * 32 + fr, npix - 1);  // clamp: pixels past npix are discarded
       const int yl = fdiv(j, fWo), xc = j - yl * Wo;
-      const unsigned char* pa0 = pbase + (yl * S * PW + xc * S) * C::PB + fh * 16;
+      // stride 2: tap column s of output column xc sits at position xc + s / 2 (even s) or
+      // HALF + xc (s = 1)
+      const unsigned char* pa0 = pbase + (yl * S * PW + xc * (S == 2 ? 1 : S)) * C::PB + fh * 16;
       const unsigned char* pa[KK];
+      const unsigned char* po[KK];
 #pragma unroll
-      for (int r = 0; r < KK; ++r) pa[r] = pa0 + r * rowb;
+      for (int r = 0; r < KK; ++r) {
+        pa[r] = pa0 + r * rowb;
+        po[r] = pa[r] + (S == 2 ? HALF * C::PB : 0);
+      }
       floatx16 acc;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -344,7 +370,10 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
       auto load = [&](int buf, int kk) __attribute__((always_inline)) {
         const int tap = kk / C::KPT, s4 = kk - (kk / C::KPT) * C::KPT;
         const int r = tap / KK, s = tap - (tap / KK) * KK;
-        af[buf] = *reinterpret_cast<const bf16x8*>(pa[r] + s * C::PB + s4 * 32);
+        if (S == 2 && s == 1)
+          af[buf] = *reinterpret_cast<const bf16x8*>(po[r] + s4 * 32);
+        else
+          af[buf] = *reinterpret_cast<const bf16x8*>(pa[r] + (S == 2 ? s / 2 : s) * C::PB + s4 * 32);
       };
 #pragma unroll
       for (int kk = 0; kk < PD; ++kk) load(kk, kk);
@@ -399,7 +428,9 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
         }
       }
     }
-    for (int q = RPF > 0 && rpre ? npix * OCH : tid; q < npix * OCH; q += NT) {
+    constexpr int SB = SPLIT ? NWD * 64 : 0;  // first storing thread
+    for (int q = RPF > 0 && rpre ? npix * OCH : tid - SB; q < npix * OCH; q += NT - SB) {
+      if (SPLIT && q < 0) break;  // a DMA wave
       const int px = q / OCH, c = q - (q / OCH) * OCH;
       const int yl = fdiv(px, fWo), xc = px - yl * Wo;
       const int oy = oy0 + yl;
@@ -416,7 +447,7 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
       *reinterpret_cast<uint4*>(Y + m * p.ldy + p.y_coff + c * 8) = v;
     }
     if constexpr (DMA) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs landed
+      if (!SPLIT || wv < NWD) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // DMAs landed
       cur ^= 1;
     }
     __syncthreads();  // patch ready, output tile free

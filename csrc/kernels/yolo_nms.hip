@@ -143,6 +143,9 @@ __device__ __forceinline__ bool iou_gt(float ax1, float ay1, float ax2, float ay
 }
 
 constexpr int kNmsWaves = 8;
+constexpr int kSel = 1024;     // top-set target size
+constexpr int kSelMax = 2048;  // top-set capacity (a wider threshold bin -> full sort)
+constexpr int kBins = 2048;    // score-bit histogram bins
 
 __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __restrict__ boxes,
                                                   const float* __restrict__ scores,
@@ -155,8 +158,10 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   __shared__ int kept_c[320];
   __shared__ unsigned long long supp[kNmsWaves];
   __shared__ unsigned long long rowp[kNmsWaves][64];
+  __shared__ unsigned long long sel[kSelMax];  // the top set; its first 8 KB hold the histogram first
   __shared__ int s_nk;
   __shared__ int ncand;
+  __shared__ int s_n2, s_T, s_nsel;
   const int n = blockIdx.x;
   const int tid = threadIdx.x;
   if (tid == 0) ncand = 0;
@@ -172,114 +177,185 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   }
   __syncthreads();
   const int cnt = min(ncand, kMaxCand);
-  int P = 64;
-  while (P < cnt) P <<= 1;
-  for (int i = cnt + tid; i < P; i += blockDim.x) keys[i] = 0ull;
-  __syncthreads();
-  // bitonic sort, descending
-  for (int k = 2; k <= P; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < P; i += blockDim.x) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const unsigned long long a = keys[i], b = keys[ixj];
-          const bool desc = (i & k) == 0;
-          if (desc ? (a < b) : (a > b)) {
-            keys[i] = b;
-            keys[ixj] = a;
+  // bitonic sort of K[0, n) (padded with zero keys to a power of two), descending
+  auto bitonic = [&](unsigned long long* K, int n) __attribute__((always_inline)) {
+    int P = 64;
+    while (P < n) P <<= 1;
+    for (int i = n + tid; i < P; i += blockDim.x) K[i] = 0ull;
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < P; i += blockDim.x) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const unsigned long long a = K[i], b = K[ixj];
+            const bool desc = (i & k) == 0;
+            if (desc ? (a < b) : (a > b)) {
+              K[i] = b;
+              K[ixj] = a;
+            }
           }
         }
+        __syncthreads();
+      }
+    }
+  };
+  // Top-set selection.  Greedy NMS reads candidates in score order and usually reaches
+  // max_det long before the end of the list, so only the head needs sorting: a 2048-bin
+  // histogram of the score bits gives the lowest bin T whose suffix holds >= kSel keys;
+  // keys in bins >= T are exactly the top keys of the total (score, index) order (equal
+  // scores share a bin).  They are compacted and sorted alone (<= 2048 instead of up to
+  // 16384 keys: the full sort was most of the 179 us the b192 step spent in NMS,
+  // profiles/r3_v7_yolov8n_b192_op_roofline.md row 64); the rest is sorted only if the top
+  // set runs out before max_det.
+  const unsigned lo = conf > 0.f ? __float_as_uint(conf) : 0u;
+  const unsigned span = 0x3F800000u - lo;  // scores are sigmoids: (conf, 1]
+  const int shift = max(0, 32 - __clz((int)(span | 1u)) - 11);
+  auto bin_of = [&](unsigned long long key) __attribute__((always_inline)) {
+    return min(kBins - 1, (int)((((unsigned)(key >> 32)) - lo) >> shift));
+  };
+  unsigned long long* K = keys;
+  int nsel = cnt;
+  if (cnt > kSel) {
+    int* hist = reinterpret_cast<int*>(sel);
+    for (int i = tid; i < kBins; i += blockDim.x) hist[i] = 0;
+    if (tid == 0) s_n2 = 0;
+    __syncthreads();
+    for (int i = tid; i < cnt; i += blockDim.x) atomicAdd(&hist[bin_of(keys[i])], 1);
+    __syncthreads();
+    if (tid < 64) {  // wave 0: lane L owns bins [32 L, 32 L + 32)
+      int sum = 0;
+      for (int b = 0; b < 32; ++b) sum += hist[tid * 32 + b];
+      int suf = sum;  // suffix sum over lanes >= L
+      for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_down(suf, off);
+        if (tid + off < 64) suf += v;
+      }
+      const unsigned long long hit = __ballot(suf >= kSel);
+      const int lt = 63 - __clzll((long long)hit);  // highest lane whose suffix reaches kSel
+      if (tid == lt) {
+        int acc = suf - sum, T = tid * 32;
+        for (int b = 31; b >= 0; --b) {
+          acc += hist[tid * 32 + b];
+          if (acc >= kSel) {
+            T = tid * 32 + b;
+            break;
+          }
+        }
+        s_T = T;
+        s_nsel = acc;
+      }
+    }
+    __syncthreads();
+    if (s_nsel <= kSelMax) {
+      const int T = s_T;
+      for (int i = tid; i < cnt; i += blockDim.x) {
+        const unsigned long long key = keys[i];
+        if (bin_of(key) >= T) sel[atomicAdd(&s_n2, 1)] = key;
       }
       __syncthreads();
+      K = sel;
+      nsel = s_n2;
     }
   }
+  bitonic(K, nsel);
   float* o = out + (long long)n * max_det * 6;
   const int lane = tid & 63, wv = tid >> 6;
   const float* bx = boxes + (long long)n * A * 4;
   const int* cl = cls + (long long)n * A;
   int nk = 0;
-  for (int base = 0; base < cnt && nk < max_det; base += 64) {
-    // every wave holds the same 64 candidates (lane = candidate)
-    const int ci = base + lane;
-    const bool valid = ci < cnt;
-    float x1 = 0, y1 = 0, x2 = 0, y2 = 0, s = 0;
-    float4 raw = make_float4(0.f, 0.f, 0.f, 0.f);
-    int c = -1;
-    if (valid) {
-      const unsigned long long key = keys[ci];
-      const int idx = (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
-      s = __uint_as_float((unsigned)(key >> 32));
-      c = cl[idx];
-      raw = *reinterpret_cast<const float4*>(bx + idx * 4);
-      const float off = (float)c * kMaxWH;
-      x1 = raw.x + off;
-      y1 = raw.y + off;
-      x2 = raw.z + off;
-      y2 = raw.w + off;
-    }
-    // 1. against the kept list, split over the NMS_WAVES waves (j = wv, wv + W, ...):
-    // independent LDS reads, no early exit, so the loads pipeline instead of one
-    // LDS round trip per kept box (the one-wave version was 290 us at batch 64 on
-    // images with ~1000 candidates).  Other classes never overlap: compare class first.
-    bool sup = false;
-    for (int j = wv; j < nk; j += kNmsWaves) {
-      const float4 kb = *reinterpret_cast<const float4*>(kept + 4 * j);
-      sup |= kept_c[j] == c && iou_gt(x1, y1, x2, y2, kb.x, kb.y, kb.z, kb.w, iou_thr);
-    }
-    // 2. in-chunk: which LATER lanes this lane's box suppresses, also split over the
-    // waves (j = wv, wv + W, ...); j is wave-uniform, so the other box comes from
-    // v_readlane (scalar broadcast), not an LDS-routed shuffle
-    const int lim = min(64, cnt - base);
-    unsigned long long row = 0ull;
-    for (int j = wv; j < lim; j += kNmsWaves) {
-      const float bx1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x1), j));
-      const float by1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, y1), j));
-      const float bx2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x2), j));
-      const float by2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, y2), j));
-      if (j > lane && iou_gt(x1, y1, x2, y2, bx1, by1, bx2, by2, iou_thr)) row |= 1ull << j;
-    }
-    rowp[wv][lane] = row;
-    const unsigned long long sb = __ballot(sup);
-    if (lane == 0) supp[wv] = sb;
-    __syncthreads();
-    if (wv == 0) {
-      unsigned long long dead = 0ull;
-      row = 0ull;
+  // greedy suppression over the sorted K[from, to), continuing the kept list
+  auto greedy = [&](const unsigned long long* K, int from, int to) __attribute__((always_inline)) {
+    for (int base = from; base < to && nk < max_det; base += 64) {
+      // every wave holds the same 64 candidates (lane = candidate)
+      const int ci = base + lane;
+      const bool valid = ci < to;
+      float x1 = 0, y1 = 0, x2 = 0, y2 = 0, s = 0;
+      float4 raw = make_float4(0.f, 0.f, 0.f, 0.f);
+      int c = -1;
+      if (valid) {
+        const unsigned long long key = K[ci];
+        const int idx = (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
+        s = __uint_as_float((unsigned)(key >> 32));
+        c = cl[idx];
+        raw = *reinterpret_cast<const float4*>(bx + idx * 4);
+        const float off = (float)c * kMaxWH;
+        x1 = raw.x + off;
+        y1 = raw.y + off;
+        x2 = raw.z + off;
+        y2 = raw.w + off;
+      }
+      // 1. against the kept list, split over the NMS_WAVES waves (j = wv, wv + W, ...):
+      // independent LDS reads, no early exit, so the loads pipeline instead of one
+      // LDS round trip per kept box (the one-wave version was 290 us at batch 64 on
+      // images with ~1000 candidates).  Other classes never overlap: compare class first.
+      bool sup = false;
+      for (int j = wv; j < nk; j += kNmsWaves) {
+        const float4 kb = *reinterpret_cast<const float4*>(kept + 4 * j);
+        sup |= kept_c[j] == c && iou_gt(x1, y1, x2, y2, kb.x, kb.y, kb.z, kb.w, iou_thr);
+      }
+      // 2. in-chunk: which LATER lanes this lane's box suppresses, also split over the
+      // waves (j = wv, wv + W, ...); j is wave-uniform, so the other box comes from
+      // v_readlane (scalar broadcast), not an LDS-routed shuffle
+      const int lim = min(64, to - base);
+      unsigned long long row = 0ull;
+      for (int j = wv; j < lim; j += kNmsWaves) {
+        const float bx1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x1), j));
+        const float by1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, y1), j));
+        const float bx2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x2), j));
+        const float by2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, y2), j));
+        if (j > lane && iou_gt(x1, y1, x2, y2, bx1, by1, bx2, by2, iou_thr)) row |= 1ull << j;
+      }
+      rowp[wv][lane] = row;
+      const unsigned long long sb = __ballot(sup);
+      if (lane == 0) supp[wv] = sb;
+      __syncthreads();
+      if (wv == 0) {
+        unsigned long long dead = 0ull;
+        row = 0ull;
 #pragma unroll
-      for (int w = 0; w < kNmsWaves; ++w) {
-        dead |= supp[w];
-        row |= rowp[w][lane];
-      }
-      const bool alive = valid && !((dead >> lane) & 1ull);
-      unsigned long long live = __ballot(alive);
-      const unsigned rlo = (unsigned)row, rhi = (unsigned)(row >> 32);
-      for (int j = 0; j < lim; ++j) {
-        if ((live >> j) & 1ull) {
-          const unsigned long long rj =
-              ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)rhi, j) << 32) |
-              (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)rlo, j);
-          live &= ~rj;
+        for (int w = 0; w < kNmsWaves; ++w) {
+          dead |= supp[w];
+          row |= rowp[w][lane];
         }
+        const bool alive = valid && !((dead >> lane) & 1ull);
+        unsigned long long live = __ballot(alive);
+        const unsigned rlo = (unsigned)row, rhi = (unsigned)(row >> 32);
+        for (int j = 0; j < lim; ++j) {
+          if ((live >> j) & 1ull) {
+            const unsigned long long rj =
+                ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)rhi, j) << 32) |
+                (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)rlo, j);
+            live &= ~rj;
+          }
+        }
+        // 3. append survivors in rank order
+        const bool keep = (live >> lane) & 1ull;
+        const int rank = __popcll(live & ((1ull << lane) - 1ull));
+        const int pos = nk + rank;
+        if (keep && pos < max_det) {
+          *reinterpret_cast<float4*>(kept + 4 * pos) = make_float4(x1, y1, x2, y2);
+          kept_c[pos] = c;
+          float* r = o + pos * 6;  // original (un-offset) coordinates: exact, no fp32 cancellation
+          r[0] = raw.x;
+          r[1] = raw.y;
+          r[2] = raw.z;
+          r[3] = raw.w;
+          r[4] = s;
+          r[5] = (float)c;
+        }
+        if (lane == 0) s_nk = min(nk + (int)__popcll(live), max_det);
       }
-      // 3. append survivors in rank order
-      const bool keep = (live >> lane) & 1ull;
-      const int rank = __popcll(live & ((1ull << lane) - 1ull));
-      const int pos = nk + rank;
-      if (keep && pos < max_det) {
-        *reinterpret_cast<float4*>(kept + 4 * pos) = make_float4(x1, y1, x2, y2);
-        kept_c[pos] = c;
-        float* r = o + pos * 6;  // original (un-offset) coordinates: exact, no fp32 cancellation
-        r[0] = raw.x;
-        r[1] = raw.y;
-        r[2] = raw.z;
-        r[3] = raw.w;
-        r[4] = s;
-        r[5] = (float)c;
-      }
-      if (lane == 0) s_nk = min(nk + (int)__popcll(live), max_det);
+      __syncthreads();
+      nk = s_nk;
     }
-    __syncthreads();
-    nk = s_nk;
+  };
+  greedy(K, 0, nsel);
+  if (nk < max_det && nsel < cnt) {
+    // the top set ran out: sort everything (its first nsel keys are the top set again,
+    // in the same order) and continue after them
+    bitonic(keys, cnt);
+    greedy(keys, nsel, cnt);
   }
   for (int i = nk * 6 + tid; i < max_det * 6; i += blockDim.x) o[i] = 0.f;
   if (tid == 0) count[n] = nk;

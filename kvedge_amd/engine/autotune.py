@@ -19,8 +19,18 @@ import torch
 from ..models.layers import record_convs
 
 
+def _hold_gpu(launches: int) -> None:
+    """Queue a spin kernel long enough to cover the host's enqueue of ``launches`` layer
+    launches, so the timed events bracket GPU execution, not host launch latency.  Without
+    it a small (edge-batch) layer measured the Python + HIP launch path -- about 5-10 us per
+    kernel -- which, for a split-K tile (GEMM + finalize: two launches), was larger than
+    the kernels themselves, and the tuner never picked the split forms at batch 1."""
+    torch.cuda._sleep(int(min(5e7, 60_000 * max(1, launches))))  # ~25 us per launch
+
+
 def _time(fn: Callable[[int], object], tile: int, iters: int) -> float:
     fn(tile)
+    _hold_gpu(iters)
     evs = []
     for _ in range(iters):
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -39,6 +49,7 @@ def _time_concurrent(fn: Callable[[int], object], tile: int, iters: int, streams
     CUs (a tile that fills every CU alone can lose to a leaner one under concurrency)."""
     cur = torch.cuda.current_stream()
     fn(tile)
+    _hold_gpu(iters * len(streams))
     evs = []
     for _ in range(iters):
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -62,6 +73,7 @@ def _time_interleaved(cands, rounds: int):
     where timing each candidate's launches back to back let a drift decide near-ties."""
     for fn, t in cands:
         fn(t)  # warm: code object loaded, first-launch costs out of the way
+    _hold_gpu(rounds * len(cands))
     evs = [[] for _ in cands]
     for _ in range(rounds):
         for i, (fn, t) in enumerate(cands):

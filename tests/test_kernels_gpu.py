@@ -332,6 +332,34 @@ def test_nms_dense_overlaps():
     assert (o.cpu() - o_ref).abs().max() < 1e-4
 
 
+@pytest.mark.parametrize("case", ["spread", "clustered", "ties"])
+def test_nms_top_set(case):
+    """YOLO-sized candidate lists (8400 anchors, most above conf) through the NMS top-set
+    path: 'spread' reaches max_det inside the sorted top set; 'clustered' (one class, boxes
+    piled on few centres) exhausts the top set first and falls back to the full sort;
+    'ties' (scores on 8 levels) puts > 2048 keys in one histogram bin (full-sort path)."""
+    g = torch.Generator().manual_seed(5)
+    A, N = 8400, 3
+    if case == "clustered":
+        ctr = torch.rand(N, 4, 2, generator=g)[:, torch.randint(0, 4, (A,), generator=g)] * 600
+        wh = torch.rand(N, A, 2, generator=g) * 4 + 60
+        cls = torch.zeros(N, A, dtype=torch.int32)
+    else:
+        ctr = torch.rand(N, A, 2, generator=g) * 640
+        wh = torch.rand(N, A, 2, generator=g) * 40 + 4
+        cls = torch.randint(0, 80, (N, A), generator=g, dtype=torch.int32)
+    boxes = torch.cat([ctr - wh / 2, ctr + wh / 2], -1)
+    scores = torch.rand(N, A, generator=g) * 0.7 + 0.3
+    if case == "ties":
+        scores = (scores * 8).floor() / 8 + 0.05
+    o_ref, n_ref = ops.nms(boxes, scores, cls, conf=0.25, iou=0.7, max_det=300)
+    o, n = ops.nms(boxes.cuda(), scores.cuda(), cls.cuda(), conf=0.25, iou=0.7, max_det=300)
+    assert torch.equal(n.cpu(), n_ref), (n, n_ref)
+    assert (o.cpu() - o_ref).abs().max() < 1e-4
+    if case == "clustered":
+        assert int(n_ref.max()) < 300  # the top set alone never reaches max_det here
+
+
 @pytest.mark.parametrize("tile", [-1] + list(range(6, DIRECT0)) + sorted(NLOOP_DUAL) + [NLOOP0 + 8]
                          + list(range(XP0, N_TILES)))
 @pytest.mark.parametrize("geom", [(2, 14, 14, 64, 128, 256, 2), (2, 7, 7, 128, 256, 512, 1),

@@ -160,11 +160,13 @@ def test_resnet50_frames_in_parity(resnet):
         lg_fused = kv.raw_outputs(fr).float()
         lg_two = kv.logits(kv.preprocess(fr)).float()
     torch.cuda.synchronize()
-    # logits, not 1000-way probabilities (~1e-3 each, where an atol says nothing)
+    # logits, not 1000-way probabilities (~1e-3 each, where an atol says nothing).  The two
+    # paths use different stems (12-channel s2d K 192 vs 16-channel K 256), so they differ
+    # by bf16 rounding carried through 50 layers (cos > 0.9995 is relative RMS < ~3 %)
     cos = torch.nn.functional.cosine_similarity(lg_fused.flatten(), lg_two.flatten(), dim=0)
     assert cos > 0.9995, float(cos)
-    assert (lg_fused - lg_two).abs().max() <= 1e-2 * lg_two.abs().max(), \
-        (lg_fused - lg_two).abs().max()
+    d = lg_fused - lg_two
+    assert d.abs().max() <= 3e-2 * lg_two.abs().max(), d.abs().max()
     assert torch.equal(lg_fused.argmax(1), lg_two.argmax(1))
 
 

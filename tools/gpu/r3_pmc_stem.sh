@@ -1,0 +1,13 @@
+# PMC passes over the stem kernels (stem_probe: 16-channel vs 12-channel s2d stems), b640
+set -o pipefail
+export TMPDIR=/tmp
+OUT=gpurun_out/pmc_stem; mkdir -p $OUT
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA" \
+           "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" \
+           "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do
+  i=$((i+1))
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d $OUT/p$i -o p$i -- \
+    python3 tools/stem_probe.py --batch 640 --reps 3 > $OUT/p$i.log 2>&1 || exit $?
+done
+python3 tools/pmc_summary.py $OUT > $OUT/summary.txt 2>&1; cat $OUT/summary.txt | head -8
