@@ -451,6 +451,36 @@ void stem12_pool_frames(const at::Tensor& x, const at::Tensor& w, const at::Tens
   TORCH_CHECK(rc == 0, "kvedge: stem12_pool_frames failed rc=", rc);
 }
 
+// YOLOv8n b0 (frames-in s2d stem) + b1 (3x3/2 16 -> 32) in one kernel (yolo_stem2.hip)
+void yolo_stem2(const at::Tensor& x, const at::Tensor& w0, const at::Tensor& b0,
+                const at::Tensor& w1, const at::Tensor& b1, at::Tensor& y) {
+  check_dev(x, "x");
+  check_bf16(w0, "w0");
+  check_bf16(w1, "w1");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.scalar_type() == at::kByte && x.dim() == 4 && x.size(3) == 3 && x.is_contiguous(),
+              "kvedge: yolo_stem2 x must be contiguous u8 [N,H,W,3]");
+  TORCH_CHECK(x.size(1) % 4 == 0 && x.size(2) % 32 == 0 && x.size(2) <= 640,
+              "kvedge: yolo_stem2 needs H % 4 == 0, W % 32 == 0, W <= 640");
+  TORCH_CHECK(w0.dim() == 2 && w0.size(0) == 16 && w0.size(1) == 64 && w0.is_contiguous(),
+              "kvedge: yolo_stem2 w0 must be [16][64]");
+  TORCH_CHECK(w1.dim() == 2 && w1.size(0) == 32 && w1.size(1) >= 144 && w1.size(1) % 8 == 0 &&
+                  w1.is_contiguous(), "kvedge: yolo_stem2 w1 must be [32][>= 144]");
+  for (const at::Tensor* b : {&b0, &b1}) {
+    check_dev(*b, "bias");
+    TORCH_CHECK(b->scalar_type() == at::kFloat && b->is_contiguous(), "kvedge: fp32 biases");
+  }
+  TORCH_CHECK(b0.numel() >= 16 && b1.numel() >= 32, "kvedge: bias sizes");
+  const int64_t N = x.size(0), H0 = x.size(1), W0 = x.size(2);
+  TORCH_CHECK(y.dim() == 4 && y.size(0) == N && y.size(1) == H0 / 4 && y.size(2) == W0 / 4 &&
+                  y.size(3) == 32 && y.is_contiguous(), "kvedge: yolo_stem2 y must be [N,H/4,W/4,32]");
+  const c10::DeviceGuard g(x.device());
+  const int rc = kv_yolo_stem2(x.data_ptr(), w0.data_ptr(), b0.data_ptr<float>(), w1.data_ptr(),
+                               (int)w1.size(1), b1.data_ptr<float>(), y.data_ptr(), (int)N,
+                               (int)H0, (int)W0, cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: yolo_stem2 failed rc=", rc);
+}
+
 void stem_pool_frames(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias,
                       at::Tensor& y, at::ArrayRef<double> mean, at::ArrayRef<double> stdv,
                       int64_t y_coff) {
@@ -560,6 +590,7 @@ TORCH_LIBRARY(kvedge, m) {
   m.def("synth_frames_dev(Tensor(a!) y, Tensor(b!) step, int seed) -> ()");
   m.def("stem_pool_frames(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, float[] mean, float[] std, int y_coff) -> ()");
   m.def("stem12_pool_frames(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, float[] mean, float[] std, int y_coff) -> ()");
+  m.def("yolo_stem2(Tensor x, Tensor w0, Tensor b0, Tensor w1, Tensor b1, Tensor(a!) y) -> ()");
   m.def("preprocess(Tensor x, Tensor(a!) y, float[] mean, float[] std) -> ()");
   m.def("batchnorm_nhwc(Tensor x, Tensor(a!) y, Tensor scale, Tensor shift, bool relu) -> ()");
   m.def("conv_num_tiles() -> int", conv_num_tiles);
@@ -586,6 +617,7 @@ TORCH_LIBRARY_IMPL(kvedge, CUDA, m) {
   m.impl("preprocess", preprocess);
   m.impl("stem_pool_frames", stem_pool_frames);
   m.impl("stem12_pool_frames", stem12_pool_frames);
+  m.impl("yolo_stem2", yolo_stem2);
   m.impl("batchnorm_nhwc", batchnorm_nhwc);
 }
 

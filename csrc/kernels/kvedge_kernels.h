@@ -103,6 +103,11 @@ int kv_stem12_pool_frames(const void* frames, const void* w, const float* bias, 
                           int H0, int W0, const float* mean3, const float* inv_std3, int ldy,
                           int y_coff, hipStream_t s);
 int kv_stem12_lds_bytes(int Ws);
+// YOLOv8n b0 + b1 fused from raw frames (yolo_stem2.hip): w0 [16][64] frames-in s2d stem,
+// w1 [32][w1_ld] 3x3/2 16 -> 32; y [N, H0/4, W0/4, 32]
+int kv_yolo_stem2(const void* frames, const void* w0, const float* bias0, const void* w1,
+                  int w1_ld, const float* bias1, void* y, int N, int H0, int W0, hipStream_t s);
+int kv_yolo_stem2_lds_bytes(int Ws);
 
 int kv_maxpool2d(const void* x, void* y, int N, int H, int W, int C, int ldx, int x_coff,
                  int ldy, int y_coff, int k, int stride, int pad, int Ho, int Wo, hipStream_t s);

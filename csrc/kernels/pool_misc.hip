@@ -137,27 +137,39 @@ __global__ __launch_bounds__(kBlock) void sppf_kernel(bf16* __restrict__ buf, in
 }
 
 // ---- K6 global average pool: one thread per (n, 8 channels) ----------------
+// 8 lanes per output chunk (8 channels of one image), each summing every 8th pixel, then a
+// 3-step xor-shuffle reduction.  One lane per chunk walking all HW pixels serialised 49
+// dependent-address loads per lane: at batch 1 (256 chunks, one workgroup) that was 15 us,
+// the longest non-conv kernel of the edge step (profiles/r3_v7_resnet50_b1_forward_splitk.md).
 __global__ __launch_bounds__(kBlock) void avgpool_kernel(const bf16* __restrict__ x,
                                                          bf16* __restrict__ y, int N, int HW,
                                                          int C) {
   const int C8 = C / 8;
-  const long long total = (long long)N * C8;
+  const long long total = (long long)N * C8 * 8;
   const float inv = 1.0f / (float)HW;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c8 = (int)(i % C8);
-    const int n = (int)(i / C8);
+       i += (long long)gridDim.x * blockDim.x) {  // total % 64 == 0: whole waves iterate
+    const int part = (int)(i & 7);
+    const long long o = i >> 3;
+    const int c8 = (int)(o % C8);
+    const int n = (int)(o / C8);
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const bf16* p = x + (long long)n * HW * C + c8 * 8;
-    for (int q = 0; q < HW; ++q) {
+    for (int q = part; q < HW; q += 8) {
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(p + (long long)q * C);
 #pragma unroll
       for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
     }
-    bf16x8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(s[j] * inv);
-    *reinterpret_cast<bf16x8*>(y + (long long)n * C + c8 * 8) = o;
+    for (int off = 1; off < 8; off <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += __shfl_xor(s[j], off);
+    if (part == 0) {
+      bf16x8 r;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = f2bf(s[j] * inv);
+      *reinterpret_cast<bf16x8*>(y + (long long)n * C + c8 * 8) = r;
+    }
   }
 }
 
@@ -361,8 +373,8 @@ extern "C" int kv_sppf_pool(void* buf, int N, int H, int W, int C, hipStream_t s
 }
 
 extern "C" int kv_global_avgpool(const void* x, void* y, int N, int HW, int C, hipStream_t s) {
-  if (C % 8) return -1;
-  const long long work = (long long)N * (C / 8);
+  if (C % 64) return -1;  // whole waves per grid-stride step (the shuffle needs every lane)
+  const long long work = (long long)N * (C / 8) * 8;
   hipLaunchKernelGGL(avgpool_kernel, dim3(grid_for(work)), dim3(kBlock), 0, s, (const bf16*)x,
                      (bf16*)y, N, HW, C);
   KV_CHECK_LAUNCH();

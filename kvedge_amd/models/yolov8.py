@@ -313,13 +313,24 @@ class KvYoloV8n:
             return ops.stem_from_frames(frames_u8, b.spec, b.w, b.b)
         return self.b0(self.preprocess(frames_u8))
 
-    def heads(self, x: torch.Tensor, stem_done: bool = False):
-        """x: preprocessed bf16 s2d [N,320,320,16] (or, with stem_done, the b0 output)
-        -> three [N,h,w,144] head outputs."""
+    fuse_b1: bool = True  # GPU: frames -> b1 output in one kernel (b0 never leaves LDS)
+
+    def stem_b1(self, frames_u8: torch.Tensor) -> torch.Tensor:
+        """uint8 frames -> b1 output [N,160,160,32]: the fused b0 + b1 kernel
+        (csrc/kernels/yolo_stem2.hip) where the shape allows, else stem() then b1."""
+        if self.fuse_b1 and frames_u8.is_cuda and ops.yolo_stem2_fits(frames_u8.shape):
+            b0, b1 = self.b0_frames, self.b1
+            return ops.yolo_stem2(frames_u8, b0.spec, b0.w, b0.b, b1.spec, b1.w, b1.b)
+        return self.b1(self.stem(frames_u8))
+
+    def heads(self, x: torch.Tensor, stem_done: bool = False, b1_done: bool = False):
+        """x: preprocessed bf16 s2d [N,320,320,16] (or, with stem_done, the b0 output; with
+        b1_done, the b1 output) -> three [N,h,w,144] head outputs."""
         N = x.shape[0]
         dev = x.device
         bf = torch.bfloat16
-        x = self.b1(x if stem_done else self.b0(x))   # [N,160,160,32]
+        if not b1_done:
+            x = self.b1(x if stem_done else self.b0(x))  # [N,160,160,32]
         x = self.b2(x)
         x = self.b3(x)                                # [N,80,80,64]
         H3 = x.shape[1]
@@ -347,11 +358,11 @@ class KvYoloV8n:
     def raw_outputs(self, frames_u8: torch.Tensor) -> torch.Tensor:
         """uint8 frames -> the three Detect head maps flattened and concatenated
         [N, 8400*144] (pre-decode, pre-NMS): what the C4 replica check hashes."""
-        feats = self.heads(self.stem(frames_u8), stem_done=True)
+        feats = self.heads(self.stem_b1(frames_u8), b1_done=True)
         N = frames_u8.shape[0]
         return torch.cat([f.reshape(N, -1) for f in feats], dim=1)
 
     def __call__(self, frames_u8: torch.Tensor):
-        feats = self.heads(self.stem(frames_u8), stem_done=True)
+        feats = self.heads(self.stem_b1(frames_u8), b1_done=True)
         boxes, scores, cls = ops.yolo_decode(feats, STRIDES, self.nc)
         return ops.nms(boxes, scores, cls, self.conf, self.iou, self.max_det)

@@ -434,6 +434,33 @@ def stem12_pool_frames(frames: torch.Tensor, w12: torch.Tensor, bias: torch.Tens
     return out
 
 
+def yolo_stem2_fits(frames_shape) -> bool:
+    """Shapes the fused YOLO b0 + b1 kernel takes (csrc/kernels/yolo_stem2.hip)."""
+    _, H, W, _ = frames_shape
+    return H % 4 == 0 and W % 32 == 0 and 0 < W <= 640
+
+
+def yolo_stem2(frames: torch.Tensor, spec0: "ConvSpec", w0: torch.Tensor, b0: torch.Tensor,
+               spec1: "ConvSpec", w1: torch.Tensor, b1: torch.Tensor,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """YOLOv8n b0 (frames-in s2d stem, SiLU) + b1 (3x3/2 16 -> 32, SiLU) in ONE pass: b0's
+    [N, H/2, W/2, 16] output stays in LDS (csrc/kernels/yolo_stem2.hip).
+    frames: uint8 [N, H, W, 3] with :func:`yolo_stem2_fits`; spec0/w0/b0: a
+    DeployedConv.stem_s2d(..., in_scale=1/255); spec1/w1/b1: the 3x3/2 16 -> 32 conv.
+    -> [N, H/4, W/4, 32].  CPU: the two reference ops in sequence (bf16 in between)."""
+    assert spec0.kh == 2 and spec0.cin == 16 and spec0.cout == 16, spec0
+    assert (spec1.kh, spec1.stride, spec1.cin, spec1.cout) == (3, 2, 16, 32), spec1
+    assert spec0.act == ACT_SILU and spec1.act == ACT_SILU
+    N, H, W, _ = frames.shape
+    if out is None:
+        out = empty(N, H // 4, W // 4, 32, dtype=torch.bfloat16, device=frames.device)
+    if not frames.is_cuda:
+        x = stem_from_frames(frames, spec0, w0, b0)
+        return conv2d(x, spec1, w1, b1, out=out)
+    _native().yolo_stem2(frames, w0, b0, w1, b1, out)
+    return out
+
+
 def stem_from_frames(frames: torch.Tensor, spec: "ConvSpec", w: torch.Tensor,
                      bias: Optional[torch.Tensor], out: Optional[torch.Tensor] = None,
                      tile: int = -1) -> torch.Tensor:

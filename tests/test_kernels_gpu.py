@@ -238,9 +238,11 @@ def test_maxpool_avgpool_softmax():
     y_ref = ops.maxpool2d(x, 3, 2, 1)
     y = ops.maxpool2d(x.cuda(), 3, 2, 1)
     assert torch.equal(y.cpu(), y_ref)
-    f = _rand((3, 7, 7, 2048), 4)
-    a = ops.global_avgpool(f.cuda()).cpu().float()
-    assert (a - f.float().mean((1, 2))).abs().max() < 0.02
+    for shp in ((3, 7, 7, 2048), (1, 7, 7, 2048), (2, 14, 14, 192), (5, 3, 2, 64)):
+        f = _rand(shp, 4)
+        a = ops.global_avgpool(f.cuda()).cpu().float()
+        ref = f.float().mean((1, 2))
+        assert ((a - ref).abs() <= 2.0 ** -8 * ref.abs() + 1e-4).all(), shp  # one bf16 rounding
     lg = _rand((5, 1000), 5, 3.0)
     p, am = ops.softmax_rows(lg.cuda())
     pr = torch.softmax(lg.float(), 1)

@@ -212,3 +212,35 @@ def test_stem12_pool_frames_kernel(resnet, hw, n):
     r = r.permute(0, 2, 3, 1)
     cos = torch.nn.functional.cosine_similarity(got[..., 8:72].float().flatten(), r.flatten(), dim=0)
     assert cos > 0.999, float(cos)
+
+
+@pytest.mark.parametrize("n,hw", [(3, (64, 96)), (2, (640, 640)), (1, (4, 32)), (7, (128, 640)),
+                                  (40, (128, 96)), (5, (36, 64))])
+def test_yolo_stem2_kernel(n, hw):
+    """Fused YOLO b0 + b1 from raw frames (csrc/kernels/yolo_stem2.hip) vs the two reference
+    ops in sequence: band ranges that start mid-image (n = 7: one band per workgroup,
+    H1 = 32) and cross image boundaries (n = 40), the full 640^2 shape, a single band."""
+    from kvedge_amd.models.yolov8 import KvYoloV8n, init_yolov8n
+
+    kv = KvYoloV8n(init_yolov8n(seed=2, calibrate=False), "cpu")
+    b0, b1 = kv.b0_frames, kv.b1
+    fr = torch.randint(0, 256, (n, hw[0], hw[1], 3), dtype=torch.uint8,
+                       generator=torch.Generator().manual_seed(17))
+    ref = ops.yolo_stem2(fr, b0.spec, b0.w, b0.b, b1.spec, b1.w, b1.b).float()
+    got = ops.yolo_stem2(fr.cuda(), b0.spec, b0.w.cuda(), b0.b.cuda(), b1.spec, b1.w.cuda(),
+                         b1.b.cuda())
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape == (n, hw[0] // 4, hw[1] // 4, 32)
+    _close(got.cpu(), ref)
+
+
+def test_yolov8n_fused_stem_b1_parity(yolo):
+    _, kv, kv_cpu = yolo
+    fr = _frames(2, 8, hw=320)
+    with torch.no_grad():
+        hg = kv.heads(kv.stem_b1(fr.cuda()), b1_done=True)
+        hc = kv_cpu.heads(kv_cpu.preprocess(fr))
+    for g, c in zip(hg, hc):
+        cos = torch.nn.functional.cosine_similarity(g.float().cpu().flatten(), c.float().flatten(),
+                                                    dim=0)
+        assert cos > 0.999, float(cos)

@@ -1,0 +1,16 @@
+# fused YOLO stem (b0+b1), NMS top set, avgpool: numerics, then benches (edge block) and the b1 profile
+set -o pipefail
+mkdir -p gpurun_out; export TMPDIR=/tmp
+P="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+timeout -k 10 700 $P tests/test_kernels_gpu.py -k "nms or splitk or avgpool" tests/test_models_gpu.py tests/test_bench_config_gpu.py > gpurun_out/pytest_ys2.log 2>&1
+rc=$?; tail -n 3 gpurun_out/pytest_ys2.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python -u bench.py --model yolov8n --steps 20 --warmup 5 > gpurun_out/bench_yolo.log 2>&1 && \
+timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 && \
+timeout -k 10 400 python -u tools/op_roofline.py --model yolov8n --batch 192 --streams 2 > gpurun_out/yolo_op_roofline_b192_v3.md 2> gpurun_out/yolo_op_roofline.err && \
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/fwd1 -o fwd1 -- python3 tools/profile_forward.py --batch 1 --reps 20 > gpurun_out/fwd1.log 2>&1 && \
+python tools/profile_forward.py --summarize gpurun_out/fwd1/fwd1_kernel_trace.csv --reps 20 > gpurun_out/fwd_b1.md
+rc=$?
+tail -n 1 gpurun_out/bench_yolo.log | cut -c1-200; tail -n 1 gpurun_out/bench.log | cut -c1-200; grep -o '"edge": \[[^]]*\]' gpurun_out/bench.log
+head -4 gpurun_out/yolo_op_roofline_b192_v3.md | tail -1; grep "^| [0-3] \|^| 6[0-9] \|Forward" gpurun_out/yolo_op_roofline_b192_v3.md
+head -12 gpurun_out/fwd_b1.md
+exit $rc
