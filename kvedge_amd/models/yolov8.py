@@ -16,6 +16,8 @@ decode, K10 NMS.
 """
 from __future__ import annotations
 
+import os
+
 import math
 from typing import List, Optional
 
@@ -313,7 +315,8 @@ class KvYoloV8n:
             return ops.stem_from_frames(frames_u8, b.spec, b.w, b.b)
         return self.b0(self.preprocess(frames_u8))
 
-    fuse_b1: bool = True  # GPU: frames -> b1 output in one kernel (b0 never leaves LDS)
+    # GPU: frames -> b1 output in one kernel (b0 never leaves LDS); KVEDGE_YOLO_FUSE_B1=0 = A/B off
+    fuse_b1: bool = os.environ.get("KVEDGE_YOLO_FUSE_B1", "1") != "0"
 
     def stem_b1(self, frames_u8: torch.Tensor) -> torch.Tensor:
         """uint8 frames -> b1 output [N,160,160,32]: the fused b0 + b1 kernel

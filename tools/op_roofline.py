@@ -96,6 +96,13 @@ def stem12_cost(frames, w12, bias, out=None, y_coff=0, mean=None, std=None):
             2.0 * m * 147 * 64, None)
 
 
+def yolo_stem2_cost(frames, spec0, w0, b0, spec1, w1, b1, out=None):
+    N, H, W, _ = frames.shape
+    m0, m1 = N * (H // 2) * (W // 2), N * (H // 4) * (W // 4)
+    return ("stem 3x3/2 3>16 + b1 3x3/2 16>32 (frames in, fused)", frames.numel() + m1 * 64,
+            2.0 * (m0 * 27 * 16 + m1 * 144 * 32), None)
+
+
 def sppf_cost(buf, C):
     return f"sppf pools c{C}", _b(buf, C) * 4, 0.0, None
 
@@ -125,6 +132,7 @@ def softmax_cost(x, out=None, argmax=None):
 
 COSTS = {"conv2d": conv2d_cost, "conv_dual": conv_dual_cost, "conv_tail": conv_tail_cost,
          "stem_from_frames": stem_from_frames_cost, "stem12_pool_frames": stem12_cost,
+         "yolo_stem2": yolo_stem2_cost,
          "sppf_pool": sppf_cost, "upsample2x": upsample_cost, "yolo_decode": decode_cost,
          "nms": nms_cost, "global_avgpool": avgpool_cost, "softmax_rows": softmax_cost}
 
