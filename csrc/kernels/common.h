@@ -70,6 +70,21 @@ __device__ __forceinline__ void kv_lds_dma16(kv_i32x4 rs, void* lds, int voff) {
 }
 #pragma clang diagnostic pop
 
+// Registers loaded once per kernel (weights, biases) and read inside a loop that also has
+// loads in flight (a band prefetch): pass them through an empty asm after loading.  hipcc's
+// wait-count pass then waits for them once, before the asm, and afterwards sees asm-defined
+// values instead of pending loads.  Without it the pass re-waited for them inside the loop
+// with a vmcnt(0) -- which also drained the next band's in-flight prefetch on every block
+// (stem12.hip, yolo_stem2.hip: PMC 30-40 % of wave cycles waiting).
+template <class T>
+__device__ __forceinline__ void kv_settle(T& v) {
+  static_assert(sizeof(T) == 16, "16-byte register groups");
+  typedef unsigned int u32x4s __attribute__((ext_vector_type(4)));
+  u32x4s u = __builtin_bit_cast(u32x4s, v);
+  asm volatile("" : "+v"(u));
+  v = __builtin_bit_cast(T, u);
+}
+
 __device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
 __device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }  // v_cvt_pk_bf16_f32, NaN-safe
 

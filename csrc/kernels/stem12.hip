@@ -93,6 +93,14 @@ __global__ __launch_bounds__(kNT, 2) void stem12_pool_kernel(
 #pragma unroll
     for (int g = 0; g < 4; ++g)
       bv[cb][g] = *reinterpret_cast<const float4*>(bias + cb * 32 + g * 8 + fh * 4);
+  // loaded once: no waits for them inside the band loop (which has the raw prefetch in flight)
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+#pragma unroll
+    for (int t = 0; t < kKs; ++t) kv_settle(wreg[cb][t]);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) kv_settle(bv[cb][g]);
+  }
 
   // ---- zero columns of every ring row (s2d X = -2, -1 and Ws, Ws + 1): written once
   for (int i = tid; i < kRing * 6; i += kNT) {

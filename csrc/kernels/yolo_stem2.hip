@@ -67,7 +67,7 @@ __global__ __launch_bounds__(kNT, 2) void yolo_stem2_kernel(
 #pragma unroll
   for (int t = 0; t < 2; ++t)
     w0r[t] = *reinterpret_cast<const bf16x8*>(w0 + q16 * 64 + t * 32 + kq * 8);
-  const float4 b0v = *reinterpret_cast<const float4*>(bias0 + kq * 4);
+  float4 b0v = *reinterpret_cast<const float4*>(bias0 + kq * 4);
   // b1 (32x32x16): lane = (cout lane & 31, k half lane >> 5), 9 taps of 16 channels
   const int fr = lane & 31, fh = lane >> 5;
   bf16x8 w1r[9];
@@ -77,6 +77,14 @@ __global__ __launch_bounds__(kNT, 2) void yolo_stem2_kernel(
   float4 b1v[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) b1v[g] = *reinterpret_cast<const float4*>(bias1 + g * 8 + fh * 4);
+  // loaded once: no waits for them inside the band loop (which has the raw prefetch in flight)
+  kv_settle(w0r[0]);
+  kv_settle(w0r[1]);
+  kv_settle(b0v);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) kv_settle(w1r[t]);
+#pragma unroll
+  for (int g = 0; g < 4; ++g) kv_settle(b1v[g]);
 
   // ---- zero column (s2d pixel -1) of every s2d ring row; stem pad slot of every stem row
   for (int i = tid; i < 3 * 2; i += kNT)
