@@ -150,25 +150,30 @@ __global__ __launch_bounds__(kNT, 2) void yolo_stem2_kernel(
   };
 
   // ---- b0: stem rows [s0, s0 + nr) from the s2d ring -> stem ring (all 4 waves)
+  // Per row, blocks b = wv, wv + 4, ... (Ws / 16 per row): the row, its ring slots and the
+  // block's column base are wave-uniform (scalar), the lane parts are constants -- no
+  // per-block integer divide (it was a third of the phase's VALU, PMC:
+  // profiles/r3_v10_pmc_yolo_stem2_b192.txt).
+  const int bpr = Ws / 16;
+  const int lslot = (q16 & 1) ? half + 1 + (q16 >> 1) : (q16 >> 1);  // stem slot of column q16
   auto stem_rows = [&](int s0, int nr) __attribute__((always_inline)) {
-    const int nblk = nr * Ws / 16;  // Ws % 16 == 0
-    for (int blk = wv; blk < nblk; blk += 4) {
-      const int j = blk * 16 + q16;
-      const int rl = j / Ws, sx = j - rl * Ws;  // Ws % 16 == 0: one row per block
+    for (int rl = 0; rl < nr; ++rl) {
       const int sy = s0 + rl;
-      floatx4 acc = {b0v.x, b0v.y, b0v.z, b0v.w};
+      const unsigned char* sa0 = sring + mod3(sy - 1) * SR + q16 * kSP + kq * 16;  // pixel sx-1
+      const unsigned char* sa1 = sring + mod3(sy) * SR + q16 * kSP + kq * 16;
+      unsigned char* td = tring + mod3(sy) * TR + lslot * kTP + kq * 8;
+      for (int b = wv; b < bpr; b += 4) {
+        floatx4 acc = {b0v.x, b0v.y, b0v.z, b0v.w};
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(sa0 + b * 16 * kSP);
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(sa1 + b * 16 * kSP);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0r[0], a0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0r[1], a1, acc, 0, 0, 0);
+        // lane holds channels kq*4 .. +3 of stem pixel (sy, 16 b + q16)
+        bf16x4 o;
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {  // tap row a: s2d row sy - 1 + a, pixels sx - 1, sx
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(
-            sring + mod3(sy - 1 + a) * SR + sx * kSP + kq * 16);  // pixel sx-1 at slot sx
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0r[a], af, acc, 0, 0, 0);
+        for (int e = 0; e < 4; ++e) o[e] = f2bf(act_c<kActSilu>(acc[e]));
+        *reinterpret_cast<bf16x4*>(td + b * 8 * kTP) = o;
       }
-      // lane holds channels kq*4 .. +3 of stem pixel (sy, sx)
-      bf16x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = f2bf(act_c<kActSilu>(acc[e]));
-      const int slot = (sx & 1) ? half + 1 + (sx >> 1) : (sx >> 1);
-      *reinterpret_cast<bf16x4*>(tring + mod3(sy) * TR + slot * kTP + kq * 8) = o;
     }
   };
 
