@@ -5,6 +5,7 @@
 // whole forward built from these ops can be captured into one hipGraph
 // (kvedge_amd/engine).  Shapes/strides are computed by the Python wrappers in
 // kvedge_amd/ops/__init__.py; this layer only validates and launches.
+#include <cstdlib>
 #include <ATen/ATen.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -28,6 +29,21 @@ void check_bf16(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.scalar_type() == at::kBFloat16, "kvedge: ", name, " must be bf16");
 }
 
+// Split-K workspace: fp32 partial sums in [0, M*Cout); when the tensor also holds the
+// KV_SK_COUNTERS arrival counters at its END (ops.splitk_workspace sizes it so), the tiles
+// finish in-kernel (last slice per tile) instead of in a separate finalize launch.
+// KVEDGE_SK_FINALIZE=1 forces the finalize launch (A/B knob).
+void set_splitk_ws(KvConvParams& p, const at::Tensor& ws, int64_t data_elems) {
+  static const bool force_finalize = [] {
+    const char* e = std::getenv("KVEDGE_SK_FINALIZE");
+    return e && e[0] == '1';
+  }();
+  p.ws = ws.data_ptr<float>();
+  p.sk_cnt = nullptr;
+  if (!force_finalize && ws.numel() >= data_elems + KV_SK_COUNTERS)
+    p.sk_cnt = reinterpret_cast<int*>(p.ws + ws.numel() - KV_SK_COUNTERS);
+}
+
 void conv(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
           const c10::optional<at::Tensor>& res, at::Tensor& y, int64_t N, int64_t H, int64_t W,
           int64_t Cin, int64_t ldx, int64_t x_coff, int64_t Ho, int64_t Wo, int64_t Cout,
@@ -43,7 +59,7 @@ void conv(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
     check_dev(*ws, "ws");
     TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= N * Ho * Wo * Cout,
                 "kvedge: split-K workspace fp32[M*Cout]");
-    p.ws = ws->data_ptr<float>();
+    set_splitk_ws(p, *ws, N * Ho * Wo * Cout);
   }
   p.x = x.data_ptr();
   p.w = w.data_ptr();
@@ -123,7 +139,7 @@ void conv_dual(const at::Tensor& x1, const at::Tensor& x2, const at::Tensor& w,
     check_dev(*ws, "ws");
     TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= (int64_t)p.M * Cout,
                 "kvedge: split-K workspace fp32[M*Cout]");
-    p.ws = ws->data_ptr<float>();
+    set_splitk_ws(p, *ws, (int64_t)p.M * Cout);
   }
   const int rc = kv_conv2d(&p, (int)tile, cur_stream(x1));
   TORCH_CHECK(rc == 0, "kvedge: conv_dual failed rc=", rc);

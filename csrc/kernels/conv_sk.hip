@@ -4,38 +4,18 @@
 namespace kvedge {
 namespace {
 
-// split-K finalize: y = act2(act1(ws + bias) (+ res)) -> bf16, and ws = 0 for the next layer
-__global__ __launch_bounds__(256) void splitk_finalize_kernel(
-    float* __restrict__ ws, const float* __restrict__ bias, const bf16* __restrict__ res,
-    bf16* __restrict__ y, int M, int Cout, int ldy, int y_coff, int ldr, int r_coff, int act) {
-  const int cpr = Cout >> 3;
+// split-K finalize (sk_cnt == NULL): y = act2(act1(ws + bias) (+ res)) -> bf16, ws = 0 again
+__global__ __launch_bounds__(256) void splitk_finalize_kernel(const KvConvParams p) {
+  const int cpr = p.Cout >> 3;
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long long)M * cpr) return;
+  if (idx >= (long long)p.M * cpr) return;
   const int m = (int)(idx / cpr), c = (int)(idx - (long long)m * cpr) * 8;
-  float4* src = reinterpret_cast<float4*>(ws + (size_t)m * Cout + c);
+  float4* src = reinterpret_cast<float4*>(p.ws + (size_t)m * p.Cout + c);
   const float4 a0 = src[0], a1 = src[1];
   src[0] = make_float4(0.f, 0.f, 0.f, 0.f);
   src[1] = make_float4(0.f, 0.f, 0.f, 0.f);
   float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-  if (bias) {
-    const float4 b0 = *reinterpret_cast<const float4*>(bias + c);
-    const float4 b1 = *reinterpret_cast<const float4*>(bias + c + 4);
-    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
-    v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
-  }
-  bf16x8 o;
-  dispatch_act(act, res != nullptr, [&](auto A1, auto A2) __attribute__((always_inline)) {
-    constexpr int act1 = decltype(A1)::value, act2 = decltype(A2)::value;
-    bf16x8 r;
-    if (res) r = *reinterpret_cast<const bf16x8*>(res + (size_t)m * ldr + r_coff + c);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float u = act_c<act1>(v[e]);
-      if (res) u = act_c<act2>((float)f2bf(u) + (float)r[e]);
-      o[e] = f2bf(u);
-    }
-  });
-  *reinterpret_cast<bf16x8*>(y + (size_t)m * ldy + y_coff + c) = o;
+  sk_finish8(p, m, c, v);
 }
 
 struct SkTile {
@@ -69,12 +49,14 @@ int sk_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   if (!p->ws) return -11;  // split-K needs the caller's zeroed fp32 workspace
   KvConvParams q = *p;
   q.ksplit = e.split < nk ? e.split : nk;  // never more slices than K steps
+  const long long tiles = (long long)((p->M + e.t.bm - 1) / e.t.bm) * ((p->Cout + e.t.bn - 1) / e.t.bn);
+  if (q.sk_cnt && tiles > KV_SK_COUNTERS) return -12;  // one arrival counter per output tile
   if (const int rc = glds_launch_entry(&q, e.t, stream, q.ksplit)) return rc;
+  if (q.sk_cnt) return 0;  // the last slice of each tile finished it in-kernel
   const long long thr = (long long)p->M * (p->Cout / 8);
   if (thr <= 0) return 0;
   hipLaunchKernelGGL(splitk_finalize_kernel, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0,
-                     stream, p->ws, p->bias, (const bf16*)p->res, (bf16*)p->y, p->M, p->Cout,
-                     p->ldy, p->y_coff, p->ldr, p->r_coff, p->act);
+                     stream, q);
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }
 

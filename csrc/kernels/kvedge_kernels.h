@@ -50,11 +50,17 @@ typedef struct KvConvParams {
   void* z;
   int n_t, ldz, z_coff, act_t;
   // Split-K (v8 tiles, small-M layers: edge batches): the launch adds fp32 partial sums
-  // of its K slice into ws [M][Cout] (zero on entry) and a finalize kernel applies bias,
-  // residual and activation, writes y and zeroes ws again.  ws = NULL: v8 tiles refuse.
+  // of its K slice into ws [M][Cout] (zero on entry).  sk_cnt != NULL (KV_SK_COUNTERS
+  // zeroed ints, one per output tile): the last slice of a tile to arrive applies bias,
+  // residual and activation, writes y and re-zeroes its ws tile and counter in the same
+  // launch; sk_cnt = NULL: a separate finalize kernel does that.  ws = NULL: v8 refuses.
   float* ws;
   int ksplit;
+  int* sk_cnt;
 } KvConvParams;
+
+// ints reserved at the END of a split-K workspace tensor for the per-tile arrival counters
+#define KV_SK_COUNTERS 4096
 
 // tile: -1 = heuristic; otherwise an index into the tile table (kv_conv_num_tiles()).
 int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream);

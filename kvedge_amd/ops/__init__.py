@@ -203,15 +203,19 @@ _WS: dict = {}
 SPLITK_MAX_ELEMS = 16 << 20  # layers with M*Cout above this never split (64 MB of fp32)
 N_SPLITK_TILES = 13          # conv_sk.hip kSkTiles: the LAST tile indices
 SPLITK0 = 1 << 30            # first split-K tile index, set by load()
+SK_COUNTERS = 4096           # KV_SK_COUNTERS: per-tile arrival counters at the workspace's end
 
 
 def splitk_workspace(device: torch.device, elems: int) -> Optional[torch.Tensor]:
+    """The stream's split-K workspace: >= ``elems`` fp32 partial sums plus SK_COUNTERS int32
+    arrival counters at its end (the last K slice of a tile finishes it in-kernel and
+    re-arms its counter; csrc/kernels/conv_glds_kernel.inc).  All zero between layers."""
     if elems > SPLITK_MAX_ELEMS:
         return None
     key = (device.index, torch.cuda.current_stream(device).cuda_stream)
     ws = _WS.get(key)
-    if ws is None or ws.numel() < elems:
-        ws = torch.zeros(max(elems, 1 << 16), dtype=torch.float32, device=device)
+    if ws is None or ws.numel() < elems + SK_COUNTERS:
+        ws = torch.zeros(max(elems, 1 << 16) + SK_COUNTERS, dtype=torch.float32, device=device)
         _WS[key] = ws
     return ws
 
