@@ -428,11 +428,15 @@ void synth_frames_dev(at::Tensor& y, at::Tensor& step, int64_t seed) {
   check_dev(y, "y");
   check_dev(step, "step");
   TORCH_CHECK(y.scalar_type() == at::kByte && y.dim() == 4 && y.size(3) == 3, "kvedge: frames u8 [N,H,W,3]");
-  TORCH_CHECK(step.scalar_type() == at::kLong && step.numel() == 1, "kvedge: step int64[1]");
+  // int64[1]: counter, bumped by a second launch; int64[2]: counter + finished-block
+  // count (zero), bumped in-kernel by the last block to finish
+  TORCH_CHECK(step.scalar_type() == at::kLong && (step.numel() == 1 || step.numel() == 2),
+              "kvedge: step int64[1] or int64[2]");
   const c10::DeviceGuard g(y.device());
   const int rc = kv_synth_frames_dev(y.data_ptr<uint8_t>(), (int)y.size(0), (int)y.size(1),
                                      (int)y.size(2), (uint64_t)seed,
-                                     reinterpret_cast<uint64_t*>(step.data_ptr<int64_t>()), cur_stream(y));
+                                     reinterpret_cast<uint64_t*>(step.data_ptr<int64_t>()),
+                                     step.numel() == 2 ? 1 : 0, cur_stream(y));
   TORCH_CHECK(rc == 0, "kvedge: synth_frames_dev failed rc=", rc);
 }
 

@@ -141,10 +141,12 @@ int kv_nms(const float* boxes, const float* scores, const int* cls, int N, int A
 // K11: on-device synthetic camera frames, uint8 NHWC3, deterministic in (seed, step).
 int kv_synth_frames(uint8_t* y, int N, int H, int W, uint64_t seed, uint64_t step,
                     hipStream_t s);
-// K11b: same but the step counter is read from device memory and incremented by
-// the kernel, so a captured hipGraph produces fresh frames on every replay.
+// K11b: same but the step counter is read from device memory and incremented, so a
+// captured hipGraph produces fresh frames on every replay.  bump_done = 1: step[1] is a
+// zeroed finished-block count and the kernel's last block advances step[0] (one launch);
+// 0: a one-thread kernel after it does.
 int kv_synth_frames_dev(uint8_t* y, int N, int H, int W, uint64_t seed, uint64_t* step,
-                        hipStream_t s);
+                        int bump_done, hipStream_t s);
 // K12: uint8 NHWC3 -> bf16 NHWC4 normalized ((x/255 - mean)/std), channel 3 = 0.
 int kv_preprocess(const uint8_t* x, void* y, int N, int H, int W, const float* mean3,
                   const float* inv_std3, hipStream_t s);

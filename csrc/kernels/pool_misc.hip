@@ -255,10 +255,27 @@ __global__ __launch_bounds__(kBlock) void synth_kernel(uint8_t* y, long long tot
   synth_body(y, total8, seed, step);
 }
 
+// step[0] = step counter.  bump_done (step has a second slot, step[1] = blocks finished,
+// zero between launches): the LAST block to finish advances the counter for the next step
+// -- every block read step[0] before it counted itself finished -- so no separate one-thread
+// bump launch (~5 us per step at edge batches, where a step is ~50 launches)
 __global__ __launch_bounds__(kBlock) void synth_dev_kernel(uint8_t* y, long long total8,
-                                                           uint64_t seed, uint64_t* step) {
+                                                           uint64_t seed, uint64_t* step,
+                                                           int bump_done) {
   const uint64_t s = *step;
   synth_body(y, total8, seed, s);
+  if (!bump_done) return;
+  __syncthreads();  // every thread of this block has read step[0]
+  if (threadIdx.x == 0) {
+    const unsigned long long prev = __hip_atomic_fetch_add(
+        reinterpret_cast<unsigned long long*>(step + 1), 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1ull) {
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(step + 1), 0ull, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(step), 1ull, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 __global__ void bump_kernel(uint64_t* step) { *step += 1; }
@@ -411,12 +428,12 @@ extern "C" int kv_synth_frames(uint8_t* y, int N, int H, int W, uint64_t seed, u
 }
 
 extern "C" int kv_synth_frames_dev(uint8_t* y, int N, int H, int W, uint64_t seed,
-                                   uint64_t* step, hipStream_t s) {
+                                   uint64_t* step, int bump_done, hipStream_t s) {
   const long long bytes = (long long)N * H * W * 3;
   if (bytes % 8) return -1;
   hipLaunchKernelGGL(synth_dev_kernel, dim3(grid_for(bytes / 8)), dim3(kBlock), 0, s, y,
-                     bytes / 8, seed, step);
-  hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(1), 0, s, step);
+                     bytes / 8, seed, step, bump_done);
+  if (!bump_done) hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(1), 0, s, step);
   KV_CHECK_LAUNCH();
 }
 

@@ -85,7 +85,8 @@ class InferenceEngine:
         self.synthetic = synthetic
         self.frames = torch.empty(batch, image_size, image_size, 3, dtype=torch.uint8,
                                   device=self.device)
-        self.step_ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
+        # [step counter, finished-block count]: synth_frames bumps it in-kernel (one launch)
+        self.step_ctr = torch.zeros(2, dtype=torch.int64, device=self.device)
         self.outputs = None
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.times = StepTimes()
@@ -141,7 +142,10 @@ class InferenceEngine:
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # capture on the warm-up stream: per-stream state made during warm-up (the split-K
+        # workspace, ops.splitk_workspace) is then reused, not re-allocated -- and zero-filled
+        # by a kernel recorded into the graph, i.e. on every replay -- for a new stream
+        with torch.cuda.graph(self.graph, stream=s):
             self._step()
         torch.cuda.synchronize(self.device)
         return self

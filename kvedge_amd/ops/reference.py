@@ -135,9 +135,9 @@ def _splitmix64(z: np.ndarray) -> np.ndarray:
 
 
 def synth_frames(out, seed, step):
-    if isinstance(step, torch.Tensor):
-        st = int(step.item())
-        step.add_(1)
+    if isinstance(step, torch.Tensor):  # int64[1] counter, or [2]: counter + done-count slot
+        st = int(step[0].item())
+        step[0] += 1
     else:
         st = int(step)
     n8 = out.numel() // 8

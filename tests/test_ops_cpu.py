@@ -69,6 +69,9 @@ def test_synth_frames_deterministic():
     ctr = torch.tensor([5])
     ops.synth_frames(b, 1, ctr)
     assert torch.equal(a, b) and int(ctr) == 6
+    ctr2 = torch.tensor([5, 0])  # [counter, done-count] (the engine's in-kernel bump form)
+    ops.synth_frames(b, 1, ctr2)
+    assert torch.equal(a, b) and ctr2.tolist() == [6, 0]
     # bytes look uniform
     big = torch.empty(4, 64, 64, 3, dtype=torch.uint8)
     ops.synth_frames(big, 0, 0)
