@@ -184,6 +184,46 @@ __global__ __launch_bounds__(kBlock) void softmax_kernel(const bf16* __restrict_
   const bf16* xr = x + (long long)row * cols;
   float mx = -INFINITY;
   int arg = 0x7fffffff;
+  if (cols <= 1024 && (cols & 7) == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0) {
+    // register-resident row (ResNet-50's 1000 classes): each lane loads 16 contiguous
+    // columns as two 16-B vectors ONCE; max / sum / store run from registers.  The strided
+    // loop below reads the row three times with 2-B loads: ~10 us at batch 1, a whole
+    // edge-batch step's worth of per-kernel floor
+    float v[16];
+    const int c0 = lane * 16;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = c0 + 8 * h;  // a chunk of 8 is either all in range or all past cols
+      bf16x8 q = {};
+      if (c < cols) q = *reinterpret_cast<const bf16x8*>(xr + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[8 * h + e] = c < cols ? (float)q[e] : -INFINITY;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (v[i] > mx) { mx = v[i]; arg = c0 + i; }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(mx, o, 64);
+      const int oa = __shfl_xor(arg, o, 64);
+      if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      v[i] = __expf(v[i] - mx);  // exp(-inf) = 0 past cols
+      sum += v[i];
+    }
+    const float inv = 1.0f / wave_sum(sum);
+    float* yr = y + (long long)row * cols;
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+      if (c0 + 4 * h < cols)
+        *reinterpret_cast<float4*>(yr + c0 + 4 * h) =
+            make_float4(v[4 * h] * inv, v[4 * h + 1] * inv, v[4 * h + 2] * inv, v[4 * h + 3] * inv);
+    if (lane == 0 && amax) amax[row] = arg;
+    return;
+  }
   for (int c = lane; c < cols; c += 64) {
     const float v = (float)xr[c];
     if (v > mx) { mx = v; arg = c; }
@@ -267,8 +307,11 @@ __global__ __launch_bounds__(kBlock) void synth_dev_kernel(uint8_t* y, long long
   if (!bump_done) return;
   __syncthreads();  // every thread of this block has read step[0]
   if (threadIdx.x == 0) {
+    // relaxed: the only ordering needed is every block's READ of step[0] before the last
+    // block's increment, and each block consumed its read before the barrier above.  (An
+    // acq_rel ticket writes back the whole L2 per block on gfx950: 19 -> 91 us at b640.)
     const unsigned long long prev = __hip_atomic_fetch_add(
-        reinterpret_cast<unsigned long long*>(step + 1), 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        reinterpret_cast<unsigned long long*>(step + 1), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == gridDim.x - 1ull) {
       __hip_atomic_store(reinterpret_cast<unsigned long long*>(step + 1), 0ull, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);

@@ -30,9 +30,11 @@ from . import reference as _ref
 
 # KVEDGE_CHECKS=1 selects the bounds-check build (python -m kvedge_amd._build with the
 # same variable set): launchers verify operand extents against their HIP allocations.
+# KVEDGE_LIB=<file name in kvedge_amd/> selects another in-tree build of the same sources
+# (A/B of one kernel change on one box: tools/ab_build.sh)
 _LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                          "_C_checks.so" if os.environ.get("KVEDGE_CHECKS", "0") not in ("", "0")
-                         else "_C.so")
+                         else os.path.basename(os.environ.get("KVEDGE_LIB", "") or "_C.so"))
 _loaded = False
 _load_error: Optional[str] = None
 

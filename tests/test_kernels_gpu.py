@@ -243,11 +243,14 @@ def test_maxpool_avgpool_softmax():
         a = ops.global_avgpool(f.cuda()).cpu().float()
         ref = f.float().mean((1, 2))
         assert ((a - ref).abs() <= 2.0 ** -8 * ref.abs() + 1e-4).all(), shp  # one bf16 rounding
-    lg = _rand((5, 1000), 5, 3.0)
-    p, am = ops.softmax_rows(lg.cuda())
-    pr = torch.softmax(lg.float(), 1)
-    assert (p.cpu() - pr).abs().max() < 1e-5
-    assert torch.equal(am.cpu(), lg.float().argmax(1))
+    # 1000 / 1024 / 8 columns: register-resident row path; 1001 / 2000: the strided loop
+    for rows, cols in ((5, 1000), (3, 1024), (2, 8), (4, 1001), (2, 2000)):
+        lg = _rand((rows, cols), 5, 3.0)
+        lg[0, cols // 3] = lg[0, cols // 2] = lg[0].max() + 1  # tie -> the lower index
+        p, am = ops.softmax_rows(lg.cuda())
+        pr = torch.softmax(lg.float(), 1)
+        assert (p.cpu() - pr).abs().max() < 1e-5, (rows, cols)
+        assert torch.equal(am.cpu(), lg.float().argmax(1)), (rows, cols)
 
 
 def test_sppf_and_upsample():

@@ -88,6 +88,9 @@ def main():
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     L = layers(a.batch)
+    # the step-counter bump is its own launch only in traces older than the in-kernel bump
+    if not any("bump_kernel" in r["Kernel_Name"] for r in rows):
+        L = [x for x in L if x[1] != "bump"]
     starts = [i for i, r in enumerate(rows) if "synth_dev" in r["Kernel_Name"]]
     step = None
     for s in reversed(starts):  # the last complete step
