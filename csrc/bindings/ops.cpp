@@ -5,7 +5,6 @@
 // whole forward built from these ops can be captured into one hipGraph
 // (kvedge_amd/engine).  Shapes/strides are computed by the Python wrappers in
 // kvedge_amd/ops/__init__.py; this layer only validates and launches.
-#include <cstdlib>
 #include <ATen/ATen.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -29,19 +28,11 @@ void check_bf16(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.scalar_type() == at::kBFloat16, "kvedge: ", name, " must be bf16");
 }
 
-// Split-K workspace: fp32 partial sums in [0, M*Cout); when the tensor also holds the
-// KV_SK_COUNTERS arrival counters at its END (ops.splitk_workspace sizes it so), the tiles
-// finish in-kernel (last slice per tile) instead of in a separate finalize launch.
-// KVEDGE_SK_FINALIZE=1 forces the finalize launch (A/B knob).
-void set_splitk_ws(KvConvParams& p, const at::Tensor& ws, int64_t data_elems) {
-  static const bool force_finalize = [] {
-    const char* e = std::getenv("KVEDGE_SK_FINALIZE");
-    return e && e[0] == '1';
-  }();
+// Split-K workspace: fp32 slabs, one per K slice of the tile ([ksplit][M][Cout]); the
+// launcher refuses a tile whose slabs do not fit (ops.splitk_workspace sizes it per tile).
+void set_splitk_ws(KvConvParams& p, const at::Tensor& ws) {
   p.ws = ws.data_ptr<float>();
-  p.sk_cnt = nullptr;
-  if (!force_finalize && ws.numel() >= data_elems + KV_SK_COUNTERS)
-    p.sk_cnt = reinterpret_cast<int*>(p.ws + ws.numel() - KV_SK_COUNTERS);
+  p.ws_elems = ws.numel();
 }
 
 void conv(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
@@ -57,9 +48,8 @@ void conv(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
   KvConvParams p{};
   if (ws.has_value() && ws->defined()) {  // split-K workspace (v8 tiles): fp32, zero, >= M*Cout
     check_dev(*ws, "ws");
-    TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= N * Ho * Wo * Cout,
-                "kvedge: split-K workspace fp32[M*Cout]");
-    set_splitk_ws(p, *ws, N * Ho * Wo * Cout);
+    TORCH_CHECK(ws->scalar_type() == at::kFloat, "kvedge: split-K workspace fp32");
+    set_splitk_ws(p, *ws);
   }
   p.x = x.data_ptr();
   p.w = w.data_ptr();
@@ -137,9 +127,8 @@ void conv_dual(const at::Tensor& x1, const at::Tensor& x2, const at::Tensor& w,
   p.ldx2 = (int)K2; p.stride2 = (int)stride2;
   if (ws.has_value() && ws->defined()) {
     check_dev(*ws, "ws");
-    TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= (int64_t)p.M * Cout,
-                "kvedge: split-K workspace fp32[M*Cout]");
-    set_splitk_ws(p, *ws, (int64_t)p.M * Cout);
+    TORCH_CHECK(ws->scalar_type() == at::kFloat, "kvedge: split-K workspace fp32");
+    set_splitk_ws(p, *ws);
   }
   const int rc = kv_conv2d(&p, (int)tile, cur_stream(x1));
   TORCH_CHECK(rc == 0, "kvedge: conv_dual failed rc=", rc);

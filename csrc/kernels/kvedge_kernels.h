@@ -49,18 +49,14 @@ typedef struct KvConvParams {
   const float* bias_t;
   void* z;
   int n_t, ldz, z_coff, act_t;
-  // Split-K (v8 tiles, small-M layers: edge batches): the launch adds fp32 partial sums
-  // of its K slice into ws [M][Cout] (zero on entry).  sk_cnt != NULL (KV_SK_COUNTERS
-  // zeroed ints, one per output tile): the last slice of a tile to arrive applies bias,
-  // residual and activation, writes y and re-zeroes its ws tile and counter in the same
-  // launch; sk_cnt = NULL: a separate finalize kernel does that.  ws = NULL: v8 refuses.
+  // Split-K (v8 tiles, small-M layers: edge batches): K slice z of the launch writes its fp32
+  // partial sums to slab z of ws [ksplit][M][Cout] with plain 16-B stores, and a finalize
+  // kernel sums the slabs, applies bias, residual and activation and writes y.  ws = NULL:
+  // v8 tiles refuse.  (ksplit is set by the tile; ws must hold ksplit x M x Cout floats.)
   float* ws;
   int ksplit;
-  int* sk_cnt;
+  long long ws_elems;  // floats in ws
 } KvConvParams;
-
-// ints reserved at the END of a split-K workspace tensor for the per-tile arrival counters
-#define KV_SK_COUNTERS 4096
 
 // tile: -1 = heuristic; otherwise an index into the tile table (kv_conv_num_tiles()).
 int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream);

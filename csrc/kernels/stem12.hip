@@ -121,13 +121,9 @@ __global__ __launch_bounds__(kNT, 2) void stem12_pool_kernel(
 
   // Raw prefetch of s2d rows [Ylo, Ylo + nrows) of image n (rows outside the image and
   // loads past the row count read nothing and commit zeros).
-  // Two register sets: the band loop keeps the next TWO bands' raw bytes in flight.  A
-  // band's MFMA phase is ~0.7 us per wave, below the loaded-HBM latency: with one band of
-  // prefetch every commit waited (vmcnt(0)) on the fetch issued at its own band's start.
-  typedef u32x3 RawSet[kMaxLoads];
-  RawSet rawA, rawB;
-  unsigned okA = 0, okB = 0;
-  auto fetch = [&](RawSet& raw, unsigned& okm, int n, int Ylo, int nrows) __attribute__((always_inline)) {
+  u32x3 raw[kMaxLoads];
+  unsigned okm = 0;
+  auto fetch = [&](int n, int Ylo, int nrows) __attribute__((always_inline)) {
     okm = 0;
 #pragma unroll
     for (int i = 0; i < kMaxLoads; ++i) {
@@ -155,7 +151,7 @@ __global__ __launch_bounds__(kNT, 2) void stem12_pool_kernel(
     }
   };
   // write the fetched rows (and zeros for the rows that are outside the image)
-  auto commit = [&](const RawSet& raw, unsigned okm, int Ylo, int nrows) __attribute__((always_inline)) {
+  auto commit = [&](int Ylo, int nrows) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < kMaxLoads; ++i) {
       const int q = tid + kNT * i;
@@ -251,52 +247,39 @@ __global__ __launch_bounds__(kNT, 2) void stem12_pool_kernel(
     const int lo = ys - 2, hi = min(2 * P + 1, Hs - 1) + 1;  // s2d rows [lo, hi]
     for (int Y = lo; Y <= hi; Y += 3) {
       const int cnt = min(3, hi - Y + 1);
-      fetch(rawA, okA, n, Y, cnt);
-      commit(rawA, okA, Y, cnt);
+      fetch(n, Y, cnt);
+      commit(Y, cnt);
     }
   }
-  // the band after (cn, cP): image, pooled row and its NEW s2d rows [lo, lo + cnt); at an
-  // image start rows -2 .. 2, of which the raw loads cover 0 .. 2 (-2, -1 are zeroed)
-  struct Next {
-    int n, P, lo, cnt;
-  };
-  auto next_of = [&](int cn, int cP) __attribute__((always_inline)) {
-    Next r{cn, cP + 1, 2 * cP + 3, 2};
-    if (r.P == Hp) r = Next{cn + 1, 0, -2, 5};
-    return r;
-  };
-  // raw loads of a band's new rows; every band issues them (no rows past the range: the
-  // lanes read beyond the descriptor) so every path has the same loads younger than the
-  // set being committed and its wait stays counted, not vmcnt(0)
-  auto fetch_band = [&](RawSet& raw, unsigned& okm, const Next& t, bool live) __attribute__((always_inline)) {
-    fetch(raw, okm, t.n, t.lo < 0 ? 0 : t.lo, live ? (t.lo < 0 ? 3 : t.cnt) : 0);
-  };
-  Next t1 = next_of(n, P);
-  fetch_band(rawB, okB, t1, b0 + 1 < b1);  // band b0+1 -> set B
   __syncthreads();
 
-  // band b (relative index k = b - b0): band k+1's raw bytes are in set (k+1) & 1, band k+2's
-  // go into set k & 1 (band k's own, committed one band ago)
-  auto band = [&](auto SET, int b) __attribute__((always_inline)) {
-    RawSet& rnext = decltype(SET)::value ? rawA : rawB;
-    unsigned& onext = decltype(SET)::value ? okA : okB;
-    RawSet& rfar = decltype(SET)::value ? rawB : rawA;
-    unsigned& ofar = decltype(SET)::value ? okB : okA;
+  for (int b = b0; b < b1; ++b) {
     const int ye = min(2 * P + 2, Hs);
-    const Next t2 = next_of(t1.n, t1.P);
-    fetch_band(rfar, ofar, t2, b + 2 < b1);
+    // next band's new s2d rows, into registers while this band's MFMAs run
+    const int bn = b + 1;
+    int nn = n, nP = P + 1, nlo = 2 * P + 3, ncnt = 2;
+    if (nP == Hp) {  // next band starts an image: s2d rows -2 .. 2 (-2, -1 are zero)
+      nn = n + 1;
+      nP = 0;
+      nlo = -2;
+      ncnt = 5;
+    }
+    const bool more = bn < b1;
+    // raw loads: data rows only (nlo = -2: rows 0..2 -> fetch (0, 3), zero rows committed
+    // from the same call through the range check)
+    if (more) fetch(nn, nlo < 0 ? 0 : nlo, nlo < 0 ? 3 : ncnt);
     stem_rows(ys, ye);
     __syncthreads();  // stem rows done; this band's s2d rows no longer read
-    if (b + 1 < b1) {
-      if (t1.lo < 0) {
-        commit(rnext, onext, 0, 3);
+    if (more) {
+      if (nlo < 0) {
+        commit(0, 3);
         // zero rows -2, -1: 2 x Ws s2d pixels x 24 B
         for (int i = tid; i < 2 * Ws * 3; i += kNT) {
           const int r = i / (Ws * 3), q = i - r * (Ws * 3);
           *reinterpret_cast<uint2*>(ring + ring6(-2 + r) * RP + 48 + q * 8) = make_uint2(0, 0);
         }
       } else {
-        commit(rnext, onext, t1.lo, t1.cnt);
+        commit(nlo, ncnt);
       }
     }
     // ---- 3x3/2 max pool of pooled row P (stem rows 2P-1 .. 2P+1, clamped) -> global
@@ -330,14 +313,9 @@ __global__ __launch_bounds__(kNT, 2) void stem12_pool_kernel(
       }
     }
     __syncthreads();  // pool reads done (stem slots reusable); committed rows visible
-    n = t1.n;
-    P = t1.P;
+    n = nn;
+    P = nP;
     ys = 2 * P;
-    t1 = t2;
-  };
-  for (int b = b0; b < b1; b += 2) {
-    band(IC<0>{}, b);  // k even: next in B, far into A
-    if (b + 1 < b1) band(IC<1>{}, b + 1);
   }
 }
 

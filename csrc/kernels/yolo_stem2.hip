@@ -104,13 +104,9 @@ __global__ __launch_bounds__(kNT, 2) void yolo_stem2_kernel(
   const int ups = 2 * upr;       // units per s2d row (two frame rows)
 
   // raw fetch of s2d rows [Y0, Y0 + nrows) of image n (rows outside [0, Hs) load nothing)
-  // into one register set; two sets: the band loop keeps the next TWO bands' raw bytes in
-  // flight (a band's compute is ~1 us, below the loaded-HBM latency: with one band of
-  // prefetch every band's commit waited on the fetch issued at its start)
-  typedef u32x3 RawSet[kMaxLoads];
-  RawSet rawA, rawB;
-  unsigned okA = 0, okB = 0;
-  auto fetch = [&](RawSet& raw, unsigned& okm, int n, int Y0, int nrows) __attribute__((always_inline)) {
+  u32x3 raw[kMaxLoads];
+  unsigned okm = 0;
+  auto fetch = [&](int n, int Y0, int nrows) __attribute__((always_inline)) {
     okm = 0;
 #pragma unroll
     for (int i = 0; i < kMaxLoads; ++i) {
@@ -125,7 +121,7 @@ __global__ __launch_bounds__(kNT, 2) void yolo_stem2_kernel(
     }
   };
   // s2d pixel (dy row part): channels dy*8 + dx*4 + c = byte (dx*3 + c) of the 6-byte group
-  auto commit = [&](const RawSet& raw, unsigned okm, int Y0, int nrows) __attribute__((always_inline)) {
+  auto commit = [&](int Y0, int nrows) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < kMaxLoads; ++i) {
       const int u = tid + kNT * i;
@@ -229,59 +225,38 @@ __global__ __launch_bounds__(kNT, 2) void yolo_stem2_kernel(
   int n = bb / H1, yo = bb - (bb / H1) * H1;
   if (yo == 0) {
     zero_row(sring + mod3(-1) * SR + kSP, Ws * kSP);  // s2d row -1
-    fetch(rawA, okA, n, 0, 2);
-    commit(rawA, okA, 0, 2);
+    fetch(n, 0, 2);
+    commit(0, 2);
   } else {
     // stem row 2yo-1 needs s2d rows 2yo-2, 2yo-1; the band's own stem rows need 2yo-1..2yo+1
-    fetch(rawA, okA, n, 2 * yo - 2, 2);
-    commit(rawA, okA, 2 * yo - 2, 2);
+    fetch(n, 2 * yo - 2, 2);
+    commit(2 * yo - 2, 2);
     __syncthreads();
     stem_rows(2 * yo - 1, 1);
     __syncthreads();  // s2d row 2yo-2 no longer read: its slot takes row 2yo+1
-    fetch(rawA, okA, n, 2 * yo, 2);
-    commit(rawA, okA, 2 * yo, 2);
+    fetch(n, 2 * yo, 2);
+    commit(2 * yo, 2);
   }
-  // (image, row) of band b + 1 and b + 2
-  auto next_band = [&](int cn, int cyo, int& nn, int& nyo) __attribute__((always_inline)) {
-    nn = cyo + 1 < H1 ? cn : cn + 1;
-    nyo = cyo + 1 < H1 ? cyo + 1 : 0;
-  };
-  int n1, yo1;
-  next_band(n, yo, n1, yo1);
-  fetch(rawB, okB, n1, 2 * yo1, bb + 1 < be ? 2 : 0);  // band bb+1 -> set B (relative index 1)
   __syncthreads();
 
-  // band b (relative index k = b - bb): raw bytes of band k+1 are in set (k+1) & 1, band
-  // k+2's go into set k & 1 (band k's own, committed one band ago)
-  auto band = [&](auto SET, int b) __attribute__((always_inline)) {
-    RawSet& rnext = decltype(SET)::value ? rawA : rawB;   // band k+1's bytes
-    unsigned& onext = decltype(SET)::value ? okA : okB;
-    RawSet& rfar = decltype(SET)::value ? rawB : rawA;    // band k+2 lands here
-    unsigned& ofar = decltype(SET)::value ? okB : okA;
+  for (int b = bb; b < be; ++b) {
     // stem row 2yo-1 = zero at an image start (its slot is not written by this band)
     if (yo == 0) zero_row(tring + mod3(-1) * TR, TR);
-    int n2, yo2;
-    next_band(n1, yo1, n2, yo2);
-    // issued on every band (no rows when there is no band b+2: the lanes read past the
-    // descriptor and load zeros) so each path has the same 3 loads younger than band k+1's
-    // and the commit below waits vmcnt(3 + ...), not vmcnt(0)
-    fetch(rfar, ofar, n2, 2 * yo2, b + 2 < be ? 2 : 0);
+    const bool more = b + 1 < be;
+    const int nn = yo + 1 < H1 ? n : n + 1;
+    const int nyo = yo + 1 < H1 ? yo + 1 : 0;
+    // next band's new s2d rows (2 nyo, 2 nyo + 1): raw bytes in flight during this band
+    if (more) fetch(nn, 2 * nyo, 2);
     stem_rows(2 * yo, 2);
     __syncthreads();  // stem rows written; s2d rows of this band no longer read
-    if (b + 1 < be) {
-      if (yo1 == 0) zero_row(sring + mod3(-1) * SR + kSP, Ws * kSP);
-      commit(rnext, onext, 2 * yo1, 2);
+    if (more) {
+      if (nyo == 0) zero_row(sring + mod3(-1) * SR + kSP, Ws * kSP);
+      commit(2 * nyo, 2);
     }
     b1_row(n, yo);
     __syncthreads();  // stem ring free for the next band; committed s2d rows visible
-    n = n1;
-    yo = yo1;
-    n1 = n2;
-    yo1 = yo2;
-  };
-  for (int b = bb; b < be; b += 2) {
-    band(IC<0>{}, b);  // k even: next in B, far into A
-    if (b + 1 < be) band(IC<1>{}, b + 1);
+    n = nn;
+    yo = nyo;
   }
 }
 

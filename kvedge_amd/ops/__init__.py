@@ -197,27 +197,29 @@ def unpack_conv_weight(wp: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
 # ---------------------------------------------------------------------------
 # ops
 # ---------------------------------------------------------------------------
-# Split-K workspaces (v8 tiles): fp32, all zero between uses -- the finalize kernel of every
-# split-K layer zeroes what it read -- one per (device, stream), since layers on one stream
-# run in order while the multi-stream engine's slices run concurrently.  Sized on first use
-# (warm-up, before hipGraph capture), grown when a larger layer needs it.
+# Split-K workspaces (v8 tiles): fp32 slabs [ksplit][M][Cout], one per K slice of a tile
+# (plain stores; the finalize kernel sums them), one workspace per (device, stream), since
+# layers on one stream run in order while the multi-stream engine's slices run concurrently.
+# Sized on first use (warm-up, before hipGraph capture) for the largest split (32) that fits
+# under SPLITK_MAX_ELEMS; a tile whose slabs do not fit is refused by the launcher (the
+# autotuner skips it), so big layers only ever take their smaller splits.
 _WS: dict = {}
-SPLITK_MAX_ELEMS = 16 << 20  # layers with M*Cout above this never split (64 MB of fp32)
-N_SPLITK_TILES = 13          # conv_sk.hip kSkTiles: the LAST tile indices
+SPLITK_MAX_ELEMS = 32 << 20  # 128 MB of fp32 per stream at most
+SPLITK_MAX_SPLIT = 32        # largest split of conv_sk.hip kSkTiles
+N_SPLITK_TILES = 19          # conv_sk.hip kSkTiles: the LAST tile indices
 SPLITK0 = 1 << 30            # first split-K tile index, set by load()
-SK_COUNTERS = 4096           # KV_SK_COUNTERS: per-tile arrival counters at the workspace's end
 
 
 def splitk_workspace(device: torch.device, elems: int) -> Optional[torch.Tensor]:
-    """The stream's split-K workspace: >= ``elems`` fp32 partial sums plus SK_COUNTERS int32
-    arrival counters at its end (the last K slice of a tile finishes it in-kernel and
-    re-arms its counter; csrc/kernels/conv_glds_kernel.inc).  All zero between layers."""
-    if elems > SPLITK_MAX_ELEMS:
+    """The stream's split-K workspace for a layer of ``elems`` = M x Cout outputs: room for
+    up to SPLITK_MAX_SPLIT slabs, capped at SPLITK_MAX_ELEMS (None if not even one fits)."""
+    if elems > SPLITK_MAX_ELEMS // 2:
         return None
+    want = min(elems * SPLITK_MAX_SPLIT, SPLITK_MAX_ELEMS)
     key = (device.index, torch.cuda.current_stream(device).cuda_stream)
     ws = _WS.get(key)
-    if ws is None or ws.numel() < elems + SK_COUNTERS:
-        ws = torch.zeros(max(elems, 1 << 16) + SK_COUNTERS, dtype=torch.float32, device=device)
+    if ws is None or ws.numel() < want:
+        ws = torch.empty(max(want, 1 << 16), dtype=torch.float32, device=device)
         _WS[key] = ws
     return ws
 

@@ -103,7 +103,7 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale
 
 
-N_TILES = 97  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue (68-83) + v8 split-K (84-96)
+N_TILES = 103  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue (68-83) + v8 split-K (84-102)
 # + v6 A-resident N-loop 1x1 GEMM (58-67, conv_nloop.hip kNlTiles: one Kpad per tile;
 # 63-65 are the fused-downsample (dual) forms, 66-67 step 128 K at a time)
 NLOOP0 = 58
@@ -605,12 +605,14 @@ def test_conv_tail_fused(case, mf):
     (1, 14, 14, 512, 512, 3, 2, ops.ACT_RELU, False),     # s4 block-0 3x3 / 2
 ])
 def test_conv_splitk(tile, case):
-    """v8 split-K: K slices add fp32 partials into the stream's workspace, the finalize
-    kernel applies bias / residual / activation, writes bf16 and re-zeroes the workspace
-    (checked: the next split-K layer on the stream relies on it)."""
+    """v8 split-K: each K slice writes its fp32 partial tile to its own slab of the stream's
+    workspace (plain stores), the finalize kernel sums the slabs and applies bias / residual
+    / activation.  The workspace is poisoned with NaN first: no output may depend on its old
+    contents (every slab element the finalize reads is written by its slice)."""
     N, H, W, cin, cout, k, s, act, res = case
+    Ho, Wo = (H + 2 * (k // 2) - k) // s + 1, (W + 2 * (k // 2) - k) // s + 1
+    ws = ops.splitk_workspace(torch.device("cuda", torch.cuda.current_device()), N * Ho * Wo * cout)
+    assert ws is not None
+    ws.fill_(float("nan"))
     err, scale = _conv_case(N, H, W, cin, cout, k, s, k // 2, act, res=res, tile=tile)
     assert err <= 0.02 * scale, (tile, case, err, scale)
-    ws = ops.splitk_workspace(torch.device("cuda", torch.cuda.current_device()), 1)
-    torch.cuda.synchronize()
-    assert int((ws != 0).sum()) == 0
