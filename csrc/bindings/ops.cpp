@@ -87,6 +87,48 @@ void conv(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
   TORCH_CHECK(rc == 0, "kvedge: kv_conv2d failed rc=", rc);
 }
 
+// Fused Detect-branch pair (v4 direct tiles): z[.., z_coff : z_coff + C2] =
+//   act(conv3x3/1(x[.., x_coff : x_coff + Cin]) + bias) . W2^T + b2
+// t = the 3x3's activated output stays in LDS (never written); tile = v4 direct tile 0-3.
+void conv_pair(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias,
+               const at::Tensor& w2, const at::Tensor& b2, at::Tensor& z, int64_t Cin,
+               int64_t x_coff, int64_t z_coff, int64_t act, int64_t tile) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_bf16(w2, "w2");
+  check_bf16(z, "z");
+  check_dev(bias, "bias");
+  check_dev(b2, "b2");
+  TORCH_CHECK(x.dim() == 4 && z.dim() == 4 && w.dim() == 2 && w2.dim() == 2, "kvedge: conv_pair shapes");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), ldx = x.size(3);
+  const int64_t Cout = w.size(0), C2 = w2.size(0);
+  TORCH_CHECK(w2.size(1) == Cout, "kvedge: conv_pair w2 must be [C2, Cout]");
+  TORCH_CHECK(z.size(0) == N && z.size(1) == H && z.size(2) == W && z_coff + C2 <= z.size(3),
+              "kvedge: conv_pair z [N, H, W, >= z_coff + C2]");
+  TORCH_CHECK(x_coff + Cin <= ldx && w.size(1) == (9 * Cin + 63) / 64 * 64, "kvedge: conv_pair x / w");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() >= Cout && b2.scalar_type() == at::kFloat &&
+              b2.numel() >= C2, "kvedge: conv_pair biases fp32");
+  TORCH_CHECK(N * H * W * ldx * 2 < (1ll << 31) && N * H * W * z.size(3) * 2 < (1ll << 31),
+              "kvedge: conv_pair operands exceed 2 GiB");
+  const c10::DeviceGuard g(x.device());
+  KvConvParams p{};
+  p.x = x.data_ptr();
+  p.w = w.data_ptr();
+  p.bias = bias.data_ptr<float>();
+  p.N = (int)N; p.H = (int)H; p.W = (int)W; p.Cin = (int)Cin;
+  p.ldx = (int)ldx; p.x_coff = (int)x_coff;
+  p.Ho = (int)H; p.Wo = (int)W; p.Cout = (int)Cout;
+  p.KH = 3; p.KW = 3; p.stride = 1; p.pad = 1;
+  p.K = (int)(9 * Cin); p.Kpad = (int)w.size(1);
+  p.M = (int)(N * H * W);
+  p.act = (int)act; p.mode = 0;
+  p.w_t = w2.data_ptr(); p.bias_t = b2.data_ptr<float>(); p.z = z.data_ptr();
+  p.n_t = (int)C2; p.ldz = (int)z.size(3); p.z_coff = (int)z_coff;
+  p.pair_1x1 = 1;
+  const int rc = kv_conv_pair(&p, (int)tile, cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: conv_pair failed rc=", rc);
+}
+
 // Bottleneck conv3 with the downsample branch folded in as extra K (mode 4):
 //   y = act( x1 (1x1) . W[:, :K1]  +  x2 (1x1, stride s2) . W[:, K1:]  + bias )
 void conv_dual(const at::Tensor& x1, const at::Tensor& x2, const at::Tensor& w,
@@ -574,6 +616,8 @@ TORCH_LIBRARY(kvedge, m) {
         "int Cin, int ldx, int x_coff, int Ho, int Wo, int Cout, int KH, int KW, int stride, "
         "int pad, int K, int ldy, int y_coff, int ldr, int r_coff, int act, int mode, int tile, "
         "Tensor(b!)? ws=None) -> ()");
+  m.def("conv_pair(Tensor x, Tensor w, Tensor bias, Tensor w2, Tensor b2, Tensor(a!) z, int Cin, "
+        "int x_coff, int z_coff, int act, int tile) -> ()");
   m.def("conv_dual(Tensor x1, Tensor x2, Tensor w, Tensor? bias, Tensor(a!) y, int stride2, int act, "
         "int tile, Tensor(b!)? ws=None) -> ()");
   m.def("conv_tail(Tensor x, Tensor? x2, Tensor w, Tensor? bias, Tensor? res, Tensor(a!) y, "
@@ -614,6 +658,7 @@ TORCH_LIBRARY_IMPL(kvedge, CUDA, m) {
   m.impl("stem_pool", stem_pool);
   m.impl("conv_frames_s2d", conv_frames_s2d);
   m.impl("conv_tail", conv_tail);
+  m.impl("conv_pair", conv_pair);
   m.impl("conv_block", conv_block);
   m.impl("sppf_pool", sppf_pool);
   m.impl("global_avgpool", global_avgpool);

@@ -75,8 +75,13 @@ __host__ __device__ constexpr int direct_patch_alloc(int patch_bytes, bool dma) 
 // 180 weight VGPRs and had room for a single 80-pixel output row per band otherwise).
 // Lane-linear DMA slots of 16 B; slot q = (pixel q / SL, chunk q % SL) with SL = PB / 16,
 // the pitch-padding chunk (q % SL == CPP) gets an out-of-range offset (zero fill).
+// C2 > 0: fused 1x1 pair (YOLO Detect branch: 3x3 + SiLU, then a 1x1 with bias and no
+// activation, C2 output channels).  The band's 3x3 output t stays in the LDS output tile
+// (bf16, as the unfused layer would have stored it) and the 1x1 runs on it from there:
+// z = t . W2^T + b2 goes to p.z [M][ldz] at z_coff and t never reaches HBM -- one launch and
+// one tensor round trip less per Detect branch.  W2 [C2][COUT] and b2 sit in LDS.
 template <int CIN, int COUT, int S, int KK, int ACT, bool RES, bool U8 = false, bool DMA = false,
-          bool PAIRS = false, int OCC = 1, int NT = kNT>
+          bool PAIRS = false, int OCC = 1, int NT = kNT, int C2 = 0>
 // OCC = workgroups per CU the launch plans for (1 or 2); the second launch-bounds argument
 // is HIP's minimum waves per SIMD (512 threads = 2 per SIMD per workgroup).  The narrow
 // (16/32-channel) layers are latency-bound at one workgroup per CU -- one band in flight,
@@ -102,6 +107,8 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
   // sit out the MFMA phase and only help with the patch fetch and the store pass
   constexpr int NPH = (NT / 64) / NCB;
   constexpr int OS = COUT + 8;           // output tile pixel stride (elements)
+  static_assert(C2 == 0 || (!RES && !U8 && KK == 3 && COUT % 16 == 0), "pair form");
+  constexpr int NCB2 = (C2 + 31) / 32;   // pair: 32-channel blocks of the 1x1's output
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   static_assert(!(DMA && U8), "DMA patch fetch: bf16 NHWC inputs only");
   const int psz = direct_patch_alloc(patch_rows * PW * C::PB, DMA);
@@ -129,6 +136,21 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
   float* lbias = reinterpret_cast<float*>(
       reinterpret_cast<unsigned char*>(otile) + ((kR * p.Wo * OS * 2 + 15) & ~15));
   if (tid < NCB * 32) lbias[tid] = (p.bias && tid < COUT) ? p.bias[tid] : 0.f;
+  // pair: b2 [NCB2 * 32] then W2 [NCB2 * 32][OS] (rows past C2 zero) above the bias slot;
+  // the W2 row pitch equals the output tile's (conflict-free ds_read_b128 of 16 rows)
+  float* lbias2 = lbias + 128;
+  bf16* w2s = reinterpret_cast<bf16*>(lbias2 + 128);
+  if constexpr (C2 > 0) {
+    static_assert(NCB2 * 32 <= 128 && NCB * 32 <= 128, "pair bias slots");
+    if (tid < NCB2 * 32) lbias2[tid] = (p.bias_t && tid < C2) ? p.bias_t[tid] : 0.f;
+    const bf16* w2 = reinterpret_cast<const bf16*>(p.w_t);
+    for (int q = tid; q < NCB2 * 32 * (COUT / 8); q += NT) {
+      const int r = q / (COUT / 8), c = (q - r * (COUT / 8)) * 8;
+      bf16x8 v = {};
+      if (r < C2) v = *reinterpret_cast<const bf16x8*>(w2 + (size_t)r * COUT + c);
+      *reinterpret_cast<bf16x8*>(w2s + r * OS + c) = v;
+    }
+  }
 
   // ---- band patch prefetch: 16-B chunk q -> patch pixel q / CPP (row-major, pitch PW)
   const int nchunks = patch_rows * PW * C::CPP;
@@ -265,7 +287,7 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
   // its stores to be acknowledged -- one HBM write latency per band on every CU.  Split, the
   // DMA waves have no stores outstanding and the store waves never wait on vmcnt.
   constexpr int NWV = NT / 64;
-  constexpr bool SPLIT = DMA && !RES && NWV >= 4;
+  constexpr bool SPLIT = DMA && !RES && NWV >= 4 && C2 == 0;
   constexpr int NWD = SPLIT ? NWV / 2 : NWV;  // waves issuing the patch DMA
   auto dma_fetch = [&](int item, unsigned char* dst) __attribute__((always_inline)) {
     const int n = item / nbands, band = item - n * nbands;
@@ -428,8 +450,49 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
         }
       }
     }
+    if constexpr (C2 > 0) {
+      // ---- pair: z = t . W2^T + b2 from the output tile, 32 pixels x 32 channels per unit,
+      // stored straight from the accumulators (a lane: 4 consecutive channels of a pixel)
+      bf16* __restrict__ Z = reinterpret_cast<bf16*>(p.z);
+      for (int u = wv; u < nblk * NCB2; u += NWV) {
+        const int b = u / NCB2, cb2 = u - b * NCB2;
+        floatx16 acc2;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 bv = *reinterpret_cast<const float4*>(lbias2 + cb2 * 32 + g * 8 + fh * 4);
+          acc2[4 * g + 0] = bv.x;
+          acc2[4 * g + 1] = bv.y;
+          acc2[4 * g + 2] = bv.z;
+          acc2[4 * g + 3] = bv.w;
+        }
+        const bf16* tp = otile + (b * 32 + fr) * OS + fh * 8;  // rows past npix: discarded
+        const bf16* wp2 = w2s + (cb2 * 32 + fr) * OS + fh * 8;
+#pragma unroll
+        for (int ks = 0; ks < COUT / 16; ++ks)
+          acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              *reinterpret_cast<const bf16x8*>(wp2 + ks * 16),
+              *reinterpret_cast<const bf16x8*>(tp + ks * 16), acc2, 0, 0, 0);
+        const int jr = b * 32 + fr;
+        if (jr < npix) {
+          const int yl = fdiv(jr, fWo), xc = jr - yl * Wo;
+          const int oy = oy0 + yl;
+          if (oy < Ho) {
+            bf16* zp = Z + ((long long)(n * Ho + oy) * Wo + xc) * p.ldz + p.z_coff + cb2 * 32 + fh * 4;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              if (cb2 * 32 + g * 8 >= C2) continue;  // compile-time for C2 % 32 == 0
+              bf16x4 o;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) o[e] = f2bf(acc2[4 * g + e]);
+              *reinterpret_cast<bf16x4*>(zp + g * 8) = o;
+            }
+          }
+        }
+      }
+    }
     constexpr int SB = SPLIT ? NWD * 64 : 0;  // first storing thread
-    for (int q = RPF > 0 && rpre ? npix * OCH : tid - SB; q < npix * OCH; q += NT - SB) {
+    for (int q = C2 > 0 ? npix * OCH : RPF > 0 && rpre ? npix * OCH : tid - SB; q < npix * OCH;
+         q += NT - SB) {
       if (SPLIT && q < 0) break;  // a DMA wave
       const int px = q / OCH, c = q - (q / OCH) * OCH;
       const int yl = fdiv(px, fWo), xc = px - yl * Wo;
@@ -465,6 +528,7 @@ struct DirectEntry {
   bool pairs = false;  // frames-in with even W: 12-B paired raw-row loads
   int occ = 1;         // workgroups per CU (launch bounds, LDS budget, grid)
   int nt = kNT;        // threads per workgroup
+  int c2 = 0;          // fused 1x1 pair: its output channels (0 = plain conv)
 };
 
 #define KV_DIRECT(CI, CO, S, A, R) {CI, CO, S, 3, A, R, conv3x3_direct_kernel<CI, CO, S, 3, A, R>}
@@ -521,6 +585,14 @@ static const DirectEntry kDirect[] = {
      conv3x3_direct_kernel<16, 16, 1, 2, kActSilu, false, true, false, true>, true, false, true},
     {16, 16, 1, 2, kActSilu, false, conv3x3_direct_kernel<16, 16, 1, 2, kActSilu, false, true>,
      true},
+    // YOLO Detect branch pairs, 3x3 + SiLU then 1x1 (no act) into the head map: box branch
+    // 64 -> 64 -> 64, cls branch 80 -> 80 -> 80 (DMA patch fetch)
+    {64, 64, 1, 3, kActSilu, false,
+     conv3x3_direct_kernel<64, 64, 1, 3, kActSilu, false, false, true, false, 1, kNT, 64>, false,
+     true, false, 1, kNT, 64},
+    {80, 80, 1, 3, kActSilu, false,
+     conv3x3_direct_kernel<80, 80, 1, 3, kActSilu, false, false, true, false, 1, kNT, 80>, false,
+     true, false, 1, kNT, 80},
 };
 #undef KV_DIRECT2
 #undef KV_DIRECT1
@@ -557,6 +629,7 @@ static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* r
       if (e.cin == p->Cin && e.cout == p->Cout && e.stride == p->stride && e.kk == kk &&
           e.act == act && e.res == res && e.u8 == (p->in_u8 != 0) &&
           (!e.u8 || e.pairs == (p->W % 2 == 0)) &&
+          e.c2 == (p->pair_1x1 ? p->n_t : 0) &&
           (pass == 1 || (e.dma == ((tile & 1) != 0) && e.occ == 1 + ((tile >> 1) & 1)))) {
         idx = i;
         break;
@@ -578,8 +651,9 @@ static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* r
   const bool dma = kDirect[idx].dma;
   auto lds_of = [&](int prows, int r) {
     const int np = dma ? 2 : 1;
+    const int c2p = (kDirect[idx].c2 + 31) / 32 * 32;  // pair: b2 slot + W2 [c2p][os]
     return np * direct_patch_alloc(prows * *PW * pb, dma) + ((r * p->Wo * os * 2 + 15) & ~15) +
-           kBiasBytes;
+           kBiasBytes + (c2p ? kBiasBytes + c2p * os * 2 : 0);
   };
   // band height: the tallest that fits (<= 8).  (A "fewest pixel-block rounds" rule was
   // measured slower on YOLO's 32-channel layers at 160^2: the extra halo rows and per-band
@@ -626,7 +700,7 @@ int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   if (tile < 0 || tile >= direct_num_tiles()) return -6;
   int kR, PW, rows, lds;
   if (direct_plan(p, tile, &kR, &PW, &rows, &lds) >= 0) return direct_launch_one(p, tile, stream);
-  if (p->res || p->Cout % 16) return -8;
+  if (p->res || p->Cout % 16 || p->pair_1x1) return -8;
   // validate the whole split before launching anything
   int cuts[8], ncut = 0, done = 0;
   while (done < p->Cout && ncut < 8) {
@@ -657,3 +731,9 @@ int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
 }
 
 }  // namespace kvedge
+
+extern "C" int kv_conv_pair(const KvConvParams* p, int tile, hipStream_t stream) {
+  if (!p->pair_1x1 || p->n_t <= 0 || !p->w_t || !p->z) return -8;
+  return kvedge::direct_launch(p, tile, stream);
+}
+extern "C" int kv_conv_pair_num_tiles(void) { return kvedge::direct_num_tiles(); }

@@ -45,10 +45,14 @@ typedef struct KvConvParams {
   // z = ReLU(y . w_t^T + bias_t) -- the NEXT block's 1x1 reduce conv -- is computed from
   // the y tile still in LDS (w_t: bf16 [n_t][Cout], resident) and written to
   // z[m * ldz + z_coff + n]: y is never re-read from HBM.  n_t = 0: no tail.
+  // pair_1x1 = 1 (v4 direct tiles, 3x3 stride 1): the same fields describe a 1x1 conv
+  // (w_t [n_t][Cout], bias_t, no activation) applied to the 3x3's activated output, whose
+  // result goes to z; y is not written (YOLO Detect branch pairs).
   const void* w_t;
   const float* bias_t;
   void* z;
   int n_t, ldz, z_coff, act_t;
+  int pair_1x1;
   // Split-K (v8 tiles, small-M layers: edge batches): K slice z of the launch writes its fp32
   // partial sums to slab z of ws [ksplit][M][Cout] with plain 16-B stores, and a finalize
   // kernel sums the slabs, applies bias, residual and activation and writes y.  ws = NULL:
@@ -66,6 +70,10 @@ int kv_conv_num_tiles(void);
 // host replay of the v6 (conv_nloop.hip) counted-wait schedules: 0 = every tile is safe
 int kv_nloop_sched_check(void);
 int kv_conv_pick_tile(const KvConvParams* p);
+// Fused 3x3 + 1x1 pair on the v4 direct family (p->pair_1x1 = 1, see KvConvParams): tile =
+// direct tile 0-3; < 0 when no instantiation covers the shape.
+int kv_conv_pair(const KvConvParams* p, int tile, hipStream_t stream);
+int kv_conv_pair_num_tiles(void);
 
 // Fused 64-wide bottleneck body (conv_block.hip), all NHWC bf16 at one H x W, stride 1:
 //   c2 = ReLU(conv3x3(t) + b2)                          t [N,H,W,64], w2 [64][576]

@@ -207,6 +207,17 @@ class InferenceEngine:
         return self._forward()
 
 
+def edge_streams(batch: int) -> int:
+    """Batch slices (HIP streams) for a serving batch: two for even batches of 32 and up --
+    at batch 64 one slice leaves most stage-3/4 launches with fewer workgroups than CUs, and
+    the second slice's kernels fill them -- else one.  KVEDGE_EDGE_STREAMS=n overrides."""
+    env = os.environ.get("KVEDGE_EDGE_STREAMS", "")
+    if env:
+        n = int(env)
+        return n if n >= 1 and batch % n == 0 else 1
+    return 2 if batch >= 32 and batch % 2 == 0 else 1
+
+
 def edge_latency(model: Callable, image_size: int, batches, device="cuda", seed: int = 0,
                  steps: int = 200, warmup: int = 20) -> List[Dict[str, float]]:
     """Edge-serving operating points (module twin ``batch``, default 64): per batch size a
@@ -215,13 +226,15 @@ def edge_latency(model: Callable, image_size: int, batches, device="cuda", seed:
     Run it after any headline timing: it re-pins the model's conv tiles."""
     out = []
     for b in batches:
-        eng = InferenceEngine(model, b, image_size, device=device, seed=seed, use_graph=True)
+        eng = InferenceEngine(model, b, image_size, device=device, seed=seed, use_graph=True,
+                              streams=edge_streams(b))
         eng.prepare(warmup=2, autotune=True)
         for _ in range(warmup):
             eng.run()
         st = eng.measure_latency(steps)
         p50, p99 = st.percentile(50), st.percentile(99)  # ms
-        out.append({"batch": b, "p50_ms": round(p50, 4), "p99_ms": round(p99, 4),
+        out.append({"batch": b, "streams": eng.n_streams, "p50_ms": round(p50, 4),
+                    "p99_ms": round(p99, 4),
                     "images_per_s": round(b / (p50 / 1e3), 1), "steps": steps})
         del eng
     return out

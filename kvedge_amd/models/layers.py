@@ -47,6 +47,15 @@ class record_convs:
         _RECORDER = None
 
 
+def _recorder_active() -> bool:
+    return _RECORDER is not None
+
+
+def _record(layer, key, fn) -> None:
+    """Record a fused layer's call for the autotuner (``layer.tile`` is what it pins)."""
+    _RECORDER.append((layer, key, fn))
+
+
 @dataclass
 class DeployedConv:
     """A conv ready for the kernel: spec + packed bf16 weight + fp32 bias.

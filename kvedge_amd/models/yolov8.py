@@ -26,7 +26,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from .layers import DeployedConv, calibrate_bn, count_flops
+from .layers import DeployedConv, _record, _recorder_active, calibrate_bn, count_flops
 
 ACT_SILU, ACT_NONE = ops.ACT_SILU, ops.ACT_NONE
 NC = 80
@@ -220,6 +220,36 @@ class DSPPF:
         return [self.cv1, self.cv2]
 
 
+class DeployedPair:
+    """A Detect branch's 3x3 (+SiLU) and 1x1 convs run as ONE kernel (ops.conv_pair): the
+    3x3's output never leaves the chip.  ``tile`` = v4 direct tile (autotuned)."""
+
+    # (Cin, Cout, C2) shapes with a direct pair instantiation (csrc/kernels/conv_direct.hip)
+    SHAPES = {(64, 64, 64), (80, 80, 80)}
+
+    def __init__(self, c1: DeployedConv, c2: DeployedConv):
+        self.c1, self.c2 = c1, c2
+        s1, s2 = c1.spec, c2.spec
+        self.fits = (s1.kh == 3 and s1.stride == 1 and s1.act == ACT_SILU and s2.kh == 1 and
+                     s2.act == ACT_NONE and (s1.cin, s1.cout, s2.cout) in self.SHAPES)
+        # the 1x1's packed weight without its K padding: [C2, Cout]
+        self.w2 = c2.w[:, :s1.cout].contiguous()
+        self.tile = 1  # DMA form
+
+    def __call__(self, x, out, x_coff=0, z_coff=0, tile=None):
+        ops.conv_pair(x, self.c1.spec, self.c1.w, self.c1.b, self.w2, self.c2.b, out,
+                      x_coff=x_coff, z_coff=z_coff, tile=self.tile if tile is None else tile)
+        if _recorder_active():
+            s = self.c1.spec
+            key = ("pair", s.cin, s.cout, self.w2.shape[0], tuple(x.shape), x_coff,
+                   tuple(out.shape), z_coff)
+            fn = lambda t, o=out: ops.conv_pair(x, s, self.c1.w, self.c1.b, self.w2,  # noqa: E731
+                                                self.c2.b, o, x_coff=x_coff, z_coff=z_coff,
+                                                tile=t)
+            _record(self, key, fn)
+        return out
+
+
 class DDetectLevel:
     """One Detect level: merged branch stems (64 box + 80 cls) -> two 3x3 -> two 1x1
     heads writing [box 64 | cls 80] slices of one [N,h,w,144] buffer."""
@@ -239,15 +269,21 @@ class DDetectLevel:
         self.a2 = DeployedConv.from_modules(a[2], None, ACT_NONE, device)
         self.b2 = DeployedConv.from_modules(b[2], None, ACT_NONE, device)
         self.nc = d.nc
+        # fused branch pairs (3x3 + SiLU -> 1x1 into the head map, the 3x3 output kept on
+        # chip: ops.conv_pair) where a v4 direct pair form exists; KVEDGE_YOLO_PAIR=0 = A/B off
+        self.pairs = [DeployedPair(self.a1, self.a2), DeployedPair(self.b1, self.b2)]
+
+    fuse_pairs: bool = os.environ.get("KVEDGE_YOLO_PAIR", "1") != "0"
 
     def __call__(self, p):
         N, h, w, _ = p.shape
         s = self.stem(p)
         feat = ops.empty(N, h, w, 4 * REG_MAX + self.nc, dtype=torch.bfloat16, device=p.device)
-        ta = self.a1(s, x_coff=0)
-        self.a2(ta, out=feat, y_coff=0)
-        tb = self.b1(s, x_coff=self.ca)
-        self.b2(tb, out=feat, y_coff=4 * REG_MAX)
+        for pair, xo, zo in ((self.pairs[0], 0, 0), (self.pairs[1], self.ca, 4 * REG_MAX)):
+            if self.fuse_pairs and p.is_cuda and pair.fits:
+                pair(s, feat, x_coff=xo, z_coff=zo)
+            else:
+                pair.c2(pair.c1(s, x_coff=xo), out=feat, y_coff=zo)
         return feat
 
     def convs(self):

@@ -288,7 +288,7 @@ class ModuleApp:
         if cfg.model == "simulated-temperature":
             self.sim = _SimTempModel(cfg.seed)
             return
-        from ..engine import InferenceEngine
+        from ..engine import InferenceEngine, edge_streams
 
         dev = self.device
         if cfg.model == "resnet50":
@@ -304,7 +304,8 @@ class ModuleApp:
         camera = cfg.source == "camera"
         self.engine = InferenceEngine(self.model, cfg.batch, cfg.resolved_image_size(), device=dev,
                                       seed=cfg.seed + self.rank, use_graph=cfg.use_graph,
-                                      synthetic=not camera)
+                                      synthetic=not camera,
+                                      streams=edge_streams(cfg.batch) if dev.type == "cuda" else 1)
         self.engine.prepare(warmup=1, autotune=dev.type == "cuda")
         if camera:
             from ..runtime import FrameRing

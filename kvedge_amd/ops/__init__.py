@@ -245,6 +245,27 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, w: torch.Tensor, bias: Optional[torc
     return out
 
 
+def conv_pair(x: torch.Tensor, spec: ConvSpec, w: torch.Tensor, bias: torch.Tensor,
+              w2: torch.Tensor, b2: torch.Tensor, out: torch.Tensor, x_coff: int = 0,
+              z_coff: int = 0, tile: int = 0) -> torch.Tensor:
+    """Fused YOLO Detect-branch pair: out[..., z_coff : z_coff + C2] =
+    act(conv3x3/1(x[..., x_coff:]) + bias) . w2^T + b2, the 3x3's output t kept on chip
+    (csrc/kernels/conv_direct.hip, C2 forms).  spec: the 3x3 (stride 1, pad 1); w2: bf16
+    [C2, Cout] (the 1x1's packed weight without K padding); tile: direct tile 0-3.
+    CPU: the two reference convs in sequence, t rounded to bf16 in between."""
+    assert spec.kh == 3 and spec.stride == 1 and spec.pad == 1 and spec.mode == MODE_GENERAL
+    C2 = w2.shape[0]
+    assert w2.shape[1] == spec.cout and out.shape[:3] == x.shape[:3]
+    if x.is_cuda:
+        _native().conv_pair(x, w, bias, w2, b2, out, spec.cin, x_coff, z_coff, spec.act, tile)
+        return out
+    t = torch.empty(*x.shape[:3], spec.cout, dtype=torch.bfloat16)
+    _ref.conv2d(x, spec, w, bias, None, t, x_coff, 0, 0)
+    z = t.float() @ w2.float().t() + b2.float()
+    out[..., z_coff:z_coff + C2] = z.to(out.dtype)
+    return out
+
+
 def conv_dual(x1: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
               act: int, stride2: int, out: Optional[torch.Tensor] = None,
               tile: int = -1) -> torch.Tensor:

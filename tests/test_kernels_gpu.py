@@ -616,3 +616,35 @@ def test_conv_splitk(tile, case):
     ws.fill_(float("nan"))
     err, scale = _conv_case(N, H, W, cin, cout, k, s, k // 2, act, res=res, tile=tile)
     assert err <= 0.02 * scale, (tile, case, err, scale)
+
+
+@pytest.mark.parametrize("tile", [0, 1])
+@pytest.mark.parametrize("case", [
+    # (N, H, W, cin, cout, c2, ldx, x_coff, ldz, z_coff) -- YOLOv8n Detect branch pairs
+    (2, 80, 80, 64, 64, 64, 144, 0, 144, 0),     # P3 box branch (s[:, :64]) -> head[:, :64]
+    (2, 80, 80, 80, 80, 80, 144, 64, 144, 64),   # P3 cls branch (s[:, 64:]) -> head[:, 64:]
+    (3, 40, 40, 64, 64, 64, 144, 0, 144, 0),     # P4
+    (3, 20, 20, 80, 80, 80, 144, 64, 144, 64),   # P5
+    (2, 13, 7, 64, 64, 64, 64, 0, 80, 8),        # odd geometry, band tails
+])
+def test_conv_pair(tile, case):
+    """Fused Detect-branch pair (ops.conv_pair: 3x3 + SiLU, then 1x1 + bias from the LDS
+    output tile) vs the two reference convs with the bf16 intermediate; NaN canaries around
+    the head-map slice it writes."""
+    N, H, W, cin, cout, c2, ldx, xo, ldz, zo = case
+    spec = ConvSpec.auto(cin, cout, 3, 1, 1, ops.ACT_SILU)
+    g = torch.Generator().manual_seed(cin + H)
+    x = _rand((N, H, W, ldx), 11)
+    w = ops.pack_conv_weight(torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (9 * cin)) ** 0.5, spec)
+    b = torch.randn(cout, generator=g) * 0.1
+    w2 = (torch.randn(c2, cout, generator=g) * (1.0 / cout) ** 0.5).to(torch.bfloat16)
+    b2 = torch.randn(c2, generator=g) * 0.1
+    ref = torch.zeros(N, H, W, ldz, dtype=torch.bfloat16)
+    ops.conv_pair(x, spec, w, b, w2, b2, ref, x_coff=xo, z_coff=zo)
+    out = torch.full((N, H, W, ldz), float("nan"), dtype=torch.bfloat16, device="cuda")
+    ops.conv_pair(x.cuda(), spec, w.cuda(), b.cuda(), w2.cuda(), b2.cuda(), out, x_coff=xo,
+                  z_coff=zo, tile=tile)
+    torch.cuda.synchronize()
+    got = out.cpu()
+    assert torch.isnan(got[..., :zo].float()).all() and torch.isnan(got[..., zo + c2:].float()).all()
+    _assert_close(got[..., zo:zo + c2], ref[..., zo:zo + c2], ("pair", case, tile))

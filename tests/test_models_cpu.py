@@ -186,3 +186,21 @@ def test_op_roofline_flops_match_model():
     assert rows[0][0].startswith("stem") and rows[-1][0] == "nms"
     assert all(r[1] > 0 for r in rows)
     assert ops.conv2d.__name__ == "conv2d"  # wrappers removed
+
+
+def test_yolo_detect_pairs_fit_and_match_unfused():
+    """Every Detect level's two branches have a fused pair form (ops.conv_pair: 3x3 + SiLU ->
+    1x1 kept on chip on the GPU), and the pair's reference equals the two convs it replaces
+    (bf16 intermediate) at the level's own slices of the head map."""
+    from kvedge_amd.models.yolov8 import KvYoloV8n, init_yolov8n
+
+    kv = KvYoloV8n(init_yolov8n(seed=3, calibrate=False), "cpu")
+    for lv, hw in zip(kv.levels, (16, 8, 4)):
+        assert all(p.fits for p in lv.pairs)
+        cin = lv.stem.spec.cin
+        x = (torch.randn(2, hw, hw, cin, generator=torch.Generator().manual_seed(hw))).to(torch.bfloat16)
+        s = lv.stem(x)
+        z = torch.zeros(2, hw, hw, 144, dtype=torch.bfloat16)
+        for pair, xo, zo in ((lv.pairs[0], 0, 0), (lv.pairs[1], lv.ca, 64)):
+            pair(s, z, x_coff=xo, z_coff=zo)
+        assert torch.equal(z, lv(x))  # the CPU forward runs the unfused convs

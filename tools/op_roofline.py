@@ -82,6 +82,15 @@ def conv_tail_cost(x, w, bias, act, w1, b1, res=None, x2=None, stride2=1, out=No
             2.0 * m * (k * co + co * nt), tile)
 
 
+def conv_pair_cost(x, spec, w, bias, w2, b2, out, x_coff=0, z_coff=0, tile=0):
+    N, H, W, _ = x.shape
+    m = N * H * W
+    c2 = w2.shape[0]
+    return (f"pair 3x3 {spec.cin}>{spec.cout} + 1x1 >{c2} @{H}x{W} (direct {tile})",
+            m * (spec.cin + c2) * 2 + _b(w) + _b(w2),
+            2.0 * m * (9 * spec.cin * spec.cout + spec.cout * c2), None)
+
+
 def stem_from_frames_cost(frames, spec, w, bias, out=None, tile=-1):
     N, H, W, _ = frames.shape
     m = N * (H // 2) * (W // 2)
@@ -131,6 +140,7 @@ def softmax_cost(x, out=None, argmax=None):
 
 
 COSTS = {"conv2d": conv2d_cost, "conv_dual": conv_dual_cost, "conv_tail": conv_tail_cost,
+         "conv_pair": conv_pair_cost,
          "stem_from_frames": stem_from_frames_cost, "stem12_pool_frames": stem12_cost,
          "yolo_stem2": yolo_stem2_cost,
          "sppf_pool": sppf_cost, "upsample2x": upsample_cost, "yolo_decode": decode_cost,
