@@ -56,6 +56,10 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const KvConvParams p
   const int t = xcd_remap(blockIdx.x, nbm * nbn);
   const int m0 = (t / nbn) * BM;
   const int n0 = (t % nbn) * BN;
+  // the tile's bias slice, one value per thread, loaded before the K loop and staged through
+  // LDS for the epilogue (per-lane global bias loads there each waited with a vmcnt(0))
+  static_assert(BN <= 256, "one bias value per thread");
+  const float bias_r = (tid < BN && p.bias && n0 + tid < p.Cout) ? p.bias[n0 + tid] : 0.f;
 
   const bf16* __restrict__ X = reinterpret_cast<const bf16*>(p.x);
   const bf16* __restrict__ Wt = reinterpret_cast<const bf16*>(p.w);
@@ -224,10 +228,16 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const KvConvParams p
   //          store — consecutive lanes cover consecutive bytes of a row, so a wave
   //          writes whole 128-256 B row segments instead of 32-B pieces.
   constexpr int CS = BN + 8;  // C-tile row stride in elements
-  static_assert(BM * CS <= 2 * (BM + BN) * BK, "C tile must fit the operand buffers");
+  static_assert(BM * CS * 2 + BN * 4 <= 2 * (BM + BN) * BK * 2, "C tile + bias slot must fit");
   const bool has_res = p.res != nullptr;
-  bf16* __restrict__ Y = reinterpret_cast<bf16*>(p.y);
-  const bf16* __restrict__ R = reinterpret_cast<const bf16*>(p.res);
+  float* const lbias = reinterpret_cast<float*>(smem + 2 * (BM + BN) * BK) - BN;  // past the C tile
+  if (tid < BN) lbias[tid] = bias_r;
+  __syncthreads();
+  typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, p.M * p.ldy * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rres = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.res), (short)0, has_res ? p.M * p.ldr * 2 : 0, 0x00020000);
+  constexpr int kOOB1 = 0x7ffffff0;
   constexpr int CPR = BN / 8;               // 16-B chunks per tile row
   constexpr int PER = BM * CPR / 256;       // chunks per thread
   dispatch_act(p.act, has_res, [&](auto A1, auto A2) __attribute__((always_inline)) {
@@ -235,8 +245,7 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const KvConvParams p
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
       const int nl = wn * WTN + tn * 16 + (lane >> 4) * 4;
-      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (p.bias && n0 + nl < p.Cout) bv = *reinterpret_cast<const float4*>(p.bias + n0 + nl);
+      const float4 bv = *reinterpret_cast<const float4*>(lbias + nl);
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
         const int ml = wm * WTM + tm * 16 + (lane & 15);
@@ -248,20 +257,32 @@ __global__ __launch_bounds__(256, 2) void conv_igemm_kernel(const KvConvParams p
         *reinterpret_cast<bf16x4*>(smem + ml * CS + nl) = o;
       }
     }
+    // the residual chunks are all loaded before the first store; range-checked buffer
+    // loads / stores (out-of-tile: offset past the end), so the loop has no branches
+    u32x4v rv[PER];
+    if (has_res) {
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int idx = tid + 256 * j;
+        const int m = m0 + idx / CPR, n = n0 + (idx % CPR) * 8;
+        const int off = (m < p.M && n < p.Cout) ? (m * p.ldr + p.r_coff + n) * 2 : kOOB1;
+        rv[j] = __builtin_amdgcn_raw_buffer_load_b128(rres, off, 0, 0);
+      }
+    }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       const int idx = tid + 256 * j;
       const int ml = idx / CPR, ch = idx % CPR;
       const int m = m0 + ml, n = n0 + ch * 8;
-      if (m >= p.M || n >= p.Cout) continue;
       bf16x8 v = *reinterpret_cast<const bf16x8*>(smem + ml * CS + ch * 8);
       if (has_res) {
-        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(R + (size_t)m * p.ldr + p.r_coff + n);
+        const bf16x8 r8 = __builtin_bit_cast(bf16x8, rv[j]);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = f2bf(act_c<act2>((float)v[e] + (float)rv[e]));
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(act_c<act2>((float)v[e] + (float)r8[e]));
       }
-      *reinterpret_cast<bf16x8*>(Y + (size_t)m * p.ldy + p.y_coff + n) = v;
+      const int off = (m < p.M && n < p.Cout) ? (m * p.ldy + p.y_coff + n) * 2 : kOOB1;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), ry, off, 0, 0);
     }
   });
 }
