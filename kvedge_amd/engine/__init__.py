@@ -208,14 +208,16 @@ class InferenceEngine:
 
 
 def edge_streams(batch: int) -> int:
-    """Batch slices (HIP streams) for a serving batch: two for even batches of 32 and up --
-    at batch 64 one slice leaves most stage-3/4 launches with fewer workgroups than CUs, and
-    the second slice's kernels fill them -- else one.  KVEDGE_EDGE_STREAMS=n overrides."""
+    """Batch slices (HIP streams) for a serving batch: one.  Two half-batch slices on two
+    streams were measured SLOWER at the serving sizes on the same box (b32 0.95 vs 0.87 ms,
+    b64 1.41 vs 1.30 ms p50, profiles/r3_v11_edge_streams_ab.txt): at these sizes the
+    half-batch kernels lose more to their own launch floors than the overlap recovers.
+    KVEDGE_EDGE_STREAMS=n overrides (n must divide the batch)."""
     env = os.environ.get("KVEDGE_EDGE_STREAMS", "")
     if env:
         n = int(env)
         return n if n >= 1 and batch % n == 0 else 1
-    return 2 if batch >= 32 and batch % 2 == 0 else 1
+    return 1
 
 
 def edge_latency(model: Callable, image_size: int, batches, device="cuda", seed: int = 0,
