@@ -29,6 +29,11 @@ const GldsTile kXpTiles[] = {
     {256, 256, &glds_get<256, 256, 2, 4, 5, 32, 16, true, true>, 512},
     {256, 128, &glds_get<256, 128, 2, 2, 3, 32, 16, false, true>},
     {128, 128, &glds_get<128, 128, 2, 2, 2, 64, 16, false, true>},
+    // N = 144 (YOLO Detect branch stems, box 64 + cls 80): a 160-wide N tile (ten 16x16
+    // blocks per wave, 4 x 1 waves of 32 px) computes 10 % padding channels where 128- and
+    // 256-wide tiles computed 44 %; B rows past Cout are zero-filled by the range check
+    {128, 160, &glds_get<128, 160, 4, 1, 2, 64, 16, false, true>},
+    {128, 160, &glds_get<128, 160, 4, 1, 3, 64, 16, false, true>},
 };
 
 }  // namespace

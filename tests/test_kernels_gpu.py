@@ -103,12 +103,12 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale
 
 
-N_TILES = 103  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue (68-83) + v8 split-K (84-102)
+N_TILES = 105  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue / N-160 (68-85) + v8 split-K (86-104)
 # + v6 A-resident N-loop 1x1 GEMM (58-67, conv_nloop.hip kNlTiles: one Kpad per tile;
 # 63-65 are the fused-downsample (dual) forms, 66-67 step 128 K at a time)
 NLOOP0 = 58
 XP0 = 68  # v7: the v2 kernel's cross-stage pipelined loop (BK 32 rings, 8 waves)
-SK0 = 84  # v8: split-K (conv_sk.hip kSkTiles): K slices per tile (clamped to the K steps)
+SK0 = 86  # v8: split-K (conv_sk.hip kSkTiles): K slices per tile (clamped to the K steps)
 NLOOP_KPAD = [128, 256, 256, 256, 256, 384, 384, 768, 256, 256]
 NLOOP_DUAL = {63, 64, 65}
 STREAM0 = 32  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
