@@ -474,9 +474,14 @@ extern "C" int kv_synth_frames_dev(uint8_t* y, int N, int H, int W, uint64_t see
                                    uint64_t* step, int bump_done, hipStream_t s) {
   const long long bytes = (long long)N * H * W * 3;
   if (bytes % 8) return -1;
-  hipLaunchKernelGGL(synth_dev_kernel, dim3(grid_for(bytes / 8)), dim3(kBlock), 0, s, y,
-                     bytes / 8, seed, step, bump_done);
-  if (!bump_done) hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(1), 0, s, step);
+  // the in-kernel ticket costs one same-address atomic per block: at 2048 blocks (batch
+  // 640+) those serialise to ~13 us, more than the separate one-thread launch; at edge
+  // batches (tens of blocks) it is free and saves the launch
+  const unsigned g = grid_for(bytes / 8);
+  const int in_kernel = bump_done && g <= 256;
+  hipLaunchKernelGGL(synth_dev_kernel, dim3(g), dim3(kBlock), 0, s, y, bytes / 8, seed, step,
+                     in_kernel);
+  if (!in_kernel) hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(1), 0, s, step);
   KV_CHECK_LAUNCH();
 }
 

@@ -302,6 +302,16 @@ def test_synth_preprocess_bn():
         ops.synth_frames(big_ref, 7, 3 + k)
         torch.cuda.synchronize()
         assert torch.equal(big.cpu(), big_ref) and ctr2.tolist() == [4 + k, 0], (k, ctr2.tolist())
+    # a grid too large for the in-kernel ticket (2048 blocks): the separate bump launch
+    huge = torch.empty(48, 224, 224, 3, dtype=torch.uint8, device="cuda")
+    ctr3 = torch.tensor([9, 0], dtype=torch.int64, device="cuda")
+    ops.synth_frames(huge, 7, ctr3)
+    ops.synth_frames(huge, 7, ctr3)
+    torch.cuda.synchronize()
+    assert ctr3.tolist() == [11, 0]
+    ref2 = torch.empty(2, 224, 224, 3, dtype=torch.uint8)
+    ops.synth_frames(ref2, 7, 10)
+    assert torch.equal(huge[:2].cpu(), ref2)
     p_ref = ops.preprocess(fr)
     p = ops.preprocess(fr.cuda()).cpu()
     assert (p.float() - p_ref.float()).abs().max() <= 0.02
