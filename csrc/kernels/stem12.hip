@@ -286,8 +286,14 @@ __global__ __launch_bounds__(kNT, 2) void stem12_pool_kernel(
     {
       const int r0 = max(2 * P - 1, 0) % kSR, r1 = (2 * P) % kSR, r2 = min(2 * P + 1, Hs - 1) % kSR;
       bf16* yrow = y + (long long)(n * Hp + P) * Wp * ldy + y_coff;
-      for (int q = tid; q < Wp * 8; q += kNT) {
-        const int px = q >> 3, c8 = q & 7;
+      // lane -> (pixel, 16-B chunk): the two 8-lane halves of each 16-lane ds_read_b128 group
+      // take pooled pixels p and p + 4, whose window columns are 8 stem pixels apart (1152 B =
+      // 32 banks mod 64): the halves hit disjoint banks.  With neighbouring pixels (2 stem
+      // pixels = 288 B apart) every pool read was 2-way bank-conflicted.
+      for (int q = tid; q < (Wp + 7) / 8 * 64; q += kNT) {
+        const int g16 = q >> 4, c8 = q & 7;
+        const int px = 8 * (g16 >> 2) + (g16 & 3) + 4 * ((q >> 3) & 1);
+        if (px >= Wp) continue;
         const int xs[3] = {max(2 * px - 1, 0), 2 * px, min(2 * px + 1, Ws - 1)};
         const int rs[3] = {r0, r1, r2};
         uint4 v[9];

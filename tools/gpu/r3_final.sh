@@ -1,0 +1,18 @@
+# Round 3 final tree: all GPU tests + smoke, stem12 pool remap A/B (_C_ab.so = previous
+# stem12.hip), benches (ResNet-50 with the edge block, YOLOv8n)
+set -o pipefail
+mkdir -p gpurun_out; export TMPDIR=/tmp
+T=${TAG:-r3n}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/${T}_t.txt 2>&1 || { tail -30 gpurun_out/${T}_t.txt; exit 1; }
+tail -1 gpurun_out/${T}_t.txt
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.txt 2>&1 || exit $?
+tail -1 gpurun_out/${T}_smoke.txt
+for i in 1 2; do
+  timeout -k 10 200 python -u tools/stem_ab.py >> gpurun_out/${T}_stem.txt 2>&1 || exit $?
+  KVEDGE_LIB=_C_ab.so timeout -k 10 200 python -u tools/stem_ab.py >> gpurun_out/${T}_stem.txt 2>&1 || exit $?
+done
+grep '^{' gpurun_out/${T}_stem.txt
+timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/${T}_bench.txt 2>&1 || exit $?
+KVEDGE_LIB=_C_ab.so timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 --edge "" > gpurun_out/${T}_bench_ab.txt 2>&1 || exit $?
+timeout -k 10 400 python -u bench.py --model yolov8n --steps 20 --warmup 5 --edge "" > gpurun_out/${T}_yolo.txt 2>&1 || exit $?
+for f in bench bench_ab yolo; do echo "$f $(grep -o '"value": [0-9.]*' gpurun_out/${T}_$f.txt) $(grep -o '"edge": \[[^]]*\]' gpurun_out/${T}_$f.txt)"; done
