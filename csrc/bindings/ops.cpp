@@ -383,6 +383,27 @@ void global_avgpool(const at::Tensor& x, at::Tensor& y, int64_t N, int64_t HW, i
   TORCH_CHECK(rc == 0, "kvedge: avgpool failed rc=", rc);
 }
 
+// Edge-batch classifier head: y [N, ncls] bf16 = fc(global_avgpool(x)), x [N, H, W, C]
+void pooled_fc(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+               at::Tensor& y) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 2 && y.dim() == 2, "kvedge: pooled_fc shapes");
+  const int64_t N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3), ncls = w.size(0);
+  TORCH_CHECK(w.size(1) >= C && y.size(0) == N && y.size(1) == ncls, "kvedge: pooled_fc w / y");
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_dev(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= ncls, "kvedge: pooled_fc bias");
+    bp = bias->data_ptr<float>();
+  }
+  const c10::DeviceGuard g(x.device());
+  const int rc = kv_pooled_fc(x.data_ptr(), (int)N, (int)HW, (int)C, w.data_ptr(), (int)w.size(1),
+                              bp, y.data_ptr(), (int)ncls, cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: pooled_fc failed rc=", rc);
+}
+
 void softmax_rows(const at::Tensor& x, at::Tensor& y, at::Tensor& argmax) {
   check_bf16(x, "x");
   check_dev(y, "y");
@@ -632,6 +653,7 @@ TORCH_LIBRARY(kvedge, m) {
   m.def("sppf_pool(Tensor(a!) buf, int N, int H, int W, int C) -> ()");
   m.def("global_avgpool(Tensor x, Tensor(a!) y, int N, int HW, int C) -> ()");
   m.def("softmax_rows(Tensor x, Tensor(a!) y, Tensor(b!) argmax) -> ()");
+  m.def("pooled_fc(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y) -> ()");
   m.def("upsample2x(Tensor x, Tensor(a!) y, int N, int H, int W, int C, int ldx, int x_coff, int ldy, "
         "int y_coff) -> ()");
   m.def("yolo_decode(Tensor f0, Tensor f1, Tensor f2, int h0, int w0, int h1, int w1, int h2, "
@@ -663,6 +685,7 @@ TORCH_LIBRARY_IMPL(kvedge, CUDA, m) {
   m.impl("sppf_pool", sppf_pool);
   m.impl("global_avgpool", global_avgpool);
   m.impl("softmax_rows", softmax_rows);
+  m.impl("pooled_fc", pooled_fc);
   m.impl("upsample2x", upsample2x);
   m.impl("yolo_decode", yolo_decode);
   m.impl("nms", nms);

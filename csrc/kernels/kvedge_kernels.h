@@ -126,6 +126,10 @@ int kv_maxpool2d(const void* x, void* y, int N, int H, int W, int C, int ldx, in
 int kv_sppf_pool(void* buf, int N, int H, int W, int C, hipStream_t s);
 // K6: global average pool NHWC -> [N, C] bf16.
 int kv_global_avgpool(const void* x, void* y, int N, int HW, int C, hipStream_t s);
+// K6+K1 at edge batches: y[n, :ncls] = bf16(fc(bf16(mean over HW of x[n]))), x [N, HW, C] bf16,
+// w [ncls][ldw] bf16 (packed 1x1 conv weight), bias fp32 [ncls] or NULL.
+int kv_pooled_fc(const void* x, int N, int HW, int C, const void* w, int ldw, const float* bias,
+                 void* y, int ncls, hipStream_t s);
 // K7: row softmax, bf16 [rows, cols] -> fp32 probabilities; also writes argmax.
 int kv_softmax_rows(const void* x, float* y, int64_t* argmax, int rows, int cols, hipStream_t s);
 // K8: nearest 2x upsample of x [N,H,W,C] written into channel slice of y [N,2H,2W,ldy].

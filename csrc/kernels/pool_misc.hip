@@ -173,6 +173,47 @@ __global__ __launch_bounds__(kBlock) void avgpool_kernel(const bf16* __restrict_
   }
 }
 
+// ---- K6+K1 fused head for edge batches: logits = fc(global_avgpool(x)) -----------------
+// At batch 1-16 the classifier is a GEMV (K = 2048, N = 1000): as a tiled GEMM it was a
+// 16-32-workgroup launch walking 32 K steps (~13 us), after a separate pooling launch.  Here
+// workgroup (column block, image) pools the image's C channels into LDS (rounded to bf16, as
+// the pooling kernel stores them), then each wave dots 8 weight rows with it: 16-B weight
+// loads, a wave reduction per column.  One launch, weights read once per image.
+__global__ __launch_bounds__(256) void pooled_fc_kernel(const bf16* __restrict__ x, int HW, int C,
+                                                        const bf16* __restrict__ w, int ldw,
+                                                        const float* __restrict__ bias,
+                                                        bf16* __restrict__ y, int ncls) {
+  extern __shared__ float pooled[];  // C values
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const bf16* xb = x + (size_t)b * HW * C;
+  const float inv = 1.0f / (float)HW;
+  for (int c8 = tid; c8 < C / 8; c8 += 256) {
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 7
+    for (int q = 0; q < HW; ++q) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(xb + (size_t)q * C + c8 * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += (float)v[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) pooled[c8 * 8 + e] = (float)f2bf(s[e] * inv);
+  }
+  __syncthreads();
+  for (int j = 0; j < 8; ++j) {
+    const int n = blockIdx.x * 32 + wv * 8 + j;  // wave-uniform
+    if (n >= ncls) break;
+    const bf16* wr = w + (size_t)n * ldw;
+    float acc = 0.f;
+    for (int k = lane * 8; k < C; k += 512) {
+      const bf16x8 wk = *reinterpret_cast<const bf16x8*>(wr + k);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc += (float)wk[e] * pooled[k + e];
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) y[(size_t)b * ncls + n] = f2bf(acc + (bias ? bias[n] : 0.f));
+  }
+}
+
 // ---- K7 row softmax + argmax: one wave64 per row ---------------------------
 __global__ __launch_bounds__(kBlock) void softmax_kernel(const bf16* __restrict__ x,
                                                          float* __restrict__ y,
@@ -437,6 +478,15 @@ extern "C" int kv_global_avgpool(const void* x, void* y, int N, int HW, int C, h
   const long long work = (long long)N * (C / 8) * 8;
   hipLaunchKernelGGL(avgpool_kernel, dim3(grid_for(work)), dim3(kBlock), 0, s, (const bf16*)x,
                      (bf16*)y, N, HW, C);
+  KV_CHECK_LAUNCH();
+}
+
+extern "C" int kv_pooled_fc(const void* x, int N, int HW, int C, const void* w, int ldw,
+                            const float* bias, void* y, int ncls, hipStream_t s) {
+  if (N <= 0 || C % 8 || ldw < C || ldw % 8 || C > 16384) return -1;
+  hipLaunchKernelGGL(pooled_fc_kernel, dim3((unsigned)((ncls + 31) / 32), (unsigned)N), dim3(256),
+                     (unsigned)(C * sizeof(float)), s, (const bf16*)x, HW, C, (const bf16*)w, ldw,
+                     bias, (bf16*)y, ncls);
   KV_CHECK_LAUNCH();
 }
 

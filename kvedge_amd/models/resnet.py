@@ -14,6 +14,8 @@ Deployed forward (all HIP kernels on GPU):
 """
 from __future__ import annotations
 
+import os
+
 from typing import List, Optional
 
 import torch
@@ -313,8 +315,13 @@ class KvResNet50:
     def logits(self, x: torch.Tensor, frames_in: bool = False) -> torch.Tensor:
         f = self.features(x, frames_in)
         B = f.shape[0]
+        if f.is_cuda and B <= ops.POOLED_FC_MAX_BATCH and self.fuse_head:
+            return ops.pooled_fc(f, self.fc.w, self.fc.b)  # one GEMV launch at edge batches
         pooled = ops.global_avgpool(f).view(B, 1, 1, 2048)
         return self.fc(pooled).view(B, self.num_classes)
+
+    # edge batches: avgpool + fc as one GEMV kernel (ops.pooled_fc); KVEDGE_FUSE_HEAD=0 = A/B off
+    fuse_head: bool = os.environ.get("KVEDGE_FUSE_HEAD", "1") != "0"
 
     def raw_outputs(self, frames_u8: torch.Tensor) -> torch.Tensor:
         """uint8 frames -> pre-softmax logits [B, C] (same kernel path as __call__); the

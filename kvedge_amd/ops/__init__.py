@@ -549,6 +549,28 @@ def global_avgpool(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch
     return out
 
 
+POOLED_FC_MAX_BATCH = 16  # edge batches: the head runs as one GEMV launch up to here
+
+
+def pooled_fc(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Classifier head at edge batches in ONE launch: out [N, ncls] bf16 =
+    fc(global_avgpool(x)) with the pooled vector rounded to bf16 as global_avgpool stores it.
+    x: [N, H, W, C] bf16; w: the fc's packed [ncls, Kpad] bf16 weight (Kpad >= C).
+    CPU: global_avgpool then the 1x1 conv reference."""
+    N, H, W, C = x.shape
+    ncls = w.shape[0]
+    if out is None:
+        out = empty(N, ncls, dtype=torch.bfloat16, device=x.device)
+    if x.is_cuda:
+        _native().pooled_fc(x, w, bias, out)
+        return out
+    pooled = global_avgpool(x).view(N, 1, 1, C)
+    spec = ConvSpec(C, ncls, 1, 1, 1, 0, ACT_NONE, MODE_GEMM)
+    _ref.conv2d(pooled, spec, w, bias, None, out.view(N, 1, 1, ncls))
+    return out
+
+
 def softmax_rows(x: torch.Tensor, out: Optional[torch.Tensor] = None,
                  argmax: Optional[torch.Tensor] = None):
     if out is None:

@@ -658,3 +658,19 @@ def test_conv_pair(tile, case):
     got = out.cpu()
     assert torch.isnan(got[..., :zo].float()).all() and torch.isnan(got[..., zo + c2:].float()).all()
     _assert_close(got[..., zo:zo + c2], ref[..., zo:zo + c2], ("pair", case, tile))
+
+
+@pytest.mark.parametrize("N,H,W,C,ncls,ldw", [(1, 7, 7, 2048, 1000, 2048), (5, 7, 7, 2048, 1000, 2048),
+                                              (3, 3, 5, 64, 40, 128), (16, 7, 7, 2048, 1000, 2048)])
+def test_pooled_fc(N, H, W, C, ncls, ldw):
+    """Edge-batch classifier head (avgpool + fc in one GEMV launch) vs the two reference ops
+    (bf16 pooled vector in between); Kpad > C exercises the weight row pitch."""
+    x = _rand((N, H, W, C), 21)
+    g = torch.Generator().manual_seed(C + ncls)
+    w = (torch.randn(ncls, ldw, generator=g) * (1.0 / C) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(ncls, generator=g) * 0.1
+    ref = ops.pooled_fc(x, w, b)
+    got = ops.pooled_fc(x.cuda(), w.cuda(), b.cuda())
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape == (N, ncls)
+    _assert_close(got.cpu(), ref, ("pooled_fc", N, C, ncls))
