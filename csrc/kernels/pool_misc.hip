@@ -206,8 +206,10 @@ __global__ __launch_bounds__(256) void pooled_fc_kernel(const bf16* __restrict__
     float acc = 0.f;
     for (int k = lane * 8; k < C; k += 512) {
       const bf16x8 wk = *reinterpret_cast<const bf16x8*>(wr + k);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc += (float)wk[e] * pooled[k + e];
+      const float4 p0 = *reinterpret_cast<const float4*>(pooled + k);  // ds_read_b128
+      const float4 p1 = *reinterpret_cast<const float4*>(pooled + k + 4);
+      acc += (float)wk[0] * p0.x + (float)wk[1] * p0.y + (float)wk[2] * p0.z + (float)wk[3] * p0.w;
+      acc += (float)wk[4] * p1.x + (float)wk[5] * p1.y + (float)wk[6] * p1.z + (float)wk[7] * p1.w;
     }
     acc = wave_sum(acc);
     if (lane == 0) y[(size_t)b * ncls + n] = f2bf(acc + (bias ? bias[n] : 0.f));
