@@ -320,8 +320,9 @@ class KvResNet50:
         pooled = ops.global_avgpool(f).view(B, 1, 1, 2048)
         return self.fc(pooled).view(B, self.num_classes)
 
-    # edge batches: avgpool + fc as one GEMV kernel (ops.pooled_fc); KVEDGE_FUSE_HEAD=0 = A/B off
-    fuse_head: bool = os.environ.get("KVEDGE_FUSE_HEAD", "1") != "0"
+    # edge batches: avgpool + fc as one GEMV kernel (ops.pooled_fc), opt-in with
+    # KVEDGE_FUSE_HEAD=1 until it has a same-box edge A/B (the GPU pool gave no box for one)
+    fuse_head: bool = os.environ.get("KVEDGE_FUSE_HEAD", "0") == "1"
 
     def raw_outputs(self, frames_u8: torch.Tensor) -> torch.Tensor:
         """uint8 frames -> pre-softmax logits [B, C] (same kernel path as __call__); the

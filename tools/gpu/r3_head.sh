@@ -7,7 +7,7 @@ tail -1 gpurun_out/${T}_t.txt
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.txt 2>&1 || exit $?
 tail -1 gpurun_out/${T}_smoke.txt
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/${T}_bench.txt 2>&1 || exit $?
-KVEDGE_FUSE_HEAD=0 timeout -k 10 400 python -u bench.py --steps 5 --warmup 2 --batch 64 --edge 1,8 > gpurun_out/${T}_edge_nohead.txt 2>&1 || exit $?
-timeout -k 10 400 python -u bench.py --steps 5 --warmup 2 --batch 64 --edge 1,8 > gpurun_out/${T}_edge_head.txt 2>&1 || exit $?
+timeout -k 10 400 python -u bench.py --steps 5 --warmup 2 --batch 64 --edge 1,8 > gpurun_out/${T}_edge_nohead.txt 2>&1 || exit $?
+KVEDGE_FUSE_HEAD=1 timeout -k 10 400 python -u bench.py --steps 5 --warmup 2 --batch 64 --edge 1,8 > gpurun_out/${T}_edge_head.txt 2>&1 || exit $?
 timeout -k 10 400 python -u bench.py --model yolov8n --steps 20 --warmup 5 --edge "" > gpurun_out/${T}_yolo.txt 2>&1 || exit $?
 for f in bench edge_head edge_nohead yolo; do echo "$f $(grep -o '"value": [0-9.]*' gpurun_out/${T}_$f.txt) $(grep -o '"edge": \[[^]]*\]' gpurun_out/${T}_$f.txt)"; done
