@@ -32,6 +32,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "images/sec ResNet-50 edge module at 1/2/4/8 MI355X; VM boot-to-ready sec"
+# per-model metric strings: only the ResNet-50 run is BASELINE.json's headline
+METRICS = {"resnet50": METRIC,
+           "yolov8n": "images/sec YOLOv8n detection edge module (incl. decode + NMS) on MI355X"}
 
 
 def main(argv=None):
@@ -75,16 +78,16 @@ def main(argv=None):
     raw = list(sys.argv[1:] if argv is None else argv)
     a = ap.parse_args(raw)
 
-    import torch
-    from kvedge_amd import ops, parallel
-    from kvedge_amd.engine import BENCH_BATCH, BENCH_STREAMS, InferenceEngine
+    from kvedge_amd import parallel
 
     if a.gpus < 1:
         print("--gpus must be >= 1", file=sys.stderr)
         return 2
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # launcher path: no torch.cuda.* call may run here (HIP would initialise in the
+        # parent of the GPU ranks); devices are counted from the KFD topology in sysfs
         if not a.cpu:
-            ndev = torch.cuda.device_count()  # counts only; HIP stays uninitialised here
+            ndev = parallel.visible_gpu_count()
             if a.gpus > ndev:
                 print(f"--gpus {a.gpus} but only {ndev} GPU(s) visible", file=sys.stderr)
                 return 2
@@ -93,6 +96,10 @@ def main(argv=None):
     if int(os.environ.get("WORLD_SIZE", "1")) != a.gpus:
         print(f"# note: --gpus {a.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')}; "
               "reporting the launched world size", file=sys.stderr)
+
+    import torch
+    from kvedge_amd import ops
+    from kvedge_amd.engine import BENCH_BATCH, BENCH_STREAMS, InferenceEngine
 
     if a.hang_rank >= 0 and a.hang_rank == int(os.environ.get("RANK", "0")):
         while True:  # test hook (tests/test_bench_cpu.py): a rank that never arrives
@@ -192,7 +199,7 @@ def main(argv=None):
     ms_per_step = max_elapsed / a.steps * 1e3
     flops = model.flops_per_image(hw) if hasattr(model, "flops_per_image") else None
     res = {
-        "metric": METRIC,
+        "metric": METRICS[a.model],
         "value": round(value, 2),
         "unit": "images/sec",
         "n_gpus": world,

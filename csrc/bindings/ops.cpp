@@ -80,7 +80,7 @@ void conv(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tens
   TORCH_CHECK(N > 0 && H * W * ldx * 2 < (1ll << 31) && Ho * Wo * ldy * 2 < (1ll << 31),
               "kvedge: one image's activations exceed 2 GiB");
   TORCH_CHECK(x.numel() >= N * H * W * ldx, "kvedge: x smaller than N*H*W*ldx");
-  TORCH_CHECK(x_coff + Cin <= ldx, "kvedge: x channel slice out of range");
+  TORCH_CHECK(x_coff >= 0 && x_coff + Cin <= ldx, "kvedge: x channel slice out of range");
   TORCH_CHECK(y.numel() >= (int64_t)p.M * ldy && y_coff + Cout <= ldy, "kvedge: y too small");
   if (p.res) TORCH_CHECK(res->numel() >= (int64_t)p.M * ldr && r_coff + Cout <= ldr, "kvedge: residual too small");
   const int rc = kv_conv2d(&p, (int)tile, cur_stream(x));
@@ -106,6 +106,10 @@ void conv_pair(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias,
   TORCH_CHECK(z.size(0) == N && z.size(1) == H && z.size(2) == W && z_coff + C2 <= z.size(3),
               "kvedge: conv_pair z [N, H, W, >= z_coff + C2]");
   TORCH_CHECK(x_coff + Cin <= ldx && w.size(1) == (9 * Cin + 63) / 64 * 64, "kvedge: conv_pair x / w");
+  // the C2 store path writes 8-B bf16x4 chunks at z + pixel * ldz + z_coff + 4j
+  TORCH_CHECK(x_coff >= 0 && z_coff >= 0, "kvedge: conv_pair channel offsets must be >= 0");
+  TORCH_CHECK(z_coff % 4 == 0 && z.size(3) % 4 == 0,
+              "kvedge: conv_pair z_coff and the z row pitch must be multiples of 4 channels");
   TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() >= Cout && b2.scalar_type() == at::kFloat &&
               b2.numel() >= C2, "kvedge: conv_pair biases fp32");
   TORCH_CHECK(N * H * W * ldx * 2 < (1ll << 31) && N * H * W * z.size(3) * 2 < (1ll << 31),

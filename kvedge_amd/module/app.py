@@ -96,6 +96,11 @@ class _CameraSource:
         self._stop = threading.Event()
         self.thread = threading.Thread(target=self._run, name="kvedge-camera", daemon=True)
         self.thread.start()
+        # a daemon thread parked inside the GIL-releasing native ring.put() while the
+        # interpreter tears down ends in std::terminate: always stop it before exit
+        import atexit
+
+        atexit.register(self.stop)
 
     def _run(self):
         period = self.batch / self.fps if self.fps > 0 else 0.0
@@ -110,9 +115,14 @@ class _CameraSource:
                 time.sleep(max(0.0, nxt - time.perf_counter()))
 
     def stop(self):
+        if self._stop.is_set() and not self.thread.is_alive():
+            return
         self._stop.set()
         self.ring.close()
         self.thread.join(timeout=5)
+        import atexit
+
+        atexit.unregister(self.stop)
 
 
 class ModuleApp:
@@ -137,6 +147,11 @@ class ModuleApp:
         self._win_imgs = 0
         self._win_t0 = 0.0
         self._lat_ms = []
+        # the last non-empty telemetry window: a report() that lands right after an
+        # automatic one (empty window) re-publishes it with its own window_s instead of
+        # claiming 0 img/s
+        self._last_window: Optional[Dict[str, Any]] = None
+        self._closed = False
         # native log-linear histogram (csrc/runtime): replicas merge it with one SUM
         # all-reduce, so the reported p99 is the fleet's true p99, not a max of p99s.
         # (device != cuda and no built library: plain list, CPU tests only)
@@ -236,9 +251,22 @@ class ModuleApp:
         self._stop_req = True
 
     def stop(self):
+        """Stop the camera thread, persist counters, disconnect.  Idempotent."""
+        if self._closed:
+            return
+        self._closed = True
         self._stop_camera()
         self._save_state()
         self.tr.disconnect()
+
+    close = stop
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.stop()
+        return False
 
     def _stop_camera(self):
         if self.camera is not None:
@@ -507,17 +535,25 @@ class ModuleApp:
                 return n
 
     def _summary(self) -> Dict[str, Any]:
+        """This rank's window since the last report.  An empty window (no step finished
+        since the last report) carries the last non-empty one, flagged ``carried``."""
         now = self.clock()
         win = max(now - self._win_t0, 1e-9)
+        if self._win_imgs == 0 and self._last_window is not None:
+            return dict(self._last_window, carried=True)
         ips = self._win_imgs / win
         if self._hist is not None:
             p50, p99 = self._hist.quantiles_us([0.5, 0.99])
-            return {"images_per_s": ips, "p50_ms": p50 / 1e3, "p99_ms": p99 / 1e3,
-                    "window_s": win, "steps": self._hist.count}
-        lat = sorted(self._lat_ms)
-        q = lambda p: lat[min(len(lat) - 1, int(round(p / 100 * (len(lat) - 1))))] if lat else 0.0  # noqa
-        return {"images_per_s": ips, "p50_ms": q(50), "p99_ms": q(99), "window_s": win,
-                "steps": len(lat)}
+            s = {"images_per_s": ips, "p50_ms": p50 / 1e3, "p99_ms": p99 / 1e3,
+                 "window_s": win, "steps": self._hist.count}
+        else:
+            lat = sorted(self._lat_ms)
+            q = lambda p: lat[min(len(lat) - 1, int(round(p / 100 * (len(lat) - 1))))] if lat else 0.0  # noqa
+            s = {"images_per_s": ips, "p50_ms": q(50), "p99_ms": q(99), "window_s": win,
+                 "steps": len(lat)}
+        if self._win_imgs > 0:
+            self._last_window = dict(s)
+        return dict(s, carried=False)
 
     def report(self) -> Dict[str, Any]:
         """Telemetry.  Collective at world > 1: call it only from a control boundary or
@@ -528,7 +564,8 @@ class ModuleApp:
             ips_total = parallel.allreduce_scalars([s["images_per_s"]], op="sum")[0]
             if self._hist is not None:  # fleet p99 from the merged histogram
                 self._hist.allreduce()
-                lat_max = self._hist.quantiles_us([0.99])[0] / 1e3
+                if self._hist.count > 0:  # empty fleet window: keep the carried p99
+                    lat_max = self._hist.quantiles_us([0.99])[0] / 1e3
             else:
                 lat_max = parallel.allreduce_scalars([s["p99_ms"]], op="max")[0]
         msg = {"ts": now_iso(), "model": self.cfg.model, "batch": self.cfg.batch,
@@ -537,6 +574,7 @@ class ModuleApp:
                "latency_ms": {"p50": round(s["p50_ms"], 3), "p99": round(lat_max, 3)},
                "total_images": self.state["total_images"], "rank": self.rank,
                "world_size": self.world, "heartbeat": self.state["total_steps"],
+               "window_s": round(s["window_s"], 6), "window_carried": s["carried"],
                "source": self.cfg.source}
         if self.ring is not None:
             msg["frames_dropped"] = self.ring.dropped

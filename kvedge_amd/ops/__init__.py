@@ -211,15 +211,20 @@ SPLITK0 = 1 << 30            # first split-K tile index, set by load()
 
 
 def splitk_workspace(device: torch.device, elems: int) -> Optional[torch.Tensor]:
-    """The stream's split-K workspace for a layer of ``elems`` = M x Cout outputs: room for
-    up to SPLITK_MAX_SPLIT slabs, capped at SPLITK_MAX_ELEMS (None if not even one fits)."""
+    """The stream's split-K workspace for a layer of ``elems`` = M x Cout outputs (None if
+    not even two slabs fit under SPLITK_MAX_ELEMS).
+
+    Allocated ONCE per (device, stream) at the full SPLITK_MAX_ELEMS (128 MB of fp32 --
+    noise in 288 GB of HBM) and never replaced: a captured hipGraph holds the raw pointer,
+    not the tensor, and torch hands out pooled stream handles round-robin, so a later
+    engine or the autotuner can reach the same key.  Growing the buffer would free memory
+    a live graph still writes its slabs into."""
     if elems > SPLITK_MAX_ELEMS // 2:
         return None
-    want = min(elems * SPLITK_MAX_SPLIT, SPLITK_MAX_ELEMS)
     key = (device.index, torch.cuda.current_stream(device).cuda_stream)
     ws = _WS.get(key)
-    if ws is None or ws.numel() < want:
-        ws = torch.empty(max(want, 1 << 16), dtype=torch.float32, device=device)
+    if ws is None:
+        ws = torch.empty(SPLITK_MAX_ELEMS, dtype=torch.float32, device=device)
         _WS[key] = ws
     return ws
 

@@ -42,17 +42,74 @@ def info() -> DistInfo:
     return _INFO
 
 
-def _child_preexec():  # pragma: no cover - runs in the forked child
-    """Child side of launch_local: die with the launcher.  PR_SET_PDEATHSIG makes the
-    kernel SIGTERM the rank if the launcher is SIGKILLed (no handler of ours runs then),
-    so no rank can outlive it holding a GPU."""
-    import ctypes
-    import signal
+# Child bootstrap of launch_local, run as ``python -c _RANK_BOOT <argv...>``.  It arms
+# PR_SET_PDEATHSIG in the (single-threaded, GPU-clean) child itself, so the launcher
+# needs no ``preexec_fn``: that hook runs Python in the forked child while the parent's
+# stderr pump threads may hold the allocator or loader locks, and it
+# forces a fork+exec instead of posix_spawn.  If the launcher died before the signal
+# was armed, the child's parent is no longer the launcher: exit at once.
+_RANK_BOOT = r"""
+import ctypes, os, runpy, signal, sys
+try:
+    ctypes.CDLL(None, use_errno=True).prctl(1, int(signal.SIGTERM))  # PR_SET_PDEATHSIG
+except (OSError, AttributeError):
+    pass
+if os.getppid() != int(os.environ.get("KVEDGE_LAUNCHER_PID", os.getppid())):
+    sys.exit(143)
+args = sys.argv[1:]
+if args[:1] == ["-m"]:
+    sys.argv = [args[1]] + args[2:]
+    runpy.run_module(args[1], run_name="__main__", alter_sys=True)
+else:
+    sys.argv = list(args)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(args[0])))
+    runpy.run_path(args[0], run_name="__main__")
+"""
 
-    try:
-        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM))  # PR_SET_PDEATHSIG
-    except OSError:
-        pass
+
+_KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def visible_gpu_count(topology: Optional[str] = None) -> int:
+    """Number of GPUs this process would see, WITHOUT initialising HIP.
+
+    ``torch.cuda.device_count()`` on ROCm falls back to ``hipGetDeviceCount`` when amdsmi
+    is unavailable, which initialises the HIP runtime in the caller; a launcher that then
+    forks GPU ranks breaks the rule that a GPU-initialised process never spawns or execs
+    GPU work.  This reads the KFD topology instead: one node per agent, GPUs are the nodes
+    whose ``gfx_target_version`` is non-zero (CPU nodes report 0).  The visibility masks
+    are applied in the runtime's order: ROCR_VISIBLE_DEVICES selects among the agents,
+    then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES index into what is left.
+    ``KVEDGE_KFD_TOPOLOGY`` overrides the sysfs root (tests)."""
+    import glob
+
+    root = topology or os.environ.get("KVEDGE_KFD_TOPOLOGY", _KFD_TOPOLOGY)
+    n = 0
+    for prop in glob.glob(os.path.join(root, "*", "properties")):
+        try:
+            with open(prop) as f:
+                for ln in f:
+                    k, _, v = ln.partition(" ")
+                    if k == "gfx_target_version":
+                        n += int(v.strip() or 0) != 0
+                        break
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        mask = os.environ.get(var)
+        if mask is None:
+            continue
+        ids = [x.strip() for x in mask.split(",") if x.strip()]
+        valid = []
+        for x in ids:
+            if x.isdigit() and int(x) < n:
+                valid.append(x)
+            elif not x.isdigit() and x.upper().startswith("GPU-"):
+                valid.append(x)  # UUID form: cannot be checked without HIP, trust it
+            else:
+                break  # the runtime stops at the first invalid entry
+        n = len(valid)
+    return n
 
 
 def _pump_prefixed(stream, out, prefix: bytes):
@@ -78,7 +135,9 @@ def launch_local(nproc: int, argv: Sequence[str], env: Optional[dict] = None,
     and every node must be given the same master_addr/port (rank 0's node).
 
     The parent must not have touched the GPU (a process that initialised HIP must not
-    be replaced or fork GPU children); it only counts devices.
+    be replaced or fork GPU children); it counts devices with :func:`visible_gpu_count`
+    (sysfs, no HIP).  Children are spawned without a ``preexec_fn`` and arm their own
+    parent-death signal (``_RANK_BOOT``).
 
     Stop paths, all bounded:
       * one rank exits non-zero -> its peers would block in their next collective until
@@ -109,6 +168,7 @@ def launch_local(nproc: int, argv: Sequence[str], env: Optional[dict] = None,
     base = dict(os.environ if env is None else env)
     base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host
     base.setdefault("PYTHONUNBUFFERED", "1")  # prefixed stderr lines arrive as written
+    base["KVEDGE_LAUNCHER_PID"] = str(os.getpid())
     procs, pumps = [], []
     got_signal = []
 
@@ -126,13 +186,14 @@ def launch_local(nproc: int, argv: Sequence[str], env: Optional[dict] = None,
             e = dict(base, RANK=str(grank), LOCAL_RANK=str(r),
                      WORLD_SIZE=str(nnodes * nproc), LOCAL_WORLD_SIZE=str(nproc),
                      MASTER_ADDR=addr, MASTER_PORT=str(master_port))
-            p = subprocess.Popen([sys.executable] + list(argv), env=e,
-                                 stderr=subprocess.PIPE if prefix_stderr else None,
-                                 preexec_fn=_child_preexec)
+            p = subprocess.Popen([sys.executable, "-c", _RANK_BOOT] + list(argv), env=e,
+                                 stderr=subprocess.PIPE if prefix_stderr else None)
             procs.append(p)
-            if prefix_stderr:
+        if prefix_stderr:  # pumps start only once every rank is spawned
+            for r, p in enumerate(procs):
                 t = threading.Thread(target=_pump_prefixed, daemon=True,
-                                     args=(p.stderr, sys.stderr.buffer, f"[rank {grank}] ".encode()))
+                                     args=(p.stderr, sys.stderr.buffer,
+                                           f"[rank {node_rank * nproc + r}] ".encode()))
                 t.start()
                 pumps.append(t)
         rc = 0

@@ -10,7 +10,7 @@ each run's one JSON line, and writes the curve:
    "ms_per_step": ..., "efficiency": per_gpu(N) / per_gpu(N0)}, ...], "base_n": N0}
 
 Weak scaling: per-GPU batch is fixed, so ideal efficiency is 1.0 at every N.  The parent never
-touches the GPU (it only counts devices, which leaves HIP uninitialised on this image), so
+touches the GPU (it counts devices from the KFD topology in sysfs, never through HIP), so
 the children start on clean devices.
 
   python -m kvedge_amd.utils.scaling --gpus 1,2,4,8 --out gpurun_out/scaling.json
@@ -69,9 +69,9 @@ def main(argv: Optional[List[str]] = None) -> int:
     a, rest = ap.parse_known_args(argv)  # everything else goes to bench.py
     ns = [int(x) for x in a.gpus.split(",") if x]
     if not a.cpu:
-        import torch
+        from kvedge_amd.parallel import visible_gpu_count
 
-        ndev = torch.cuda.device_count()  # counts only; HIP stays uninitialised here
+        ndev = visible_gpu_count()  # sysfs: this parent never initialises HIP
         skipped = [n for n in ns if n > ndev]
         if skipped:
             print(f"# skipping N={skipped}: only {ndev} GPU(s) visible", file=sys.stderr)

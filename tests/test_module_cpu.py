@@ -84,6 +84,40 @@ def test_resnet_module_twin_methods_resume(tmp_path):
     app2.stop()
 
 
+def test_report_after_auto_report_never_publishes_empty_window():
+    """with a short report interval the boundary of the LAST step
+    auto-reports (draining the window); an explicit report() right after must carry that
+    window (flagged, with its window_s), never publish 0 img/s."""
+
+    class StepClock:  # advances only when told: the test decides when a report is due
+        t = 0.0
+
+        def __call__(self):
+            return self.t
+
+    clk = StepClock()
+    tr = FakeTransport({"model": "resnet50", "batch": 1, "report_interval_s": 0.5,
+                        "image_size": 64})
+    with ModuleApp(tr, device="cpu", clock=clk).start() as app:
+        real_infer = app._infer_step
+
+        def slow_step():  # each step takes 1 s on the fake clock -> every boundary reports
+            clk.t += 1.0
+            real_infer()
+
+        app._infer_step = slow_step
+        app.run(max_steps=3)
+        auto = tr.outputs("telemetry")
+        assert len(auto) == 3 and auto[-1]["images_per_s"] > 0
+        assert auto[-1]["window_carried"] is False
+        msg = app.report()  # nothing ran since the last auto-report
+        assert msg["images_per_s"] == auto[-1]["images_per_s"] > 0
+        assert msg["window_carried"] is True and msg["window_s"] == auto[-1]["window_s"]
+        assert tr.outputs("telemetry")[-1]["images_per_s"] > 0
+    assert app._closed  # the context manager stopped it
+    app.stop()  # idempotent
+
+
 def test_stdout_transport(capsys):
     tr = StdoutTransport({"model": "simulated-temperature"})
     app = ModuleApp(tr, device="cpu", clock=Clock()).start()

@@ -95,13 +95,14 @@ def test_module_native_serving(source):
 
     tr = FakeTransport({"model": "resnet50", "batch": 8, "report_interval_s": 0.01,
                         "source": source, "steps_per_poll": 4})
-    app = ModuleApp(tr, device="cuda").start()
-    assert app.engine.graph is not None
-    app.run(max_steps=3)
-    app.report()
-    t = tr.outputs("telemetry")[-1]
-    assert t["source"] == source and t["images_per_s"] > 0
-    assert app.state["total_images"] == 3 * 4 * 8
-    if source == "camera":
-        assert app.ring.pinned and app.camera.seq >= 12
-    app.stop()
+    # a failed assertion must still stop the camera thread (a daemon thread left in the
+    # native ring.put() at interpreter exit is std::terminate): context manager
+    with ModuleApp(tr, device="cuda").start() as app:
+        assert app.engine.graph is not None
+        app.run(max_steps=3)
+        app.report()  # may follow an auto-report: then it carries that window
+        t = tr.outputs("telemetry")[-1]
+        assert t["source"] == source and t["images_per_s"] > 0
+        assert app.state["total_images"] == 3 * 4 * 8
+        if source == "camera":
+            assert app.ring.pinned and app.camera.seq >= 12
