@@ -169,6 +169,25 @@ write_files:
       done
       /usr/local/sbin/kvedge-stamp iotedge_check_timeout
       exit 1
+  - path: /usr/local/sbin/kvedge-health
+    permissions: "0755"
+    content: |
+      #!/bin/sh
+      # VMI probe (guest-agent exec): `ready` = the module heartbeat is fresh (or, with no
+      # module, iotedge check passed); `live` = no STALE heartbeat (absent is fine: booting)
+      hb=/var/lib/kvedge/heartbeat; max={{ $v.health.heartbeatMaxAgeS }}
+      age() { echo $(( $(date +%s) - $(stat -c %Y "$hb") )); }
+      case "$1" in
+        ready)
+      {{- if $v.module.enabled }}
+          [ -f "$hb" ] && [ "$(age)" -le "$max" ] ;;
+      {{- else }}
+          grep -q '^iotedge_check_pass ' /var/lib/kvedge/boot-timing 2>/dev/null ;;
+      {{- end }}
+        live)
+          [ ! -f "$hb" ] || [ "$(age)" -le "$max" ] ;;
+        *) exit 2 ;;
+      esac
   - path: /etc/systemd/system/kvedge-config.service
     content: |
       [Unit]
@@ -203,6 +222,10 @@ runcmd:
   - [systemctl, daemon-reload]
   - [systemctl, enable, --now, kvedge-config.service]
   - [systemctl, enable, --now, --no-block, kvedge-ready.service]
+{{- if $v.health.enabled }}
+  # exec probes run through the QEMU guest agent (pre-baked; apt only without the image)
+  - [sh, -c, "command -v qemu-ga >/dev/null || {{ if $v.image.prebaked }}true{{ else }}apt-get install -y qemu-guest-agent{{ end }}; systemctl enable --now qemu-guest-agent || true"]
+{{- end }}
   - [/usr/local/sbin/kvedge-gpu-check, "{{ $v.gpu.count }}", "{{ $v.guest.gpuWaitSeconds }}"]
   - [/usr/local/sbin/kvedge-stamp, runcmd_done]
 final_message: "kvedge guest {{ $v.guest.hostname }}{{ include "kvedge.sfx" . }} up after $UPTIME s"

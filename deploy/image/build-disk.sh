@@ -55,13 +55,13 @@ virt-customize -a build/kvedge-guest.qcow2 \
   --run-command "curl -fsSL https://packages.microsoft.com/config/ubuntu/${UBUNTU_VER}/packages-microsoft-prod.deb -o /tmp/ms.deb && dpkg -i /tmp/ms.deb" \
   --run-command "mkdir -p /etc/apt/keyrings && curl -fsSL https://repo.radeon.com/rocm/rocm.gpg.key | gpg --dearmor -o /etc/apt/keyrings/rocm.gpg" \
   --run-command "echo 'deb [arch=amd64 signed-by=/etc/apt/keyrings/rocm.gpg] ${ROCM_REPO} ${UBUNTU} main' > /etc/apt/sources.list.d/amdgpu.list" \
-  --run-command "apt-get update && DEBIAN_FRONTEND=noninteractive apt-get install -y linux-generic moby-engine aziot-edge dkms" \
+  --run-command "apt-get update && DEBIAN_FRONTEND=noninteractive apt-get install -y linux-generic moby-engine aziot-edge dkms qemu-guest-agent" \
   --run-command "KVER=\$(ls /lib/modules | sort -V | tail -1) && DEBIAN_FRONTEND=noninteractive apt-get install -y linux-headers-\$KVER && DEBIAN_FRONTEND=noninteractive apt-get install -y --no-install-recommends amdgpu-dkms && dkms autoinstall -k \$KVER && modinfo -k \$KVER amdgpu > /var/log/kvedge-amdgpu-modinfo.txt && echo \$KVER > /etc/kvedge-guest-kernel" \
   --run-command "echo 'blacklist amdgpu_fbdev' > /etc/modprobe.d/kvedge.conf" \
   --mkdir /var/lib/kvedge/images \
   --copy-in build/images:/var/lib/kvedge \
   --copy-in build/kvedge-preload.service:/etc/systemd/system \
-  --run-command "systemctl enable docker kvedge-preload.service aziot-edged || true" \
+  --run-command "systemctl enable docker kvedge-preload.service aziot-edged qemu-guest-agent || true" \
   --run-command "apt-get clean && rm -rf /var/lib/apt/lists/*" \
   --run-command "cloud-init clean --logs || true"
 # proof the module exists for the guest kernel (the command above already failed the

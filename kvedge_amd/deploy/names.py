@@ -1,5 +1,5 @@
 """Resource names the chart renders, computed without rendering (for the boot-timing
-collector and the resilience KubectlAdapter).  Mirrors deploy/helm/templates/_helpers.tpl
+collector and the resilience KubectlCluster).  Mirrors deploy/helm/templates/_helpers.tpl
 (reference naming rule _helper.tpl:6-8: default .Chart.Name .Values.nameOverride |
 trunc 40 | trimSuffix "-"; replica i > 0 appends "-<i>").  tests/test_chart.py checks
 these against an actual render."""

@@ -69,6 +69,8 @@ def main(argv=None):
     ap.add_argument("--sync-every", type=int, default=d.sync_every,
                     help="module steps between lockstep control boundaries (0 = auto)")
     ap.add_argument("--state", default=os.environ.get("KVEDGE_STATE", "/var/lib/kvedge/module-state.json"))
+    ap.add_argument("--heartbeat", default=os.environ.get("KVEDGE_HEARTBEAT", ""),
+                    help="heartbeat file rewritten at every report (VMI health probes)")
     ap.add_argument("--stamps", default=os.environ.get("KVEDGE_STAMPS", "/var/lib/kvedge/boot-timing"),
                     help="guest boot-timing stamp file (module_first_inference is appended)")
     a = ap.parse_args(argv)
@@ -81,7 +83,7 @@ def main(argv=None):
     # one IoT Edge identity per VM: only local rank 0 talks to edgeHub
     kind = a.transport if di.local_rank == 0 or a.transport != "azure" else "null"
     app = ModuleApp(make_transport(kind), cfg, state_path=a.state,
-                    stamp_path=a.stamps or None)
+                    stamp_path=a.stamps or None, heartbeat_path=a.heartbeat or None)
     # SIGTERM (edgeAgent stop, VM shutdown) only votes to stop: the replicas leave the
     # loop together at the next control boundary, so the final report's collectives match
     signal.signal(signal.SIGTERM, lambda *_: app.request_stop())

@@ -128,7 +128,8 @@ class _CameraSource:
 class ModuleApp:
     def __init__(self, transport: Transport, config: Optional[ModuleConfig] = None,
                  device: Optional[str] = None, state_path: Optional[str] = None,
-                 clock=time.perf_counter, stamp_path: Optional[str] = None):
+                 clock=time.perf_counter, stamp_path: Optional[str] = None,
+                 heartbeat_path: Optional[str] = None):
         self.tr = transport
         self.cfg = (config or ModuleConfig()).validate()
         self.device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
@@ -136,6 +137,9 @@ class ModuleApp:
         # guest boot-timing stamp file (chart cloud-init writes the same file); the module
         # adds ``module_first_inference`` -- one leg of the boot-to-ready headline
         self.stamp_path = stamp_path
+        # module liveness for the VMI probes (chart: kvedge-health reads its mtime): one
+        # small JSON rewritten atomically at every telemetry report, local rank 0 only
+        self.heartbeat_path = heartbeat_path
         self.clock = clock
         self.engine = None
         self.model = None
@@ -171,6 +175,7 @@ class ModuleApp:
             self.state_path = f"{root}.rank{self.rank}{ext}"
         if parallel.info().local_rank != 0:
             self.stamp_path = None  # one boot-timing stamp per VM
+            self.heartbeat_path = None  # one heartbeat per VM
         # lockstep control plane
         self._events: List[Tuple[str, Any]] = []      # queued since the last boundary
         self._replies: List[Optional[Deferred]] = []  # parallel to _events (own rank)
@@ -303,6 +308,20 @@ class ModuleApp:
                 f.write(f"{name} {time.time():.6f}\n")
         except OSError:
             pass  # read-only / missing mount: timing is best-effort, never fatal
+
+    def _heartbeat(self, msg: Dict[str, Any]):
+        if not self.heartbeat_path:
+            return
+        try:
+            os.makedirs(os.path.dirname(self.heartbeat_path) or ".", exist_ok=True)
+            tmp = self.heartbeat_path + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump({"ts": time.time(), "heartbeat": self.state["total_steps"],
+                           "images_per_s": msg.get("images_per_s"),
+                           "model": self.cfg.model, "rank": self.rank}, f)
+            os.replace(tmp, self.heartbeat_path)
+        except OSError:
+            pass  # read-only / missing mount: the probe then reports not-ready, never fatal
 
     def _build_local(self):
         """Build model + engine for self.cfg on this rank (no collectives)."""
@@ -441,6 +460,7 @@ class ModuleApp:
                 self.state["messages"] += 1
                 self._last_report = now
                 self._save_state()
+                self._heartbeat({})
                 if not self._first_inference_stamped:
                     self._first_inference_stamped = True
                     self._stamp("module_first_message")
@@ -587,6 +607,7 @@ class ModuleApp:
             self.tr.send_message("telemetry", msg)
             self.state["messages"] += 1
         self.last_telemetry = msg
+        self._heartbeat(msg)
         self._win_imgs, self._lat_ms = 0, []
         if self._hist is not None:
             self._hist.reset()

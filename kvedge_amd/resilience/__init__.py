@@ -9,7 +9,10 @@ kvedge adds, for VMs with VFIO-passed GPUs (which KubeVirt cannot live-migrate):
   * a controller that turns drain / node loss / GPU failure into a COLD migration:
     stop the VMI, release its GPUs, pick a node with free MI355X capacity whose storage
     can attach the boot PVC (RWX anywhere, RWO only on its bound node), start it,
-    re-attach GPUs, wait for the module heartbeat -- with a per-phase timeline;
+    re-attach GPUs, wait for the VMI Running AND for the module to report healthy (the
+    chart's VMI readinessProbe reads the module heartbeat file through the guest agent)
+    -- with a per-phase timeline (stop -> schedule -> PVC attach -> GPU attach -> VMI
+    Running -> module ready, :attr:`Recovery.phases`);
   * ONE controller (:class:`ResilienceController`) that drives any :class:`Cluster`:
     the dict-backed :class:`FakeCluster` (simulated clock, fault injection; tests) or
     :class:`KubectlCluster`, which reads ``kubectl get vm/vmi/node -o json`` and issues
@@ -45,6 +48,7 @@ class Timings:
     gpu_attach: float = 3.0
     guest_boot: float = 45.0
     module_ready: float = 15.0
+    module_ready_timeout: float = 300.0  # a module that never turns healthy: give up after
     source: str = "assumed"
 
     @classmethod
@@ -136,6 +140,14 @@ class Cluster(Protocol):
 
     def fail_node(self, node: str) -> None: ...
 
+    def wait_module_ready(self, vm_name: str) -> bool: ...
+
+
+# event name -> phase it ends (Recovery.phases): the time since the previous event
+PHASES = {"stopped": "stop", "scheduled": "schedule", "pvc_attached": "pvc_attach",
+          "gpu_attached": "gpu_attach", "running": "vmi_running",
+          "module_ready": "module_ready", "module_not_ready": "module_ready"}
+
 
 class FakeCluster:
     """Dict-backed KubeVirt-ish cluster with a simulated clock and fault injection."""
@@ -148,6 +160,7 @@ class FakeCluster:
         self.t = 0.0
         self.timings = timings or Timings()
         self.events: List[Event] = []
+        self.unhealthy: set = set()  # fault injection: modules that never turn healthy
 
     def log(self, vm, what, detail=""):
         self.events.append(Event(self.t, vm, what, detail))
@@ -174,6 +187,16 @@ class FakeCluster:
 
     def fail_node(self, node: str) -> None:
         self.node_down(node)
+
+    def wait_module_ready(self, vm_name: str) -> bool:
+        """The VMI's readiness probe (module heartbeat) turning true, or the timeout."""
+        if vm_name in self.unhealthy or vm_name not in self.vmis:
+            self.advance(self.timings.module_ready_timeout)
+            self.log(vm_name, "module_not_ready", "readiness probe failing")
+            return False
+        self.advance(self.timings.module_ready)
+        self.log(vm_name, "module_ready", self.vmis[vm_name].node)
+        return True
 
     # --- objects -------------------------------------------------------------
     def add_node(self, name: str, n_gpus: int):
@@ -228,8 +251,6 @@ class FakeCluster:
         vmi = VMI(vm_name, node.name, ids)
         self.vmis[vm_name] = vmi
         self.log(vm_name, "running", node.name)
-        self.advance(tm.module_ready)
-        self.log(vm_name, "module_ready", node.name)
         return vmi
 
     def stop(self, vm_name: str, graceful: bool = True):
@@ -256,6 +277,11 @@ class FakeCluster:
                 self.log(name, "fault", f"node {node} lost")
         self.advance(self.timings.node_failure_detect)
 
+    def break_module(self, vm_name: str):
+        """The guest runs but its module never reports healthy (bad image, GPU fault
+        inside the guest, ...): the readiness probe keeps failing."""
+        self.unhealthy.add(vm_name)
+
     def gpu_failure(self, gpu_id: str):
         node = self.nodes[gpu_id.split("/")[0]]
         vm = node.used.get(gpu_id)
@@ -268,21 +294,48 @@ class FakeCluster:
 @dataclass
 class Recovery:
     vm: str
-    ok: bool
+    ok: bool  # VMI Running AND module healthy
     from_node: Optional[str]
     to_node: Optional[str]
     seconds: float
     live_migration_refused: bool = False
     reason: str = ""
     gpu_ids: List[str] = field(default_factory=list)
+    module_ready: bool = False
+    # seconds per phase, in order (keys of PHASES' values): stop, schedule, pvc_attach,
+    # gpu_attach, vmi_running, module_ready -- the phases this cluster can observe
+    phases: Dict[str, float] = field(default_factory=dict)
 
 
 class ResilienceController:
     """Reconciles VMs with runStrategy Always; implements drain as cold migration.
-    Drives any :class:`Cluster` (fake or kubectl) through the same code path."""
+    Drives any :class:`Cluster` (fake or kubectl) through the same code path.  A recovery
+    counts as done only when the module is healthy again (``Cluster.wait_module_ready``:
+    the VMI's readiness probe), not when the VMI is merely Running."""
 
     def __init__(self, cluster: Cluster):
         self.c = cluster
+
+    def _finish(self, name: str, vmi: Optional[VMI], t0: float, from_node: Optional[str],
+                refused: bool = False) -> Recovery:
+        ready = vmi is not None and self.c.wait_module_ready(name)
+        reason = "" if ready else (self._why(name) if vmi is None else
+                                   "module not ready: readiness probe failing")
+        return Recovery(name, ready, from_node, vmi.node if vmi else None, self.c.now() - t0,
+                        refused, reason, vmi.gpu_ids if vmi else [], module_ready=ready,
+                        phases=self.phases(name, t0))
+
+    def phases(self, vm: str, t0: float) -> Dict[str, float]:
+        """Per-phase seconds of the recovery of ``vm`` that started at ``t0``."""
+        out: Dict[str, float] = {}
+        prev = t0
+        for e in self.c.events:
+            if e.vm != vm or e.t < t0 or e.what not in PHASES:
+                continue
+            ph = PHASES[e.what]
+            out[ph] = out.get(ph, 0.0) + (e.t - prev)
+            prev = e.t
+        return out
 
     def reconcile(self) -> List[Recovery]:
         out = []
@@ -290,10 +343,7 @@ class ResilienceController:
         for name, vm in self.c.list_vms().items():
             if vm.run_strategy == "Always" and name not in vmis:
                 t0 = self.c.now()
-                vmi = self.c.wait_recreated(name)
-                out.append(Recovery(name, vmi is not None, None, vmi.node if vmi else None,
-                                    self.c.now() - t0, reason="" if vmi else self._why(name),
-                                    gpu_ids=vmi.gpu_ids if vmi else []))
+                out.append(self._finish(name, self.c.wait_recreated(name), t0, None))
         return out
 
     def _why(self, name):
@@ -302,7 +352,8 @@ class ResilienceController:
 
     def drain(self, node_name: str, request_live_migration: bool = True) -> List[Recovery]:
         """Cordon, then cold-migrate every VMI on the node: stop (releases its MI355X),
-        start (the scheduler picks a node with free GPUs the boot PVC can attach to)."""
+        start (the scheduler picks a node with free GPUs the boot PVC can attach to), wait
+        until the module is healthy."""
         self.c.cordon(node_name)
         vms = self.c.list_vms()
         res = []
@@ -315,23 +366,14 @@ class ResilienceController:
                 self.c.log(name, "live_migration_refused", "VFIO host devices are not migratable")
             t0 = self.c.now()
             self.c.stop(name, graceful=True)
-            new = self.c.start(name)
-            res.append(Recovery(name, new is not None, node_name, new.node if new else None,
-                                self.c.now() - t0, refused, "" if new else self._why(name),
-                                new.gpu_ids if new else []))
+            res.append(self._finish(name, self.c.start(name), t0, node_name, refused))
         return res
 
     def recover_node_loss(self, node_name: str) -> List[Recovery]:
         victims = sorted(n for n, v in self.c.list_vmis().items() if v.node == node_name)
         t0 = self.c.now()
         self.c.fail_node(node_name)
-        res = []
-        for name in victims:
-            new = self.c.start(name)
-            res.append(Recovery(name, new is not None, node_name, new.node if new else None,
-                                self.c.now() - t0, reason="" if new else self._why(name),
-                                gpu_ids=new.gpu_ids if new else []))
-        return res
+        return [self._finish(name, self.c.start(name), t0, node_name) for name in victims]
 
     def timeline(self, vm: str) -> List[Tuple[float, str, str]]:
         return [(e.t, e.what, e.detail) for e in self.c.events if e.vm == vm]
@@ -349,6 +391,9 @@ class KubectlCluster:
                  {.status.phase}=Running``, then the VMI is re-read for its node
       wait_recreated -> only the Running wait (runStrategy Always: KubeVirt's VM
                  controller recreates the VMI itself)
+      wait_module_ready -> ``kubectl wait vmi/VM --for=condition=Ready``: the VMI Ready
+                 condition is the chart's readinessProbe (guest-agent exec of
+                 ``kvedge-health ready``: a fresh module heartbeat file)
     A failed wait (timeout: no node with a free MI355X, RWO PVC bound elsewhere) makes
     the operation return None and logs ``unschedulable`` with kubectl's message.
     ``dry_run`` executes nothing: the VMI after a start is reported on node
@@ -359,13 +404,15 @@ class KubectlCluster:
                  snapshot: Optional[Dict[str, dict]] = None,
                  runner: Optional[Callable[[List[str]], str]] = None,
                  clock: Callable[[], float] = time.monotonic,
-                 stop_timeout_s: int = 300, start_timeout_s: int = 600):
+                 stop_timeout_s: int = 300, start_timeout_s: int = 600,
+                 ready_timeout_s: int = 900):
         self.ns = namespace
         self.dry_run = dry_run
         self.snapshot = dict(snapshot or {})
         self.runner = runner or self._subprocess
         self.clock = clock
         self.stop_timeout_s, self.start_timeout_s = stop_timeout_s, start_timeout_s
+        self.ready_timeout_s = ready_timeout_s
         self.commands: List[List[str]] = []
         self.events: List[Event] = []
         self._gone: set = set()  # dry-run bookkeeping: VMIs stopped and not restarted
@@ -475,58 +522,11 @@ class KubectlCluster:
                 self.stop(name, graceful=False)
                 self.log(name, "fault", f"node {node} lost")
 
-
-class KubectlAdapter:
-    """The same operations against a real cluster (kubectl + virtctl).  dry_run=True
-    returns the command lines without executing them.  VM names come from
-    :class:`kvedge_amd.deploy.names.ChartNames` (checked against a chart render in
-    tests/test_resilience.py)."""
-
-    def __init__(self, namespace: str = "default", dry_run: bool = True):
-        self.ns = namespace
-        self.dry_run = dry_run
-        self.log: List[List[str]] = []
-
-    def _run(self, *cmd: str) -> str:
-        self.log.append(list(cmd))
-        if self.dry_run:
-            return ""
-        return subprocess.run(list(cmd), check=True, capture_output=True, text=True).stdout
-
-    def drain_node(self, node: str):
-        self._run("kubectl", "cordon", node)
-        # VFIO VMIs refuse live migration: stop them explicitly so the VM controller
-        # (runStrategy Always) reschedules them cold on another node
-        self._run("kubectl", "drain", node, "--ignore-daemonsets", "--delete-emptydir-data",
-                  "--pod-selector=kubevirt.io=virt-launcher", "--timeout=300s")
-
-    def restart_vm(self, vm: str):
-        self._run("virtctl", "restart", vm, "-n", self.ns)
-
-    def stop_vm(self, vm: str):
-        self._run("virtctl", "stop", vm, "-n", self.ns)
-
-    def start_vm(self, vm: str):
-        self._run("virtctl", "start", vm, "-n", self.ns)
-
-    def wait_running(self, vm: str, timeout_s: int = 600):
-        self._run("kubectl", "wait", f"vmi/{vm}", "-n", self.ns, "--for=jsonpath={.status.phase}=Running",
-                  f"--timeout={timeout_s}s")
-
-    def uncordon(self, node: str):
-        self._run("kubectl", "uncordon", node)
-
-    def wait_deleted(self, vm: str, timeout_s: int = 300):
-        self._run("kubectl", "wait", f"vmi/{vm}", "-n", self.ns, "--for=delete",
-                  f"--timeout={timeout_s}s")
-
-    def cold_migrate(self, vm: str, from_node: str, timeout_s: int = 600):
-        """Drain one node's GPU VM the only way VFIO allows: cordon, stop (releases the
-        MI355X), wait until the VMI is gone, start (scheduler picks a node with a free
-        GPU; RWX storage lets it leave the node), wait Running; uncordon is left to the
-        operator after maintenance."""
-        self._run("kubectl", "cordon", from_node)
-        self.stop_vm(vm)
-        self.wait_deleted(vm)
-        self.start_vm(vm)
-        self.wait_running(vm, timeout_s)
+    def wait_module_ready(self, vm_name: str) -> bool:
+        err = self._write("kubectl", "wait", f"vmi/{vm_name}", "-n", self.ns,
+                          "--for=condition=Ready", f"--timeout={self.ready_timeout_s}s")
+        if err is not None:
+            self.log(vm_name, "module_not_ready", err)
+            return False
+        self.log(vm_name, "module_ready", "")
+        return True

@@ -151,7 +151,7 @@ def helm_first_deployed(status_json: dict) -> float:
 class ClusterReader:
     """Reads the timeline inputs from a live cluster (kubectl, helm, virtctl ssh).
     ``dry_run`` records the command lines and returns nothing (no cluster in CI) -- the
-    same adapter pattern as kvedge_amd.resilience.KubectlAdapter."""
+    same adapter pattern as kvedge_amd.resilience.KubectlCluster."""
 
     def __init__(self, namespace: str = "default", dry_run: bool = False,
                  ssh_user: str = "ubuntu"):

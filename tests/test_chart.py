@@ -458,3 +458,57 @@ def test_guest_image_build_targets_guest_kernel():
     assert "set -euo pipefail" in txt
     assert "kvedge-preload.service" in txt and "Before=aziot-edged.service" in txt
     assert "docker save" in txt and "--copy-in build/images:/var/lib/kvedge" in txt
+
+
+def test_vmi_health_probes_and_heartbeat_script(tmp_path):
+    """the VM template carries guest-agent exec readiness / liveness
+    probes; `kvedge-health` reads the module heartbeat the module writes (fresh -> ready,
+    stale -> not live, absent -> not ready but live); the module manifest points the
+    module at that file; health.enabled=false removes the probes."""
+    import time
+
+    from kvedge_amd.module.app import ModuleApp
+    from kvedge_amd.module.transport import FakeTransport
+
+    _, objs = render()
+    spec = by_kind(objs, "VirtualMachine")[0]["spec"]["template"]["spec"]
+    rp, lp = spec["readinessProbe"], spec["livenessProbe"]
+    assert rp["exec"]["command"] == ["/usr/local/sbin/kvedge-health", "ready"]
+    assert lp["exec"]["command"] == ["/usr/local/sbin/kvedge-health", "live"]
+    assert rp["periodSeconds"] == 10 and lp["initialDelaySeconds"] == 600
+    _, ci = _cloudinit(objs)
+    flat = [" ".join(map(str, c)) if isinstance(c, list) else c for c in ci["runcmd"]]
+    assert any("qemu-guest-agent" in c for c in flat)
+    cm = [o for o in by_kind(objs, "ConfigMap") if o["metadata"]["name"].endswith("module-deployment")][0]
+    dep = json.loads(cm["data"]["deployment.json"])
+    env = dep["modulesContent"]["$edgeAgent"]["properties.desired"]["modules"]["kvedge"]["env"]
+    assert env["KVEDGE_HEARTBEAT"]["value"] == "/var/lib/kvedge/heartbeat"
+    # the script, in a fake root
+    files = {f["path"]: f["content"] for f in ci["write_files"]}
+    (tmp_path / "var/lib/kvedge").mkdir(parents=True)
+    sh = tmp_path / "health.sh"
+    sh.write_text(_fake_root_script(files["/usr/local/sbin/kvedge-health"], tmp_path))
+    probe = lambda what: subprocess.run(["sh", str(sh), what]).returncode  # noqa: E731
+    assert probe("ready") != 0 and probe("live") == 0  # booting: no heartbeat yet
+    # the module writes the heartbeat at its first report
+    tr = FakeTransport({"model": "simulated-temperature", "send_interval_s": 1.0})
+    hb = tmp_path / "var/lib/kvedge/heartbeat"
+    app = ModuleApp(tr, device="cpu", heartbeat_path=str(hb)).start()
+    app.run(max_steps=2)
+    app.stop()
+    assert json.loads(hb.read_text())["model"] == "simulated-temperature"
+    assert probe("ready") == 0 and probe("live") == 0
+    old = time.time() - 3600
+    os.utime(hb, (old, old))  # module hung: heartbeat stale
+    assert probe("ready") != 0 and probe("live") != 0
+    # module disabled: readiness = iotedge check passed
+    _, objs2 = render(sets=["module.enabled=false"])
+    _, ci2 = _cloudinit(objs2)
+    f2 = {f["path"]: f["content"] for f in ci2["write_files"]}["/usr/local/sbin/kvedge-health"]
+    sh.write_text(_fake_root_script(f2, tmp_path))
+    assert probe("ready") != 0
+    (tmp_path / "var/lib/kvedge/boot-timing").write_text("iotedge_check_pass 1.0\n")
+    assert probe("ready") == 0
+    _, objs3 = render(sets=["health.enabled=false"])
+    spec3 = by_kind(objs3, "VirtualMachine")[0]["spec"]["template"]["spec"]
+    assert "readinessProbe" not in spec3 and "livenessProbe" not in spec3

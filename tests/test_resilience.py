@@ -2,7 +2,7 @@
 and the same controller over a dry-run / scripted KubectlCluster."""
 import json
 
-from kvedge_amd.resilience import (RWO, RWX, FakeCluster, KubectlAdapter, ResilienceController,
+from kvedge_amd.resilience import (RWO, RWX, FakeCluster, KubectlCluster, ResilienceController,
                                    Timings)
 
 
@@ -49,6 +49,13 @@ def test_drain_rwx_cold_migrates_with_gpu_reattach():
     tm = c.timings
     assert r.seconds == tm.graceful_stop + tm.schedule + tm.pvc_attach + tm.gpu_attach + \
         tm.guest_boot + tm.module_ready
+    # per-phase timeline, in order, summing to the total
+    assert list(r.phases) == ["stop", "schedule", "pvc_attach", "gpu_attach", "vmi_running",
+                              "module_ready"]
+    assert r.phases == {"stop": tm.graceful_stop, "schedule": tm.schedule,
+                        "pvc_attach": tm.pvc_attach, "gpu_attach": tm.gpu_attach,
+                        "vmi_running": tm.guest_boot, "module_ready": tm.module_ready}
+    assert r.module_ready and abs(sum(r.phases.values()) - r.seconds) < 1e-9
     assert not c.nodes[src].used  # GPUs released on the drained node
 
 
@@ -79,17 +86,36 @@ def test_node_loss_and_capacity_limits():
     assert all(r.ok for r in rec2) and len(c.vmis) == 3
 
 
-def test_kubectl_adapter_dry_run():
-    k = KubectlAdapter("edge", dry_run=True)
-    k.drain_node("n1")
-    k.restart_vm("aziot-edge-kubevirt-linux")
-    k.wait_running("aziot-edge-kubevirt-linux")
-    k.uncordon("n1")
-    cmds = [" ".join(c) for c in k.log]
-    assert cmds[0] == "kubectl cordon n1"
-    assert cmds[1].startswith("kubectl drain n1")
-    assert cmds[2] == "virtctl restart aziot-edge-kubevirt-linux -n edge"
-    assert "--for=jsonpath={.status.phase}=Running" in cmds[3]
+def test_module_never_healthy_is_not_a_recovery():
+    """a VMI that runs but whose module never turns healthy (the
+    readiness probe keeps failing) must not count as recovered."""
+    c, ctl = _cluster(access=RWX)
+    ctl.reconcile()
+    src = c.vmis["vm0"].node
+    c.break_module("vm0")
+    rec = {r.vm: r for r in ctl.drain(src)}["vm0"]
+    assert not rec.ok and not rec.module_ready and rec.to_node and rec.to_node != src
+    assert "module not ready" in rec.reason
+    assert rec.phases["module_ready"] == c.timings.module_ready_timeout
+    tl = [w for _, w, _ in ctl.timeline("vm0")]
+    assert tl[-2:] == ["running", "module_not_ready"]
+
+
+def test_kubectl_cluster_dry_run_commands():
+    snap, names = _rendered_snapshot(1)
+    k = KubectlCluster("edge", dry_run=True, snapshot=snap)
+    k.cordon("n1")
+    k.stop(names[0], graceful=False)
+    assert k.start(names[0]) is not None
+    assert k.wait_module_ready(names[0])
+    cmds = [" ".join(c) for c in k.commands]
+    assert cmds == ["kubectl cordon n1",
+                    f"virtctl stop {names[0]} -n edge --force --grace-period=0",
+                    f"kubectl wait vmi/{names[0]} -n edge --for=delete --timeout=300s",
+                    f"virtctl start {names[0]} -n edge",
+                    f"kubectl wait vmi/{names[0]} -n edge --for=jsonpath={{.status.phase}}=Running "
+                    "--timeout=600s",
+                    f"kubectl wait vmi/{names[0]} -n edge --for=condition=Ready --timeout=900s"]
 
 
 def test_timings_are_labelled_and_driven_by_boot_collector():
@@ -111,8 +137,8 @@ def test_timings_are_labelled_and_driven_by_boot_collector():
     assert rec[0].seconds == t.schedule + t.pvc_attach + t.gpu_attach + 25.0 + 27.0
 
 
-def test_kubectl_adapter_uses_rendered_chart_names():
-    """The adapter's targets are exactly the VirtualMachines the chart renders."""
+def test_kubectl_cluster_uses_rendered_chart_names():
+    """The kubectl controller's targets are exactly the VirtualMachines the chart renders."""
     from kvedge_amd.deploy.helm import Chart, manifests
     from kvedge_amd.deploy.names import ChartNames
     import os
@@ -123,17 +149,13 @@ def test_kubectl_adapter_uses_rendered_chart_names():
     vms = [o["metadata"]["name"] for o in objs if o["kind"] == "VirtualMachine"]
     names = ChartNames("aziot-edge-kubevirt", 3)
     assert names.all_vms() == vms
-    k = KubectlAdapter("edge", dry_run=True)
-    k.cold_migrate(names.vm(2), "n1")
-    cmds = [" ".join(c) for c in k.log]
-    assert cmds == ["kubectl cordon n1",
-                    f"virtctl stop {vms[2]} -n edge",
-                    f"kubectl wait vmi/{vms[2]} -n edge --for=delete --timeout=300s",
-                    f"virtctl start {vms[2]} -n edge",
-                    f"kubectl wait vmi/{vms[2]} -n edge --for=jsonpath={{.status.phase}}=Running "
-                    "--timeout=600s"]
+    snap, rendered = _rendered_snapshot(3)
+    assert rendered == vms
+    k = KubectlCluster("edge", dry_run=True, snapshot=snap)
+    assert sorted(k.list_vms()) == sorted(vms)
     dvs = {o["metadata"]["name"] for o in objs if o["kind"] == "DataVolume"}
     assert {names.dv(i) for i in range(3)} == dvs
+    assert {v.pvc for v in k.list_vms().values()} == dvs
     svcs = {o["metadata"]["name"] for o in objs if o["kind"] == "Service"}
     assert {names.ssh_service(i) for i in range(3)} | {names.rendezvous()} == svcs
     secrets = {o["metadata"]["name"] for o in objs if o["kind"] == "Secret"}
@@ -222,11 +244,14 @@ def test_one_controller_drives_kubectl_cluster_dry_run():
                  f"kubectl wait vmi/{vm} -n edge --for=delete --timeout=300s",
                  f"virtctl start {vm} -n edge",
                  f"kubectl wait vmi/{vm} -n edge --for=jsonpath={{.status.phase}}=Running "
-                 "--timeout=600s"]
+                 "--timeout=600s",
+                 f"kubectl wait vmi/{vm} -n edge --for=condition=Ready --timeout=900s"]
     assert cmds == want
     # the same controller on the fake cluster still cold-migrates (fake tests above)
     assert [w for _, w, _ in ctl.timeline(names[0])] == [
-        "live_migration_refused", "stopped", "running"]
+        "live_migration_refused", "stopped", "running", "module_ready"]
+    assert all(r.module_ready and set(r.phases) == {"stop", "vmi_running", "module_ready"}
+               for r in rec)
 
 
 def test_kubectl_cluster_reports_unschedulable_and_node_loss():
@@ -256,3 +281,4 @@ def test_kubectl_cluster_reports_unschedulable_and_node_loss():
     assert sum("--force --grace-period=0" in c for c in seen) == 2  # both VMIs on node-a
     assert rec[names[0]].ok and rec[names[0]].to_node == "node-b"
     assert not rec[names[1]].ok and "timed out" in rec[names[1]].reason
+    assert any("--for=condition=Ready" in c and names[0] in c for c in seen)
