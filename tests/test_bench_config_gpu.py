@@ -82,7 +82,9 @@ def test_yolov8n_bench_config_vs_fp32_reference():
 
     ref = init_yolov8n(seed=0)
     kv = KvYoloV8n(ref, "cuda")
-    eng = InferenceEngine(kv, BENCH_BATCH["yolov8n"], 640, device="cuda", seed=0, use_graph=True)
+    # the bench's exact configuration: batch AND stream slices
+    eng = InferenceEngine(kv, BENCH_BATCH["yolov8n"], 640, device="cuda", seed=0, use_graph=True,
+                          streams=BENCH_STREAMS["yolov8n"])
     eng.prepare(warmup=1, autotune=True)
     assert eng.graph is not None and eng.tuning
     eng.run()
