@@ -128,8 +128,6 @@ def main(argv=None):
 
         model = KvResNet50.build(seed=a.seed, device=di.device, calibrate=on_gpu)
         model.microbatch, model.microbatch_blocks = a.microbatch, a.mb_blocks
-        # A/B knob: the fused stage-1 bottleneck body (conv_block.hip, opt-in)
-        model.fuse_block = os.environ.get("KVEDGE_FUSE_BLOCK", "0") == "1"
         hw = KvResNet50.image_size
     else:
         from kvedge_amd.models.yolov8 import KvYoloV8n

@@ -249,56 +249,6 @@ void conv_tail(const at::Tensor& x, const c10::optional<at::Tensor>& x2, const a
   TORCH_CHECK(rc == 0, "kvedge: conv_tail failed rc=", rc);
 }
 
-// Fused 64-wide bottleneck body (conv_block.hip): c2 = ReLU(conv3x3(t) + b2) stays on chip;
-// y = ReLU(c2 . W3^T + b3 + res) -- or the dual form with the downsample source x2 -- and
-// z = ReLU(y . W1^T + b1), the next block's 1x1 reduce.
-void conv_block(const at::Tensor& t, const at::Tensor& w2, const at::Tensor& b2,
-                const at::Tensor& w3, const at::Tensor& b3, const c10::optional<at::Tensor>& x2,
-                const c10::optional<at::Tensor>& res, at::Tensor& y, const at::Tensor& w1,
-                const at::Tensor& b1, at::Tensor& z) {
-  check_bf16(t, "t");
-  check_bf16(w2, "w2");
-  check_bf16(w3, "w3");
-  check_bf16(y, "y");
-  check_bf16(w1, "w1");
-  check_bf16(z, "z");
-  for (const at::Tensor* b : {&b2, &b3, &b1}) {
-    check_dev(*b, "bias");
-    TORCH_CHECK(b->scalar_type() == at::kFloat, "kvedge: conv_block biases fp32");
-  }
-  TORCH_CHECK(t.dim() == 4 && t.size(3) == 64, "kvedge: conv_block t [N,H,W,64]");
-  const int64_t N = t.size(0), H = t.size(1), W = t.size(2), nt = w1.size(0);
-  TORCH_CHECK(w2.dim() == 2 && w2.size(0) == 64 && w2.size(1) == 576, "kvedge: w2 [64, 576]");
-  TORCH_CHECK(b2.numel() >= 64 && b3.numel() >= 256 && b1.numel() >= nt, "kvedge: bias sizes");
-  TORCH_CHECK(y.dim() == 4 && y.size(0) == N && y.size(1) == H && y.size(2) == W && y.size(3) == 256,
-              "kvedge: y [N,H,W,256]");
-  TORCH_CHECK(w1.dim() == 2 && w1.size(1) == 256 && (nt == 64 || nt == 128), "kvedge: w1 [64|128, 256]");
-  TORCH_CHECK(z.dim() == 4 && z.size(0) == N && z.size(1) == H && z.size(2) == W && z.size(3) == nt,
-              "kvedge: z [N,H,W,nt]");
-  const bool dual = x2.has_value() && x2->defined();
-  const bool has_res = res.has_value() && res->defined();
-  TORCH_CHECK(dual != has_res, "kvedge: conv_block takes exactly one of x2 / res");
-  KvBlockParams p{};
-  if (dual) {
-    check_bf16(*x2, "x2");
-    TORCH_CHECK(x2->sizes() == t.sizes(), "kvedge: x2 [N,H,W,64] (stride-1 downsample)");
-    TORCH_CHECK(w3.dim() == 2 && w3.size(0) == 256 && w3.size(1) == 128, "kvedge: dual w3 [256, 128]");
-    p.x2 = x2->data_ptr();
-  } else {
-    check_bf16(*res, "res");
-    TORCH_CHECK(res->sizes() == y.sizes(), "kvedge: res shape");
-    TORCH_CHECK(w3.dim() == 2 && w3.size(0) == 256 && w3.size(1) == 64, "kvedge: w3 [256, 64]");
-    p.res = res->data_ptr();
-  }
-  const c10::DeviceGuard g(t.device());
-  p.t = t.data_ptr(); p.w2 = w2.data_ptr(); p.b2 = b2.data_ptr<float>();
-  p.w3 = w3.data_ptr(); p.b3 = b3.data_ptr<float>();
-  p.y = y.data_ptr(); p.w1 = w1.data_ptr(); p.b1 = b1.data_ptr<float>(); p.z = z.data_ptr();
-  p.nt = (int)nt; p.N = (int)N; p.H = (int)H; p.W = (int)W;
-  const int rc = kv_conv_block(&p, cur_stream(t));
-  TORCH_CHECK(rc == 0, "kvedge: conv_block failed rc=", rc);
-}
-
 // Frames-in space-to-depth stem (preprocess fused): y = act(conv2x2_s2d(frames) + bias)
 // with frames uint8 [N, 2H, 2W, 3] and w the packed [Cout, 64] s2d stem weights, already
 // scaled for raw 0..255 inputs (kvedge_amd.ops.stem_from_frames).
@@ -632,6 +582,7 @@ void batchnorm_nhwc(const at::Tensor& x, at::Tensor& y, const at::Tensor& scale,
 
 int64_t conv_num_tiles() { return kv_conv_num_tiles(); }
 int64_t nloop_sched_check() { return kv_nloop_sched_check(); }
+int64_t conv_seam_num_tiles() { return kv_conv_seam_num_tiles(); }
 int64_t set_conv_chunk_bytes(int64_t b) { return kv_set_conv_chunk_bytes(b); }
 
 }  // namespace
@@ -647,8 +598,6 @@ TORCH_LIBRARY(kvedge, m) {
         "int tile, Tensor(b!)? ws=None) -> ()");
   m.def("conv_tail(Tensor x, Tensor? x2, Tensor w, Tensor? bias, Tensor? res, Tensor(a!) y, "
         "Tensor w1, Tensor? b1, Tensor(b!) z, int stride2, int act, int tile) -> ()");
-  m.def("conv_block(Tensor t, Tensor w2, Tensor b2, Tensor w3, Tensor b3, Tensor? x2, Tensor? res, "
-        "Tensor(a!) y, Tensor w1, Tensor b1, Tensor(b!) z) -> ()");
   m.def("conv_frames_s2d(Tensor frames, Tensor w, Tensor? bias, Tensor(a!) y, int act, "
         "int tile) -> ()");
   m.def("stem_pool(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int y_coff) -> ()");
@@ -674,6 +623,7 @@ TORCH_LIBRARY(kvedge, m) {
   m.def("batchnorm_nhwc(Tensor x, Tensor(a!) y, Tensor scale, Tensor shift, bool relu) -> ()");
   m.def("conv_num_tiles() -> int", conv_num_tiles);
   m.def("nloop_sched_check() -> int", nloop_sched_check);
+  m.def("conv_seam_num_tiles() -> int", conv_seam_num_tiles);
   m.def("set_conv_chunk_bytes(int bytes) -> int", set_conv_chunk_bytes);
 }
 
@@ -685,7 +635,6 @@ TORCH_LIBRARY_IMPL(kvedge, CUDA, m) {
   m.impl("conv_frames_s2d", conv_frames_s2d);
   m.impl("conv_tail", conv_tail);
   m.impl("conv_pair", conv_pair);
-  m.impl("conv_block", conv_block);
   m.impl("sppf_pool", sppf_pool);
   m.impl("global_avgpool", global_avgpool);
   m.impl("softmax_rows", softmax_rows);

@@ -343,7 +343,14 @@ int xp_launch(const KvConvParams* p, int tile, hipStream_t stream);
 // v8 split-K (conv_glds.hip SK kernels + finalize): indices after v7
 int sk_num_tiles();
 int sk_launch(const KvConvParams* p, int tile, hipStream_t stream);
+// v9 bottleneck seam, conv3 + residual -> next conv1 (conv_seam.hip): tail calls only, tile
+// indices after the whole table above (kv_conv_num_tiles() + i)
+int seam_num_tiles();
+int seam_pick_tile(const KvConvParams* p);
+int seam_launch(const KvConvParams* p, int tile, hipStream_t stream);
 }  // namespace kvedge
+
+extern "C" int kv_conv_seam_num_tiles(void) { return kvedge::seam_num_tiles(); }
 
 extern "C" int kv_nloop_sched_check(void) { return kvedge::nloop_sched_check(); }
 
@@ -462,9 +469,19 @@ extern "C" int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream) {
 
 static int kv_conv2d_one(const KvConvParams* p, int tile, hipStream_t stream) {
   if (p->Kpad % BK != 0 || p->Cout % 8 != 0) return -1;
-  if (p->n_t) {  // fused bottleneck tail: the v3 tail tile only
+  if (p->n_t) {  // fused bottleneck tail: v3 tail tiles (Cout 256) or v9 seam tiles
     const int v3 = kNumTiles + glds_num_tiles();
-    if (tile < 0) tile = v3 + stream_tail_tile(p->n_t);
+    const int v9 = kv_conv_num_tiles();
+    if (tile < 0) {
+      if (p->Cout == 256) {
+        tile = v3 + stream_tail_tile(p->n_t);
+      } else {
+        const int s = seam_pick_tile(p);
+        if (s < 0) return -8;
+        tile = v9 + s;
+      }
+    }
+    if (tile >= v9) return seam_launch(p, tile - v9, stream);
     if (tile < v3 || tile >= v3 + stream_num_tiles()) return -8;
     return stream_launch(p, tile - v3, stream);
   }

@@ -1,0 +1,450 @@
+// v9 -- bottleneck seam: conv3 (+bias +residual, ReLU) -> next block's conv1, one launch.
+//
+// Stages 2-4 of ResNet-50 end every bottleneck with an expand conv3 (K3 = 128 / 256 / 512
+// -> Cout = 4 K3, + residual) whose output y is immediately re-read by the next block's
+// 1x1 reduce conv1 (Cout -> N1 = K3, or 2 K3 at a stage boundary).  As two launches the
+// pair moves A + R + y (write) + y (read) + z bytes and runs each half at its own
+// latency-bound rate (profiles/r3_v12_resnet50_b640_roofline.md rows 25/26: 137 + 83 us
+// per stage-3 seam at batch 640 against a 96 + 54 us HBM floor).  Fused, y never makes the
+// HBM round trip and the conv1 MFMAs overlap the conv3 memory stream.
+//
+// Structure (the v6 A-resident N-loop, conv_nloop.hip, extended):
+//  * one 8-wave workgroup per CU owns BM = 128 output rows; its A rows (BM x K3) are
+//    DMA'd into LDS once and stay resident;
+//  * it walks the T = Cout / 64 y tiles.  Tile t: 64-channel conv3 tile from A and W3
+//    (NK3 64-deep K steps), epilogue y = ReLU(acc + b3 + R(t)) in place over the residual
+//    slot, y tile stored with 16-B stores -- and the SAME LDS tile is then the A operand
+//    of a 64-deep K slice of conv1: z[BM][N1] += y_t . W1[:, 64t : 64t + 64]^T (NZ = N1/64
+//    steps of 64 z channels each).  z stays in registers (NZ x 16 floats per lane) across
+//    the whole tile walk and leaves once, ReLU(z + b1), at the end;
+//  * W3 and W1 stream through ONE ring of 8-KB stages (64 rows x 64 K, bf16): per tile NK3
+//    W3 stages then NZ W1 stages.  The weights are shared by every workgroup, so they come
+//    from L2; each workgroup reads W3 + W1 once (1 MB at stage 3);
+//  * the residual of tile t is DMA'd RD - 1 tiles ahead into an RD-slot ring.
+// Every VMEM op is an LDS DMA (kv_lds_dma16, invisible to hipcc's wait-count pass) or an
+// unconditional buffer store, so every wave issues a fixed op sequence and every wait is an
+// exact counted `s_waitcnt vmcnt(n)` from the constexpr replay SmSched below.
+//
+// MFMA v_mfma_f32_16x16x32_bf16 with the operand swap (D = W . A^T: a lane's accumulators
+// are 4 consecutive channels of one pixel); 8 waves as 4 (rows) x 2 (channel halves), each
+// a 32 x 32 sub-tile of every 128 x 64 (tile, stage) product, conv3 and conv1 alike.
+#include "common.h"
+#include "kvedge_kernels.h"
+
+namespace kvedge {
+namespace {
+
+constexpr int kSmOOB = 0x7ffffff0;  // byte offset past every operand: DMA zero-fills, store drops
+constexpr int kSmBM = 128, kSmNW = 8, kSmNT = 64 * kSmNW;
+constexpr int kSmLdsMax = 160 * 1024;
+
+template <int I>
+struct SmIC {
+  static constexpr int value = I;
+};
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void sm_static_for(F&& f) {
+  if constexpr (I < N) {
+    f(SmIC<I>{});
+    sm_static_for<N, I + 1>(f);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void sm_wait_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt field");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Per-wave VMEM issue order (every wave issues the same sequence; bias DMAs come first and
+// are older than everything waited on):
+//   prologue: A chunks (2 per 64-K chunk), R(0 .. RD-2) (2 each), B(0 .. D-2) (1 each)
+//   tile t, ring step j = 0 .. SPT-1 (s = t SPT + j):
+//     j == NK3: WAIT(R(t)) | y epilogue | y stores (2)
+//     WAIT(B(s)) | barrier | B(s + D - 1) | j == 0: R(t + RD - 1) | MFMAs
+// vmcnt counts in issue order, so "X landed" = vmcnt(#ops issued after X).  The waits are
+// computed by replaying that sequence at compile time.
+template <int NK3, int NZ, int D, int RD>
+struct SmSched {
+  static constexpr int SPT = NK3 + NZ;
+  static constexpr int kB = 1, kR = 2, kS = 2, kA = 2 * NK3;
+  static constexpr int kFar = 12;
+  static constexpr int kTiles = kFar + 2;
+  // kind 0: wait before reading ring stage s; kind 1: wait before tile t's epilogue
+  static constexpr int wait(int kind, int idx) {
+    long endB[kTiles * SPT + D + 2] = {};
+    long endR[kTiles + RD + 2] = {};
+    long pos = kA;
+    for (int t = 0; t < RD - 1; ++t) endR[t] = (pos += kR);
+    for (int s = 0; s < D - 1; ++s) endB[s] = (pos += kB);
+    for (int t = 0; t < kTiles; ++t) {
+      for (int j = 0; j < SPT; ++j) {
+        const int s = t * SPT + j;
+        if (j == NK3) {
+          if (kind == 1 && idx == t) return (int)(pos - endR[t]);
+          pos += kS;
+        }
+        if (kind == 0 && idx == s) return (int)(pos - endB[s]);
+        endB[s + D - 1] = (pos += kB);
+        if (j == 0) endR[t + RD - 1] = (pos += kR);
+      }
+    }
+    return -1;
+  }
+  static constexpr int wB(int t, int j) { return wait(0, t * SPT + j); }
+  static constexpr int wE(int t) { return wait(1, t); }
+  static constexpr int steady_from() {
+    int t0 = 0;
+    for (int t = 0; t < kFar; ++t) {
+      bool same = wE(t) == wE(kFar);
+      for (int j = 0; j < SPT; ++j) same = same && wB(t, j) == wB(kFar, j);
+      if (!same) t0 = t + 1;
+    }
+    return t0;
+  }
+  static constexpr int kSteady = steady_from();
+  static constexpr int safe_B(int j) {  // min over the warm-up tiles: never under-waits
+    int m = wB(kFar, j);
+    for (int t = 0; t <= kSteady; ++t) m = wB(t, j) < m ? wB(t, j) : m;
+    return m;
+  }
+  static constexpr int safe_E() {
+    int m = wE(kFar);
+    for (int t = 0; t <= kSteady; ++t) m = wE(t) < m ? wE(t) : m;
+    return m;
+  }
+  static constexpr bool ok() {
+    for (int t = 0; t <= kFar; ++t) {
+      if (wE(t) < 0 || wE(t) > 63) return false;
+      for (int j = 0; j < SPT; ++j)
+        if (wB(t, j) < 0 || wB(t, j) > 63) return false;
+    }
+    return kSteady < kFar;
+  }
+};
+
+__device__ __forceinline__ int sm_sw(int r) { return (r >> 1) & 7; }
+
+// Workgroup barrier for LDS hand-offs only: this wave's LDS ops retired, then s_barrier.
+// (__syncthreads()' fence may also wait for the wave's global stores, and vmcnt drains in
+// order, so it would drain every ring prefetch behind them.)
+__device__ __forceinline__ void sm_lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int NK3, int NZ, int D, int RD>
+__global__ __launch_bounds__(kSmNT, 1) void conv_seam_kernel(const KvConvParams p, int ntiles) {
+  using S = SmSched<NK3, NZ, D, RD>;
+  static_assert(S::ok(), "counted-wait schedule out of range or not periodic");
+  constexpr int SPT = S::SPT, BM = kSmBM;
+  constexpr int A_BYTES = NK3 * BM * 128, B_STAGE = 64 * 128, R_SLOT = BM * 64 * 2;
+  constexpr int B_OFF = A_BYTES, R_OFF = B_OFF + D * B_STAGE, BIAS_OFF = R_OFF + RD * R_SLOT;
+  extern __shared__ __attribute__((aligned(16))) char sm_smem[];
+  char* const lds = sm_smem;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wv >> 1, wn = wv & 1;  // 32-row block, 32-channel half of each stage
+  const int nbm = (p.M + BM - 1) / BM;
+  const int m0 = xcd_remap(blockIdx.x, nbm) * BM;
+  const int Cout = p.Cout, N1 = p.n_t;
+  // bias DMAs are 1 KB per wave-instruction, 8 KB per round over the 8 waves
+  const int b1_off = BIAS_OFF + ((Cout * 4 + 8191) / 8192) * 8192;
+
+  const kv_i32x4 rx = kv_rsrc4(p.x, p.M * p.ldx * 2);
+  const kv_i32x4 rw3 = kv_rsrc4(p.w, Cout * p.Kpad * 2);
+  const kv_i32x4 rw1 = kv_rsrc4(p.w_t, N1 * Cout * 2);
+  const kv_i32x4 rr = kv_rsrc4(p.res, p.M * p.ldr * 2);
+  const kv_i32x4 rb3 = kv_rsrc4(p.bias, Cout * 4);
+  const kv_i32x4 rb1 = kv_rsrc4(p.bias_t, N1 * 4);
+  const __amdgpu_buffer_rsrc_t ry =
+      __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, p.M * p.ldy * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rz =
+      __builtin_amdgcn_make_buffer_rsrc(p.z, (short)0, p.M * p.ldz * 2, 0x00020000);
+
+  // DMA lane roles: 8 rows x 8 chunks of 16 B per instruction; row r's logical chunk
+  // (lane & 7) ^ sw(r) lands at position lane & 7 (the read side XORs it back)
+  const int lrow = lane >> 3, pch = lane & 7;
+  int arow_off[2], r_src[2], lc8[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wv * 2 + i) * 8 + lrow;
+    const int lc = pch ^ sm_sw(row);
+    lc8[i] = lc * 8;
+    const int m = m0 + row;
+    arow_off[i] = m < p.M ? (m * p.ldx + p.x_coff + lc * 8) * 2 : kSmOOB;
+    r_src[i] = m < p.M ? (m * p.ldr + p.r_coff + lc * 8) * 2 : kSmOOB;
+  }
+  const int brow = wv * 8 + lrow, bch = (pch ^ sm_sw(brow)) * 8;  // one weight DMA per wave
+  const int w3_src = (brow * p.Kpad + bch) * 2;
+  const int w1_src = (brow * Cout + bch) * 2;
+
+  // ring stage (tile tt, step jj): jj < NK3 -> W3 rows 64 tt.., K chunk jj; else W1 rows
+  // 64 (jj - NK3).., K = y channels 64 tt..
+  auto issue_B = [&](int tt, auto JJ) __attribute__((always_inline)) {
+    constexpr int jj = decltype(JJ)::value;
+    const int s = tt * SPT + jj;
+    char* dst = lds + B_OFF + (s % D) * B_STAGE + wv * 1024;
+    if constexpr (jj < NK3) {
+      const int n = tt * 64 + brow;
+      const int v = (tt < ntiles && n < Cout) ? w3_src + (tt * 64 * p.Kpad + jj * 64) * 2 : kSmOOB;
+      kv_lds_dma16(rw3, dst, v);
+    } else {
+      const int zr = (jj - NK3) * 64 + brow;
+      const int v = (tt < ntiles && zr < N1) ? w1_src + ((jj - NK3) * 64 * Cout + tt * 64) * 2 : kSmOOB;
+      kv_lds_dma16(rw1, dst, v);
+    }
+  };
+  auto issue_R = [&](int tt) __attribute__((always_inline)) {
+    char* dst = lds + R_OFF + (tt % RD) * R_SLOT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int n = tt * 64 + lc8[i];
+      const int v = (tt < ntiles && n < Cout && r_src[i] != kSmOOB) ? r_src[i] + tt * 128 : kSmOOB;
+      kv_lds_dma16(rr, dst + (wv * 2 + i) * 1024, v);
+    }
+  };
+
+  // ---- prologue ---------------------------------------------------------------
+  for (int i = 0; i < (Cout * 4 + 8191) / 8192; ++i) {
+    const int off = (i * kSmNW + wv) * 1024;
+    kv_lds_dma16(rb3, lds + BIAS_OFF + off, off + lane * 16);
+  }
+  for (int i = 0; i < (N1 * 4 + 8191) / 8192; ++i) {
+    const int off = (i * kSmNW + wv) * 1024;
+    kv_lds_dma16(rb1, lds + b1_off + off, off + lane * 16);
+  }
+#pragma unroll
+  for (int kc = 0; kc < NK3; ++kc)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      char* dst = lds + kc * (BM * 128) + (wv * 2 + i) * 1024;
+      const int v = (arow_off[i] != kSmOOB && kc * 64 + lc8[i] < p.Cin) ? arow_off[i] + kc * 128 : kSmOOB;
+      kv_lds_dma16(rx, dst, v);
+    }
+#pragma unroll
+  for (int t = 0; t < RD - 1; ++t) issue_R(t);
+  sm_static_for<D - 1>([&](auto JJ) __attribute__((always_inline)) {
+    constexpr int s = decltype(JJ)::value;
+    issue_B(s / SPT, SmIC<s % SPT>{});
+  });
+
+  const int fr = lane & 15, fh = lane >> 4;
+  floatx4 acc[2][2];
+  floatx4 accz[NZ][2][2];
+#pragma unroll
+  for (int zc = 0; zc < NZ; ++zc)
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) accz[zc][a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // one 64-deep K step: acc[tn][tm] += Bs[wn*32 + tn*16 ..] . As[wm*32 + tm*16 ..]^T
+  auto mma64 = [&](const char* As, const char* Bs, floatx4 (&c)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int q = ks * 4 + fh;
+      bf16x8 af[2], bfg[2];
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm) {
+        const int row = wm * 32 + tm * 16 + fr;
+        af[tm] = *reinterpret_cast<const bf16x8*>(As + row * 128 + ((q ^ sm_sw(row)) << 4));
+      }
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn) {
+        const int row = wn * 32 + tn * 16 + fr;
+        bfg[tn] = *reinterpret_cast<const bf16x8*>(Bs + row * 128 + ((q ^ sm_sw(row)) << 4));
+      }
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+          c[tn][tm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[tn], af[tm], c[tn][tm], 0, 0, 0);
+    }
+  };
+
+  dispatch_act(p.act, true, [&](auto A1, auto A2) __attribute__((always_inline)) {
+    constexpr int act1 = decltype(A1)::value, act2 = decltype(A2)::value;
+    for (int t = 0; t < ntiles; ++t) {
+      const bool warm = t < S::kSteady;
+      char* Rs = lds + R_OFF + (t % RD) * R_SLOT;
+      sm_static_for<SPT>([&](auto JC) __attribute__((always_inline)) {
+        constexpr int j = decltype(JC)::value;
+        const int s = t * SPT + j;
+        if constexpr (j == NK3) {
+          // ---- y epilogue of tile t: residual slot t % RD holds R(t); y overwrites it
+          if (warm) sm_wait_vm<S::safe_E()>();
+          else sm_wait_vm<S::wE(S::kFar)>();
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+          const float* bias_t = reinterpret_cast<const float*>(lds + BIAS_OFF) + t * 64;
+#pragma unroll
+          for (int tn = 0; tn < 2; ++tn) {
+            const int c0 = wn * 32 + tn * 16 + fh * 4;
+            const float4 bv = *reinterpret_cast<const float4*>(bias_t + c0);
+#pragma unroll
+            for (int tm = 0; tm < 2; ++tm) {
+              const int row = wm * 32 + tm * 16 + fr;
+              bf16x4* ptr = reinterpret_cast<bf16x4*>(Rs + row * 128 + (((c0 >> 3) ^ sm_sw(row)) << 4) +
+                                                      (c0 & 7) * 2);
+              const bf16x4 rv = *ptr;
+              bf16x4 o;
+              o[0] = f2bf(act_c<act2>(act_c<act1>(acc[tn][tm][0] + bv.x) + (float)rv[0]));
+              o[1] = f2bf(act_c<act2>(act_c<act1>(acc[tn][tm][1] + bv.y) + (float)rv[1]));
+              o[2] = f2bf(act_c<act2>(act_c<act1>(acc[tn][tm][2] + bv.z) + (float)rv[2]));
+              o[3] = f2bf(act_c<act2>(act_c<act1>(acc[tn][tm][3] + bv.w) + (float)rv[3]));
+              *ptr = o;
+            }
+          }
+          sm_lds_barrier();
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int idx = tid + kSmNT * i;
+            const int row = idx >> 3, c = idx & 7;
+            const bf16x8 v = *reinterpret_cast<const bf16x8*>(Rs + row * 128 + ((c ^ sm_sw(row)) << 4));
+            const int m = m0 + row, n = t * 64 + c * 8;
+            const int off = (m < p.M && n < Cout) ? (m * p.ldy + p.y_coff + n) * 2 : kSmOOB;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(kv_i32x4, v), ry, off, 0, 0);
+          }
+        }
+        if constexpr (j == 0) {
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        if (warm) sm_wait_vm<S::safe_B(j)>();
+        else sm_wait_vm<S::wB(S::kFar, j)>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR: last step's reads retired
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        constexpr int jn = (j + D - 1) % SPT, tadv = (j + D - 1) / SPT;
+        issue_B(t + tadv, SmIC<jn>{});
+        if constexpr (j == 0) issue_R(t + RD - 1);
+        const char* Bs = lds + B_OFF + (s % D) * B_STAGE;
+        if constexpr (j < NK3) {
+          mma64(lds + j * (BM * 128), Bs, acc);
+        } else {
+          mma64(Rs, Bs, accz[j - NK3]);
+        }
+      });
+    }
+  });
+
+  // ---- z epilogue: ReLU(z + b1) staged through the (drained) residual slots -----------
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const float* b1 = reinterpret_cast<const float*>(lds + b1_off);
+  const bool relu_z = p.act_t == 1;
+  sm_static_for<NZ>([&](auto ZC) __attribute__((always_inline)) {
+    constexpr int zc = decltype(ZC)::value;
+    char* Zs = lds + R_OFF + (zc % RD) * R_SLOT;
+    if constexpr (zc > 0 && zc % RD == 0) __syncthreads();  // previous group's stores read it
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) {
+      const int c0 = wn * 32 + tn * 16 + fh * 4;
+      const float4 bv = *reinterpret_cast<const float4*>(b1 + zc * 64 + c0);
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm) {
+        const int row = wm * 32 + tm * 16 + fr;
+        float v0 = accz[zc][tn][tm][0] + bv.x, v1 = accz[zc][tn][tm][1] + bv.y;
+        float v2 = accz[zc][tn][tm][2] + bv.z, v3 = accz[zc][tn][tm][3] + bv.w;
+        if (relu_z) {
+          v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+        }
+        bf16x4 o;
+        o[0] = f2bf(v0); o[1] = f2bf(v1); o[2] = f2bf(v2); o[3] = f2bf(v3);
+        *reinterpret_cast<bf16x4*>(Zs + row * 128 + (((c0 >> 3) ^ sm_sw(row)) << 4) + (c0 & 7) * 2) = o;
+      }
+    }
+    if constexpr (zc % RD == RD - 1 || zc == NZ - 1) {
+      __syncthreads();
+      constexpr int z0 = zc - zc % RD;
+#pragma unroll
+      for (int g = z0; g <= zc; ++g) {
+        const char* Zg = lds + R_OFF + (g % RD) * R_SLOT;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int idx = tid + kSmNT * i;
+          const int row = idx >> 3, c = idx & 7;
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(Zg + row * 128 + ((c ^ sm_sw(row)) << 4));
+          const int m = m0 + row, n = g * 64 + c * 8;
+          const int off = (m < p.M && n < N1) ? (m * p.ldz + p.z_coff + n) * 2 : kSmOOB;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(kv_i32x4, v), rz, off, 0, 0);
+        }
+      }
+    }
+  });
+}
+
+typedef void (*SmFn)(const KvConvParams, int);
+
+struct SmTile {
+  int nk3, nz, d, rd;
+  SmFn fn;
+};
+
+template <int NK3, int NZ, int D, int RD>
+constexpr SmTile sm_tile() {
+  return SmTile{NK3, NZ, D, RD, &conv_seam_kernel<NK3, NZ, D, RD>};
+}
+
+// LDS = A (K3 x 128 x 2) + d x 8 KB ring + rd x 16 KB residual ring + bias tables.
+static const SmTile kSmTiles[] = {
+    sm_tile<2, 2, 6, 3>(),  // stage 2: K3 128, Cout 512 -> N1 128
+    sm_tile<2, 2, 4, 4>(),
+    sm_tile<2, 4, 6, 3>(),  // stage 2 -> 3: N1 256
+    sm_tile<4, 4, 5, 2>(),  // stage 3: K3 256, Cout 1024 -> N1 256
+    sm_tile<4, 4, 3, 3>(),
+    sm_tile<4, 4, 4, 3>(),
+    sm_tile<4, 8, 4, 3>(),  // stage 3 -> 4: N1 512
+};
+
+int sm_lds_bytes(const SmTile& e, int cout, int n1) {
+  return e.nk3 * kSmBM * 128 + e.d * 64 * 128 + e.rd * kSmBM * 128 +
+         ((cout * 4 + 8191) / 8192) * 8192 + ((n1 * 4 + 8191) / 8192) * 8192;
+}
+
+}  // namespace
+
+int seam_num_tiles() { return (int)(sizeof(kSmTiles) / sizeof(kSmTiles[0])); }
+
+// the first tile (table order) that takes the shape; -1 if none does
+int seam_pick_tile(const KvConvParams* p) {
+  for (int i = 0; i < seam_num_tiles(); ++i) {
+    const SmTile& e = kSmTiles[i];
+    if (p->Kpad == e.nk3 * 64 && p->n_t == e.nz * 64 && sm_lds_bytes(e, p->Cout, p->n_t) <= kSmLdsMax)
+      return i;
+  }
+  return -1;
+}
+
+int seam_launch(const KvConvParams* p, int tile, hipStream_t stream) {
+  if (tile < 0 || tile >= seam_num_tiles()) return -6;
+  const SmTile& e = kSmTiles[tile];
+  // plain conv3 + residual only (the dual conv3 + downsample form keeps too much A resident)
+  if (p->mode != 1 || !p->res || p->x2 || !p->w_t || !p->z || p->in_u8 || p->pair_1x1) return -8;
+  if (p->Kpad != e.nk3 * 64 || p->Cin > p->Kpad || p->n_t != e.nz * 64 || p->Cout % 64) return -8;
+  if (p->ldx % 8 || p->x_coff % 8 || p->ldy % 8 || p->y_coff % 8 || p->ldr % 8 || p->r_coff % 8 ||
+      p->ldz % 8 || p->z_coff % 8 || p->x_coff + p->Cin > p->ldx || p->y_coff + p->Cout > p->ldy ||
+      p->r_coff + p->Cout > p->ldr || p->z_coff + p->n_t > p->ldz)
+    return -8;
+  if ((long long)p->M * p->ldy * 2 >= kSmOOB || (long long)p->M * p->ldr * 2 >= kSmOOB ||
+      (long long)p->M * p->ldx * 2 >= kSmOOB || (long long)p->M * p->ldz * 2 >= kSmOOB ||
+      (long long)p->Cout * p->Kpad * 2 >= kSmOOB || (long long)p->n_t * p->Cout * 2 >= kSmOOB)
+    return -9;
+  const int lds = sm_lds_bytes(e, p->Cout, p->n_t);
+  if (lds > kSmLdsMax) return -11;
+  const int nbm = (p->M + kSmBM - 1) / kSmBM, ntiles = p->Cout / 64;
+  if (nbm <= 0 || ntiles <= 0) return 0;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(e.fn),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+    return -7;
+  hipLaunchKernelGGL(e.fn, dim3((unsigned)nbm), dim3(kSmNT), (unsigned)lds, stream, *p, ntiles);
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}
+
+}  // namespace kvedge

@@ -70,34 +70,13 @@ int kv_conv_num_tiles(void);
 // host replay of the v6 (conv_nloop.hip) counted-wait schedules: 0 = every tile is safe
 int kv_nloop_sched_check(void);
 int kv_conv_pick_tile(const KvConvParams* p);
+// v9 seam tiles (conv3 + residual -> next conv1, p->n_t set): valid tile arguments of a tail
+// call are kv_conv_num_tiles() + i, i < kv_conv_seam_num_tiles()
+int kv_conv_seam_num_tiles(void);
 // Fused 3x3 + 1x1 pair on the v4 direct family (p->pair_1x1 = 1, see KvConvParams): tile =
 // direct tile 0-3; < 0 when no instantiation covers the shape.
 int kv_conv_pair(const KvConvParams* p, int tile, hipStream_t stream);
 int kv_conv_pair_num_tiles(void);
-
-// Fused 64-wide bottleneck body (conv_block.hip), all NHWC bf16 at one H x W, stride 1:
-//   c2 = ReLU(conv3x3(t) + b2)                          t [N,H,W,64], w2 [64][576]
-//   y  = ReLU(c2 . W3^T + b3 + res)                     w3 [256][64], res [N,H,W,256]
-//     or ReLU([c2 | x2] . W3^T + b3)                    w3 [256][128], x2 [N,H,W,64]
-//   z  = ReLU(y . W1^T + b1)                            w1 [nt][256], z [N,H,W,nt]
-// c2 never leaves the chip; y is written once.  One image row (W <= 64) per tile.
-typedef struct KvBlockParams {
-  const void* t;
-  const void* w2;
-  const float* b2;
-  const void* w3;
-  const float* b3;
-  const void* x2;   // downsample source (dual form) or NULL
-  const void* res;  // residual (plain form) or NULL
-  void* y;
-  const void* w1;
-  const float* b1;
-  void* z;
-  int nt;           // 64 or 128
-  int N, H, W;
-} KvBlockParams;
-int kv_conv_block(const KvBlockParams* p, hipStream_t stream);
-int kv_conv_block_lds_bytes(int dual, int nt);
 
 // K5: max pool NHWC (k x k, stride, pad); C % 8 == 0.  ldx/ldy allow channel slices.
 // Fused ResNet stem (4x4 stride-1 conv over the s2d image [N,H,W,16], Cout 64, weights

@@ -139,14 +139,22 @@ class DeployedBottleneck:
         return self.c3(y, res=idt, out=out)
 
     def can_tail(self, nxt: "DeployedBottleneck") -> bool:
-        """conv3 (or the fused downsample GEMM) + the next block's conv1 as one fused tail:
-        the tail kernel holds a whole y row (Cout = 256) and both weight slices in LDS."""
+        """conv3 (or the fused downsample GEMM) + the next block's conv1 as one fused tail.
+        Stage 1 (Cout = 256): the v3 tail tile holds a whole y row and both weight slices in
+        LDS.  Stages 2-3 (plain conv3 + residual, K3 = 128 / 256): the v9 seam kernel
+        (conv_seam.hip) walks the y tiles with conv3's A resident and keeps the next conv1's
+        z in registers (ops.SEAM_SHAPES; KVEDGE_SEAM=0 turns it off for A/Bs)."""
         c1 = nxt.c1.spec
         cout = self.c3.spec.cout
+        if not (c1.kh == 1 and c1.stride == 1 and c1.pad == 0 and c1.cin == cout and
+                c1.act == ACT_RELU and self.c3.spec.act == ACT_RELU):
+            return False
+        if cout != 256:
+            k3 = self.c3.spec.cin
+            return (ops.SEAM_ENABLED and self.down is None and self.dual is None and
+                    (k3, cout, c1.cout) in ops.SEAM_SHAPES)
         k = self.c3.spec.cin + (self.dual.w.shape[1] - self.dual.k1 if self.dual is not None else 0)
-        return (cout == 256 and c1.kh == 1 and c1.stride == 1 and c1.pad == 0 and
-                c1.cin == cout and c1.cout in (64, 128) and c1.act == ACT_RELU and
-                self.c3.spec.act == ACT_RELU and (self.dual is not None or self.down is None) and
+        return (c1.cout in (64, 128) and (self.dual is not None or self.down is None) and
                 (self.dual is None or c1.cout == 64) and k <= 128)
 
     def call_tail(self, x, nxt: "DeployedBottleneck", t1=None, out=None, z=None):
@@ -161,29 +169,6 @@ class DeployedBottleneck:
                                  out=out, z=z)
         return ops.conv_tail(y, self.c3.w, self.c3.b, self.c3.spec.act, c1.w, c1.b, res=x,
                              out=out, z=z)
-
-    def can_block(self, nxt: "DeployedBottleneck") -> bool:
-        """conv2 (3x3, 64 -> 64, stride 1) + the fused tail as ONE kernel (ops.conv_block):
-        the 64-channel conv2 output never reaches HBM.  Stage 1 of ResNet-50 (the dual
-        form with a stride-1 64-channel downsample source, or the residual form)."""
-        c2 = self.c2.spec
-        if not (c2.kh == 3 and c2.stride == 1 and c2.pad == 1 and c2.cin == 64 and
-                c2.cout == 64 and c2.act == ACT_RELU and self.can_tail(nxt)):
-            return False
-        if self.dual is not None:
-            return (self.dual.stride2 == 1 and self.dual.k1 == 64 and
-                    self.dual.w.shape[1] == 128 and nxt.c1.spec.cout == 64)
-        return True
-
-    def call_block(self, x, nxt: "DeployedBottleneck", t1=None):
-        """-> (this block's output y, the next block's conv1 output z) with conv2, conv3
-        (+ residual or fused downsample) and the next conv1 in one kernel."""
-        t = self.c1(x) if t1 is None else t1
-        c1 = nxt.c1
-        if self.dual is not None:
-            return ops.conv_block(t, self.c2.w, self.c2.b, self.dual.w, self.dual.b, c1.w, c1.b,
-                                  x2=x)
-        return ops.conv_block(t, self.c2.w, self.c2.b, self.c3.w, self.c3.b, c1.w, c1.b, res=x)
 
     def out_shape(self, x_shape):
         N, H, W, _ = x_shape
@@ -247,12 +232,6 @@ class KvResNet50:
     # conv3 (+ fused downsample) and the NEXT block's conv1 as one kernel wherever the
     # tail tile fits (layer1 -> layer2 boundary included): y is never re-read from HBM
     fuse_tail: bool = True
-    # stage 1: conv2 (3x3) + the fused tail in ONE kernel (conv_block.hip): the 64-channel
-    # conv2 output is never written to HBM.  Opt-in: it moves 17-22 % fewer bytes but, with
-    # one workgroup per CU, cannot overlap its 3x3 phase with its memory phase, and measures
-    # level with or slower than direct + tail (docs/kernels.md, profiles/r2_v8_block_probe.md)
-    fuse_block: bool = False
-
     # frames-in stem: the 12-channel s2d kernel (stem12.hip, K 192, two workgroups per CU)
     # instead of the 16-channel one (stem_pool.hip, K 256)
     stem12: bool = True
@@ -303,10 +282,7 @@ class KvResNet50:
             rest = self.blocks
         for i, b in enumerate(rest):
             nxt = rest[i + 1] if i + 1 < len(rest) else None
-            if (self.fuse_block and x.is_cuda and nxt is not None and b.can_block(nxt) and
-                    ops.conv_block_fits(x)):
-                x, t1 = b.call_block(x, nxt, t1=t1)
-            elif self.fuse_tail and x.is_cuda and nxt is not None and b.can_tail(nxt):
+            if self.fuse_tail and x.is_cuda and nxt is not None and b.can_tail(nxt):
                 x, t1 = b.call_tail(x, nxt, t1=t1)
             else:
                 x, t1 = b(x, t1=t1), None

@@ -317,42 +317,10 @@ def conv_tail(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], ac
     return out, z
 
 
-def conv_block_fits(t: torch.Tensor) -> bool:
-    """Whether :func:`conv_block`'s single launch covers ``t``: one image row (W <= 64) per
-    tile, 32-bit byte offsets of the 256-channel y / residual (larger batches take the
-    two-kernel path, whose launchers split by image)."""
-    N, H, W, _ = t.shape
-    return W <= 64 and N * H * W * 256 * 2 < 0x7ffffff0
-
-
-def conv_block(t: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor, w3: torch.Tensor,
-               b3: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor,
-               res: Optional[torch.Tensor] = None, x2: Optional[torch.Tensor] = None,
-               out: Optional[torch.Tensor] = None, z: Optional[torch.Tensor] = None):
-    """Fused 64-wide bottleneck body (csrc/kernels/conv_block.hip), stride 1:
-    c2 = ReLU(conv3x3(t) + b2) -- never written to HBM --, then
-    y = ReLU(c2 . W3^T + b3 + res)   (or, with ``x2``, ReLU([c2 | x2] . W3^T + b3): the
-    fused 1x1 downsample) and z = ReLU(y . W1^T + b1), the next block's conv1.
-    t: [N,H,W,64]; w2 packed [64, 576]; w3 [256, 64] (dual: [256, 128]); w1 [n_t, 256].
-    Returns (y, z)."""
-    N, H, W, c = t.shape
-    assert c == 64 and w2.shape == (64, 576) and w3.shape[0] == 256
-    nt = w1.shape[0]
-    if out is None:
-        out = empty(N, H, W, 256, dtype=torch.bfloat16, device=t.device)
-    if z is None:
-        z = empty(N, H, W, nt, dtype=torch.bfloat16, device=t.device)
-    if t.is_cuda:
-        _native().conv_block(t, w2, b2, w3, b3, x2, res, out, w1, b1, z)
-        return out, z
-    spec2 = ConvSpec.auto(64, 64, 3, 1, 1, ACT_RELU)
-    c2 = _ref.conv2d(t, spec2, w2, b2, None, torch.empty(N, H, W, 64, dtype=torch.bfloat16), 0, 0, 0)
-    if x2 is not None:
-        _ref.conv_dual(c2, x2, w3, b3, ACT_RELU, 1, out)
-    else:
-        _ref.conv2d(c2, ConvSpec.auto(64, 256, 1, 1, 0, ACT_RELU), w3, b3, res, out, 0, 0, 0)
-    _ref.conv2d(out, ConvSpec.auto(256, nt, 1, 1, 0, ACT_RELU), w1, b1, None, z, 0, 0, 0)
-    return out, z
+# v9 bottleneck seams (csrc/kernels/conv_seam.hip) the tail path takes: (conv3 K3, conv3
+# Cout, next conv1 Cout) -- ResNet-50 stage 2, 2 -> 3, 3 and 3 -> 4
+SEAM_SHAPES = {(128, 512, 128), (128, 512, 256), (256, 1024, 256), (256, 1024, 512)}
+SEAM_ENABLED = os.environ.get("KVEDGE_SEAM", "1") != "0"
 
 
 def stem_pool(x: torch.Tensor, spec: "ConvSpec", w: torch.Tensor, bias: torch.Tensor,

@@ -150,14 +150,19 @@ def test_tile_count():
 def test_conv_every_tile(tile, case):
     N, H, W, cin, cout, k, s, p, act, res, lx, xc = case
     if DIRECT0 <= tile < XP0:
-        # the direct family takes only its instantiated shapes (a 1x1 64 -> 128 runs as two
-        # Cout slices of the 64 -> 64 form); anything else must be refused, never run wrong
-        try:
+        # the direct family takes only its instantiated shapes; of these cases exactly the
+        # 1x1 64 -> 128 from a channel slice is one (two Cout slices of the 64 -> 64 form,
+        # every direct tile).  The others must be refused (3x3 + residual before the act, no
+        # 3x3 48 -> 80 form, strided 1x1, 4x4, Cout 136 with no activation), never run wrong
+        # -- and the accepted one must not be refused
+        if (cin, cout, k, s) == (64, 128, 1, 1):
             err, scale = _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx,
                                     x_coff=xc, tile=tile)
-        except RuntimeError:
-            return
-        assert err <= 0.02 * scale, (tile, case, err, scale)
+            assert err <= 0.02 * scale, (tile, case, err, scale)
+        else:
+            with pytest.raises(RuntimeError):
+                _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
+                           tile=tile)
         return
     if STREAM0 <= tile < DIRECT0 and (k != 1 or s != 1 or not _stream_fits(tile, (cin * k * k + 63) // 64 * 64, res)):
         with pytest.raises(RuntimeError):
@@ -674,3 +679,52 @@ def test_pooled_fc(N, H, W, C, ncls, ldw):
     torch.cuda.synchronize()
     assert got.shape == ref.shape == (N, ncls)
     _assert_close(got.cpu(), ref, ("pooled_fc", N, C, ncls))
+
+
+def _seam_tiles():
+    try:
+        return int(torch.ops.kvedge.conv_seam_num_tiles()) if ops.load() else 0
+    except Exception:  # noqa: BLE001 -- collection on a box without the library
+        return 0
+
+
+@pytest.mark.parametrize("case", [
+    # (N, H, W, k3, n_t) -- conv3 K3 -> Cout = 4 K3 (+ residual) -> next conv1 n_t
+    (2, 28, 28, 128, 128),    # stage-2 seam
+    (3, 13, 11, 128, 128),    # M tail (M % 128 != 0)
+    (2, 28, 28, 128, 256),    # stage 2 -> 3 boundary
+    (2, 14, 14, 256, 256),    # stage-3 seam
+    (1, 9, 7, 256, 256),      # one partial row block
+    (2, 14, 14, 256, 512),    # stage 3 -> 4 boundary
+])
+def test_conv_seam(case):
+    """v9 seam (conv_seam.hip): y = ReLU(t . W3^T + b3 + res) and z = ReLU(y . W1^T + b1) in
+    one kernel, vs the reference composition (bf16 y in between), through every seam tile
+    that takes the shape; y and z outputs NaN-poisoned first."""
+    N, H, W, k3, nt = case
+    cout = 4 * k3
+    g = torch.Generator().manual_seed(k3 + nt + H)
+    t = _rand((N, H, W, k3), 5)
+    w = (torch.randn(cout, k3, generator=g) * (2.0 / k3) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(cout, generator=g) * 0.1
+    w1 = (torch.randn(nt, cout, generator=g) * (2.0 / cout) ** 0.5).to(torch.bfloat16)
+    b1 = torch.randn(nt, generator=g) * 0.1
+    r = _rand((N, H, W, cout), 6)
+    y_ref, z_ref = ops.conv_tail(t, w, b, ops.ACT_RELU, w1, b1, res=r)
+    base = int(torch.ops.kvedge.conv_num_tiles())
+    ran = 0
+    for st in [-1] + list(range(_seam_tiles())):
+        y = torch.full((N, H, W, cout), float("nan"), dtype=torch.bfloat16, device="cuda")
+        z = torch.full((N, H, W, nt), float("nan"), dtype=torch.bfloat16, device="cuda")
+        try:
+            ops.conv_tail(t.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, w1.cuda(), b1.cuda(),
+                          res=r.cuda(), out=y, z=z, tile=-1 if st < 0 else base + st)
+        except RuntimeError as e:
+            assert st >= 0 and ("rc=-8" in str(e) or "rc=-11" in str(e)), (st, e)
+            continue  # that tile's K3 / n_t differ from the shape
+        torch.cuda.synchronize()
+        ran += 1
+        for got, ref in ((y, y_ref), (z, z_ref)):
+            assert not torch.isnan(got.float()).any(), ("seam nan", case, st)
+            _assert_close(got.cpu(), ref, ("seam", case, st))
+    assert ran >= 2, "the default pick and at least one explicit seam tile must run"

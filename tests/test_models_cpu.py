@@ -127,25 +127,33 @@ def test_yolo_frames_in_stem_matches_preprocess_path():
     assert (fused - plain).abs().max().item() <= 0.02 * plain.abs().max().item() + 0.02
 
 
-def test_resnet_stage1_block_fusion_plumbing():
-    """The three stage-1 bottlenecks take the fused conv2 + tail kernel (ops.conv_block) on
-    the GPU; on CPU its reference composition equals the two-kernel path bit for bit."""
+def test_resnet_tail_and_seam_plumbing():
+    """Which bottleneck boundaries run fused on the GPU: the stage-1 v3 tails (blocks 0-2)
+    and the v9 seams (conv_seam.hip: plain conv3 + residual -> next conv1, stages 2-3 and
+    both stage boundaries).  The dual (downsample) blocks 3, 7, 13 and stage 4 stay
+    unfused.  On CPU every fused call equals the unfused two-conv composition bit for bit."""
     import torch
 
+    from kvedge_amd import ops
     from kvedge_amd.models.resnet import KvResNet50, init_resnet50
 
     kv = KvResNet50(init_resnet50(0, calibrate=False), "cpu")
-    fused = [i for i, b in enumerate(kv.blocks[:-1]) if b.can_block(kv.blocks[i + 1])]
-    assert fused == [0, 1, 2]
+    fused = [i for i, b in enumerate(kv.blocks[:-1]) if b.can_tail(kv.blocks[i + 1])]
+    if ops.SEAM_ENABLED:
+        assert fused == [0, 1, 2, 4, 5, 6, 8, 9, 10, 11, 12]
+    else:
+        assert fused == [0, 1, 2]
     g = torch.Generator().manual_seed(1)
-    x = torch.randn(1, 10, 9, 64, generator=g).relu().to(torch.bfloat16)
-    for i in fused:
+    for i in (4, 6, 9, 12):  # seam shapes: stage 2, 2 -> 3, stage 3, 3 -> 4
         b, nxt = kv.blocks[i], kv.blocks[i + 1]
-        y_f, z_f = b.call_block(x, nxt)
-        y_t, z_t = b.call_tail(x, nxt)
-        assert torch.equal(y_f, y_t) and torch.equal(z_f, z_t)
-        x = y_f
-
+        k3, cout = b.c3.spec.cin, b.c3.spec.cout
+        x = torch.randn(1, 3, 5, cout, generator=g).relu().to(torch.bfloat16)
+        t1 = torch.randn(1, 3, 5, k3, generator=g).relu().to(torch.bfloat16)
+        c2 = b.c2(t1)
+        y_f, z_f = b.call_tail(x, nxt, t1=t1)
+        y_u = b.c3(c2, res=x)
+        z_u = nxt.c1(y_u)
+        assert torch.equal(y_f, y_u) and torch.equal(z_f, z_u), i
 
 def test_engine_streams_cpu_and_split_check():
     from kvedge_amd.engine import _cat_outputs

@@ -127,26 +127,3 @@ def test_s2d_stem_equals_strided_conv():
         ref = F.conv2d(x4, conv.weight.detach().to(torch.bfloat16).float(), None, 2, p)
         assert y.shape == ref.permute(0, 2, 3, 1).shape
         assert (y - ref.permute(0, 2, 3, 1)).abs().max() < 0.05 * ref.abs().max() + 0.05
-
-
-def test_conv_block_reference_composes_the_three_convs():
-    """CPU path of ops.conv_block == conv2d(3x3) -> conv2d(1x1)+res -> conv2d(1x1)."""
-    import torch
-
-    from kvedge_amd import ops
-    from kvedge_amd.ops import ConvSpec
-
-    g = torch.Generator().manual_seed(0)
-    t = torch.randn(2, 6, 5, 64, generator=g).relu().to(torch.bfloat16)
-    w2 = (torch.randn(64, 576, generator=g) * 0.05).to(torch.bfloat16)
-    b2 = torch.randn(64, generator=g) * 0.1
-    w3 = (torch.randn(256, 64, generator=g) * 0.1).to(torch.bfloat16)
-    b3 = torch.randn(256, generator=g) * 0.1
-    w1 = (torch.randn(64, 256, generator=g) * 0.05).to(torch.bfloat16)
-    b1 = torch.randn(64, generator=g) * 0.1
-    res = torch.randn(2, 6, 5, 256, generator=g).to(torch.bfloat16)
-    y, z = ops.conv_block(t, w2, b2, w3, b3, w1, b1, res=res)
-    c2 = ops.conv2d(t, ConvSpec.auto(64, 64, 3, 1, 1, ops.ACT_RELU), w2, b2)
-    y2 = ops.conv2d(c2, ConvSpec.auto(64, 256, 1, 1, 0, ops.ACT_RELU), w3, b3, res=res)
-    z2 = ops.conv2d(y2, ConvSpec.auto(256, 64, 1, 1, 0, ops.ACT_RELU), w1, b1)
-    assert torch.equal(y, y2) and torch.equal(z, z2)

@@ -16,7 +16,7 @@ import argparse
 import csv
 
 
-def layers(B):
+def layers(B, seam=False):
     """[(name, kernel-name fragment, bytes, flops)] in launch order for batch B."""
     MB = 1e-6
     L = []
@@ -41,35 +41,39 @@ def layers(B):
         L.append((f"s1.b{b} tail conv3{'+down' if dual else '+res'} -> next conv1 ({nt})", "conv",
                   t(B, 56, 64) + src + t(B, 56, 256) + t(B, 56, nt),
                   gemm(m1, 64 + (64 if dual else 0), 256) + gemm(m1, 256, nt)))
-    m2 = B * 28 * 28
-    L.append(("s2.b0 conv2 3x3/2 128>128", "conv", t(B, 56, 128) + t(B, 28, 128), gemm(m2, 1152, 128)))
-    L.append(("s2.b0 conv3+down (dual) 384>512", "conv",
-              t(B, 28, 128) + t(B, 28, 256) + t(B, 28, 512), gemm(m2, 384, 512)))
-    for b in range(1, 4):
-        L.append((f"s2.b{b} conv1 512>128", "conv", t(B, 28, 512) + t(B, 28, 128), gemm(m2, 512, 128)))
-        L.append((f"s2.b{b} conv2 3x3 128>128", "conv", 2 * t(B, 28, 128), gemm(m2, 1152, 128)))
-        L.append((f"s2.b{b} conv3 128>512 +res", "conv", t(B, 28, 128) + 2 * t(B, 28, 512),
-                  gemm(m2, 128, 512)))
-    m3 = B * 14 * 14
-    L.append(("s3.b0 conv1 512>256 (28x28)", "conv", t(B, 28, 512) + t(B, 28, 256), gemm(m2, 512, 256)))
-    L.append(("s3.b0 conv2 3x3/2 256>256", "conv", t(B, 28, 256) + t(B, 14, 256), gemm(m3, 2304, 256)))
-    L.append(("s3.b0 conv3+down (dual) 768>1024", "conv",
-              t(B, 14, 256) + t(B, 14, 512) + t(B, 14, 1024), gemm(m3, 768, 1024)))
-    for b in range(1, 6):
-        L.append((f"s3.b{b} conv1 1024>256", "conv", t(B, 14, 1024) + t(B, 14, 256), gemm(m3, 1024, 256)))
-        L.append((f"s3.b{b} conv2 3x3 256>256", "conv", 2 * t(B, 14, 256), gemm(m3, 2304, 256)))
-        L.append((f"s3.b{b} conv3 256>1024 +res", "conv", t(B, 14, 256) + 2 * t(B, 14, 1024),
-                  gemm(m3, 256, 1024)))
-    m4 = B * 7 * 7
-    L.append(("s4.b0 conv1 1024>512 (14x14)", "conv", t(B, 14, 1024) + t(B, 14, 512), gemm(m3, 1024, 512)))
-    L.append(("s4.b0 conv2 3x3/2 512>512", "conv", t(B, 14, 512) + t(B, 7, 512), gemm(m4, 4608, 512)))
-    L.append(("s4.b0 conv3+down (dual) 1536>2048", "conv",
-              t(B, 7, 512) + t(B, 7, 1024) + t(B, 7, 2048), gemm(m4, 1536, 2048)))
-    for b in range(1, 3):
-        L.append((f"s4.b{b} conv1 2048>512", "conv", t(B, 7, 2048) + t(B, 7, 512), gemm(m4, 2048, 512)))
-        L.append((f"s4.b{b} conv2 3x3 512>512", "conv", 2 * t(B, 7, 512), gemm(m4, 4608, 512)))
-        L.append((f"s4.b{b} conv3 512>2048 +res", "conv", t(B, 7, 512) + 2 * t(B, 7, 2048),
-                  gemm(m4, 512, 2048)))
+    # stages 2-4; with seam=True the v9 seam kernel (conv_seam.hip) runs a plain
+    # conv3 + residual together with the NEXT block's conv1 (stages 2, 2->3, 3, 3->4)
+    seam_shapes = {(128, 512, 128), (128, 512, 256), (256, 1024, 256), (256, 1024, 512)}
+    stages = [  # (stage, hw_in, hw, width, blocks)
+        (2, 56, 28, 128, 4), (3, 28, 14, 256, 6), (4, 14, 7, 512, 3)]
+    pending_c1 = 128  # conv1 of the next block already computed (stage-1 tail, or a seam)
+    for si, (st, hwi, hw, wd, nb) in enumerate(stages):
+        m = B * hw * hw
+        cout = 4 * wd
+        for b in range(nb):
+            cin = (2 * wd if st > 2 else 256) if b == 0 else cout
+            hin = hwi if b == 0 else hw
+            if pending_c1 is None:
+                L.append((f"s{st}.b{b} conv1 {cin}>{wd}" + (f" ({hin}x{hin})" if b == 0 and st > 2 else ""),
+                          "conv", t(B, hin, cin) + t(B, hin, wd), gemm(B * hin * hin, cin, wd)))
+            pending_c1 = None
+            if b == 0:
+                L.append((f"s{st}.b0 conv2 3x3/2 {wd}>{wd}", "conv", t(B, hin, wd) + t(B, hw, wd),
+                          gemm(m, 9 * wd, wd)))
+                L.append((f"s{st}.b0 conv3+down (dual) {wd + cin}>{cout}", "conv",
+                          t(B, hw, wd) + t(B, hw, cin) + t(B, hw, cout), gemm(m, wd + cin, cout)))
+                continue
+            L.append((f"s{st}.b{b} conv2 3x3 {wd}>{wd}", "conv", 2 * t(B, hw, wd), gemm(m, 9 * wd, wd)))
+            last = b == nb - 1
+            nt = (2 * wd if st < 4 else None) if last else wd
+            if seam and nt is not None and (wd, cout, nt) in seam_shapes:
+                L.append((f"s{st}.b{b} seam conv3+res -> next conv1 ({nt})", "seam",
+                          t(B, hw, wd) + 2 * t(B, hw, cout) + t(B, hw, nt),
+                          gemm(m, wd, cout) + gemm(m, cout, nt)))
+                pending_c1 = nt
+            else:
+                L.append((f"s{st}.b{b} conv3 {wd}>{cout} +res", "conv", t(B, hw, wd) + 2 * t(B, hw, cout),
+                          gemm(m, wd, cout)))
     L.append(("global avgpool", "avgpool", t(B, 7, 2048) + B * 2048 * 2, 0))
     L.append(("fc 2048>1000", "conv", B * 2048 * 2 + B * 1000 * 2 + 2048 * 1000 * 2,
               gemm(B, 2048, 1000)))
@@ -84,10 +88,13 @@ def main():
     ap.add_argument("--batch", type=int, default=640)
     ap.add_argument("--hbm", type=float, default=6.0, help="HBM floor, TB/s")
     ap.add_argument("--peak", type=float, default=2.5, help="dense bf16 MFMA floor, PF/s")
+    ap.add_argument("--seam", type=int, default=None,
+                    help="1/0: the trace does / does not use the v9 seam kernel (default: detect)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    L = layers(a.batch)
+    seam = a.seam if a.seam is not None else any("seam" in r["Kernel_Name"] for r in rows)
+    L = layers(a.batch, seam)
     # the step-counter bump is its own launch only in traces older than the in-kernel bump
     if not any("bump_kernel" in r["Kernel_Name"] for r in rows):
         L = [x for x in L if x[1] != "bump"]
@@ -104,7 +111,7 @@ def main():
     tot_us = tot_floor = tot_b = tot_f = 0.0
     for i, ((name, frag, byts, flops), r) in enumerate(zip(L, step)):
         kn = r["Kernel_Name"].replace("void ", "").replace("kvedge::(anonymous namespace)::", "")
-        assert frag in kn or frag == "conv" and "conv" in kn, (i, name, kn[:60])
+        assert frag in kn or frag == "conv" and "conv" in kn and "seam" not in kn, (i, name, kn[:60])
         us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         floor = max(byts / (a.hbm * 1e12), flops / (a.peak * 1e15)) * 1e6
         tot_us += us
