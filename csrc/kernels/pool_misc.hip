@@ -176,31 +176,47 @@ __global__ __launch_bounds__(kBlock) void avgpool_kernel(const bf16* __restrict_
 // ---- K6+K1 fused head for edge batches: logits = fc(global_avgpool(x)) -----------------
 // At batch 1-16 the classifier is a GEMV (K = 2048, N = 1000): as a tiled GEMM it was a
 // 16-32-workgroup launch walking 32 K steps (~13 us), after a separate pooling launch.  Here
-// workgroup (column block, image) pools the image's C channels into LDS (rounded to bf16, as
-// the pooling kernel stores them), then each wave dots 8 weight rows with it: 16-B weight
-// loads, a wave reduction per column.  One launch, weights read once per image.
-__global__ __launch_bounds__(256) void pooled_fc_kernel(const bf16* __restrict__ x, int HW, int C,
-                                                        const bf16* __restrict__ w, int ldw,
-                                                        const float* __restrict__ bias,
-                                                        bf16* __restrict__ y, int ncls) {
-  extern __shared__ float pooled[];  // C values
+// workgroup (column block of 64, image) pools the image's C channels into LDS (rounded to
+// bf16, as the pooling kernel stores them), then each of its 8 waves dots 8 weight rows with
+// it: 16-B weight loads, a wave reduction per column.  One launch, weights read once per
+// image.  Every column block needs the whole pooled vector, so the image is pooled once per
+// block: 16 blocks at ncls = 1000 (was 32 with 32-column blocks), each splitting
+// the HW pixels of a channel chunk over kPfSplit threads so the pooling pass is
+// ceil(HW / kPfSplit) loads deep instead of HW.
+constexpr int kPfThreads = 512, kPfCols = 64;
+__global__ __launch_bounds__(kPfThreads) void pooled_fc_kernel(const bf16* __restrict__ x, int HW,
+                                                               int C, const bf16* __restrict__ w,
+                                                               int ldw, const float* __restrict__ bias,
+                                                               bf16* __restrict__ y, int ncls,
+                                                               int split) {
+  extern __shared__ float pf_smem[];  // [split][C] partial sums, then [C] pooled (slot 0)
   const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const bf16* xb = x + (size_t)b * HW * C;
-  const float inv = 1.0f / (float)HW;
-  for (int c8 = tid; c8 < C / 8; c8 += 256) {
+  const int C8 = C / 8;
+  for (int it = tid; it < C8 * split; it += kPfThreads) {
+    const int c8 = it % C8, part = it / C8;
     float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll 7
-    for (int q = 0; q < HW; ++q) {
+#pragma unroll 4
+    for (int q = part; q < HW; q += split) {
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(xb + (size_t)q * C + c8 * 8);
 #pragma unroll
       for (int e = 0; e < 8; ++e) s[e] += (float)v[e];
     }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) pooled[c8 * 8 + e] = (float)f2bf(s[e] * inv);
+    float4* dst = reinterpret_cast<float4*>(pf_smem + part * C + c8 * 8);
+    dst[0] = make_float4(s[0], s[1], s[2], s[3]);
+    dst[1] = make_float4(s[4], s[5], s[6], s[7]);
   }
   __syncthreads();
-  for (int j = 0; j < 8; ++j) {
-    const int n = blockIdx.x * 32 + wv * 8 + j;  // wave-uniform
+  const float inv = 1.0f / (float)HW;
+  for (int c = tid; c < C; c += kPfThreads) {
+    float t = pf_smem[c];
+    for (int part = 1; part < split; ++part) t += pf_smem[part * C + c];
+    pf_smem[c] = (float)f2bf(t * inv);
+  }
+  __syncthreads();
+  const float* pooled = pf_smem;
+  for (int j = 0; j < kPfCols / 8; ++j) {
+    const int n = blockIdx.x * kPfCols + wv * 8 + j;  // wave-uniform
     if (n >= ncls) break;
     const bf16* wr = w + (size_t)n * ldw;
     float acc = 0.f;
@@ -486,9 +502,13 @@ extern "C" int kv_global_avgpool(const void* x, void* y, int N, int HW, int C, h
 extern "C" int kv_pooled_fc(const void* x, int N, int HW, int C, const void* w, int ldw,
                             const float* bias, void* y, int ncls, hipStream_t s) {
   if (N <= 0 || C % 8 || ldw < C || ldw % 8 || C > 16384) return -1;
-  hipLaunchKernelGGL(pooled_fc_kernel, dim3((unsigned)((ncls + 31) / 32), (unsigned)N), dim3(256),
-                     (unsigned)(C * sizeof(float)), s, (const bf16*)x, HW, C, (const bf16*)w, ldw,
-                     bias, (bf16*)y, ncls);
+  // pixel split of the pooling pass: enough (channel chunk, part) items for the 512 threads,
+  // while the [split][C] fp32 partials fit in 64 KB of LDS
+  int split = 1;
+  while (split < 8 && (C / 8) * split < kPfThreads && (split * 2) * C * 4 <= 65536) split *= 2;
+  hipLaunchKernelGGL(pooled_fc_kernel, dim3((unsigned)((ncls + kPfCols - 1) / kPfCols), (unsigned)N),
+                     dim3(kPfThreads), (unsigned)(split * C * sizeof(float)), s, (const bf16*)x, HW,
+                     C, (const bf16*)w, ldw, bias, (bf16*)y, ncls, split);
   KV_CHECK_LAUNCH();
 }
 

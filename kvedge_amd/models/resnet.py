@@ -157,6 +157,16 @@ class DeployedBottleneck:
         return (c1.cout in (64, 128) and (self.dual is not None or self.down is None) and
                 (self.dual is None or c1.cout == 64) and k <= 128)
 
+    def tail_fits(self, x: torch.Tensor) -> bool:
+        """Batch-size gate of the fused boundary for input ``x``: the v9 seam gives each
+        8-wave workgroup 128 rows and walks every y tile in it, so it only pays when the
+        layer has rows for a workgroup on every CU (ops.SEAM_MIN_WGS); edge batches keep
+        the split-K conv3 and conv1 launches.  The stage-1 tail has no such limit."""
+        if self.c3.spec.cout == 256:
+            return True
+        N, Ho, Wo, _ = self.out_shape(x.shape)
+        return (N * Ho * Wo + 127) // 128 >= ops.SEAM_MIN_WGS
+
     def call_tail(self, x, nxt: "DeployedBottleneck", t1=None, out=None, z=None):
         """-> (this block's output y, the next block's conv1 output z) in one fused pass.
         ``out``/``z``: preallocated destinations (micro-batch slices of full-batch tensors)."""
@@ -282,7 +292,8 @@ class KvResNet50:
             rest = self.blocks
         for i, b in enumerate(rest):
             nxt = rest[i + 1] if i + 1 < len(rest) else None
-            if self.fuse_tail and x.is_cuda and nxt is not None and b.can_tail(nxt):
+            if (self.fuse_tail and x.is_cuda and nxt is not None and b.can_tail(nxt) and
+                    b.tail_fits(x)):
                 x, t1 = b.call_tail(x, nxt, t1=t1)
             else:
                 x, t1 = b(x, t1=t1), None

@@ -321,6 +321,8 @@ def conv_tail(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], ac
 # Cout, next conv1 Cout) -- ResNet-50 stage 2, 2 -> 3, 3 and 3 -> 4
 SEAM_SHAPES = {(128, 512, 128), (128, 512, 256), (256, 1024, 256), (256, 1024, 512)}
 SEAM_ENABLED = os.environ.get("KVEDGE_SEAM", "1") != "0"
+# ... only when the layer gives every CU a 128-row workgroup (edge batches: split-K instead)
+SEAM_MIN_WGS = int(os.environ.get("KVEDGE_SEAM_MIN_WGS", "256"))
 
 
 def stem_pool(x: torch.Tensor, spec: "ConvSpec", w: torch.Tensor, bias: torch.Tensor,
