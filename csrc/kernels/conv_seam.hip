@@ -35,7 +35,6 @@ namespace kvedge {
 namespace {
 
 constexpr int kSmOOB = 0x7ffffff0;  // byte offset past every operand: DMA zero-fills, store drops
-constexpr int kSmBM = 128, kSmNW = 8, kSmNT = 64 * kSmNW;
 constexpr int kSmLdsMax = 160 * 1024;
 
 template <int I>
@@ -58,16 +57,16 @@ __device__ __forceinline__ void sm_wait_vm() {
 
 // Per-wave VMEM issue order (every wave issues the same sequence; bias DMAs come first and
 // are older than everything waited on):
-//   prologue: A chunks (2 per 64-K chunk), R(0 .. RD-2) (2 each), B(0 .. D-2) (1 each)
-//   tile t, ring step j = 0 .. SPT-1 (s = t SPT + j):
-//     j == NK3: WAIT(R(t)) | y epilogue | y stores (2)
+//   prologue: A chunks (2 per 64-K chunk), R(0 .. RD-2) (2 each), B(0 .. D-2) (kB each)
+//   tile t, ring step j = 0 .. SPT-1 (s = t SPT + j; SY conv3 steps, then SZ conv1 steps):
+//     j == SY: WAIT(R(t)) | y epilogue | y stores (2)
 //     WAIT(B(s)) | barrier | B(s + D - 1) | j == 0: R(t + RD - 1) | MFMAs
 // vmcnt counts in issue order, so "X landed" = vmcnt(#ops issued after X).  The waits are
 // computed by replaying that sequence at compile time.
-template <int NK3, int NZ, int D, int RD>
+template <int SY, int SZ, int D, int RD, int KB, int NC3>
 struct SmSched {
-  static constexpr int SPT = NK3 + NZ;
-  static constexpr int kB = 1, kR = 2, kS = 2, kA = 2 * NK3;
+  static constexpr int SPT = SY + SZ;
+  static constexpr int kB = KB, kR = 2, kS = 2, kA = 2 * NC3;
   static constexpr int kFar = 12;
   static constexpr int kTiles = kFar + 2;
   // kind 0: wait before reading ring stage s; kind 1: wait before tile t's epilogue
@@ -80,7 +79,7 @@ struct SmSched {
     for (int t = 0; t < kTiles; ++t) {
       for (int j = 0; j < SPT; ++j) {
         const int s = t * SPT + j;
-        if (j == NK3) {
+        if (j == SY) {
           if (kind == 1 && idx == t) return (int)(pos - endR[t]);
           pos += kS;
         }
@@ -134,24 +133,32 @@ __device__ __forceinline__ void sm_lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int NK3, int NZ, int D, int RD>
-__global__ __launch_bounds__(kSmNT, 1) void conv_seam_kernel(const KvConvParams p, int ntiles) {
-  using S = SmSched<NK3, NZ, D, RD>;
+// NC3 / NZC: 64-wide chunks of K3 (conv3's K) / of N1 (conv1's output channels).
+// NW waves (BM = 16 NW rows, (NW / 2) x 2 waves of 32 x 32); KS2 64-chunks per ring stage
+// (2 = 16-KB stages: half the waits and barriers per MFMA).  NW = 4 tiles fit 80 KB of LDS,
+// so two workgroups share a CU and one's ring waits hide under the other's MFMAs.
+template <int NC3, int NZC, int D, int RD, int NW = 8, int KS2 = 1>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(const KvConvParams p, int ntiles) {
+  static_assert(NW == 4 || NW == 8, "waves");
+  static_assert(NC3 % KS2 == 0 && NZC % KS2 == 0, "whole chunks per ring stage");
+  constexpr int SY = NC3 / KS2, SZ = NZC / KS2, BPW = 8 / NW;  // BPW: DMAs per wave per chunk
+  using S = SmSched<SY, SZ, D, RD, KS2 * BPW, NC3>;
   static_assert(S::ok(), "counted-wait schedule out of range or not periodic");
-  constexpr int SPT = S::SPT, BM = kSmBM;
-  constexpr int A_BYTES = NK3 * BM * 128, B_STAGE = 64 * 128, R_SLOT = BM * 64 * 2;
+  constexpr int SPT = S::SPT, BM = 16 * NW, NT = 64 * NW;
+  constexpr int A_BYTES = NC3 * BM * 128, B_CHUNK = 64 * 128, B_STAGE = KS2 * B_CHUNK;
+  constexpr int R_SLOT = BM * 64 * 2;
   constexpr int B_OFF = A_BYTES, R_OFF = B_OFF + D * B_STAGE, BIAS_OFF = R_OFF + RD * R_SLOT;
+  constexpr int BIAS_ROUND = NW * 1024;  // bias DMAs: 1 KB per wave-instruction
   extern __shared__ __attribute__((aligned(16))) char sm_smem[];
   char* const lds = sm_smem;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wv >> 1, wn = wv & 1;  // 32-row block, 32-channel half of each stage
+  const int wm = wv >> 1, wn = wv & 1;  // 32-row block, 32-channel half of each chunk
   const int nbm = (p.M + BM - 1) / BM;
   const int m0 = xcd_remap(blockIdx.x, nbm) * BM;
   const int Cout = p.Cout, N1 = p.n_t;
-  // bias DMAs are 1 KB per wave-instruction, 8 KB per round over the 8 waves
-  const int b1_off = BIAS_OFF + ((Cout * 4 + 8191) / 8192) * 8192;
+  const int b1_off = BIAS_OFF + ((Cout * 4 + BIAS_ROUND - 1) / BIAS_ROUND) * BIAS_ROUND;
 
   const kv_i32x4 rx = kv_rsrc4(p.x, p.M * p.ldx * 2);
   const kv_i32x4 rw3 = kv_rsrc4(p.w, Cout * p.Kpad * 2);
@@ -177,25 +184,37 @@ __global__ __launch_bounds__(kSmNT, 1) void conv_seam_kernel(const KvConvParams 
     arow_off[i] = m < p.M ? (m * p.ldx + p.x_coff + lc * 8) * 2 : kSmOOB;
     r_src[i] = m < p.M ? (m * p.ldr + p.r_coff + lc * 8) * 2 : kSmOOB;
   }
-  const int brow = wv * 8 + lrow, bch = (pch ^ sm_sw(brow)) * 8;  // one weight DMA per wave
-  const int w3_src = (brow * p.Kpad + bch) * 2;
-  const int w1_src = (brow * Cout + bch) * 2;
+  int w3_src[BPW], w1_src[BPW], brow[BPW];
+#pragma unroll
+  for (int i = 0; i < BPW; ++i) {
+    brow[i] = (wv * BPW + i) * 8 + lrow;
+    const int bch = (pch ^ sm_sw(brow[i])) * 8;
+    w3_src[i] = (brow[i] * p.Kpad + bch) * 2;
+    w1_src[i] = (brow[i] * Cout + bch) * 2;
+  }
 
-  // ring stage (tile tt, step jj): jj < NK3 -> W3 rows 64 tt.., K chunk jj; else W1 rows
-  // 64 (jj - NK3).., K = y channels 64 tt..
+  // ring stage (tile tt, step jj): jj < SY -> W3 rows 64 tt.., K chunks jj KS2 ..; else W1
+  // rows 64 ((jj - SY) KS2 + c).., K = y channels 64 tt..
   auto issue_B = [&](int tt, auto JJ) __attribute__((always_inline)) {
     constexpr int jj = decltype(JJ)::value;
     const int s = tt * SPT + jj;
-    char* dst = lds + B_OFF + (s % D) * B_STAGE + wv * 1024;
-    if constexpr (jj < NK3) {
-      const int n = tt * 64 + brow;
-      const int v = (tt < ntiles && n < Cout) ? w3_src + (tt * 64 * p.Kpad + jj * 64) * 2 : kSmOOB;
-      kv_lds_dma16(rw3, dst, v);
-    } else {
-      const int zr = (jj - NK3) * 64 + brow;
-      const int v = (tt < ntiles && zr < N1) ? w1_src + ((jj - NK3) * 64 * Cout + tt * 64) * 2 : kSmOOB;
-      kv_lds_dma16(rw1, dst, v);
-    }
+    char* dst = lds + B_OFF + (s % D) * B_STAGE;
+#pragma unroll
+    for (int c = 0; c < KS2; ++c)
+#pragma unroll
+      for (int i = 0; i < BPW; ++i) {
+        char* d = dst + c * B_CHUNK + (wv * BPW + i) * 1024;
+        if constexpr (jj < SY) {
+          const int n = tt * 64 + brow[i];
+          const int v = (tt < ntiles && n < Cout) ? w3_src[i] + (tt * 64 * p.Kpad + (jj * KS2 + c) * 64) * 2 : kSmOOB;
+          kv_lds_dma16(rw3, d, v);
+        } else {
+          const int zc = (jj - SY) * KS2 + c;
+          const int zr = zc * 64 + brow[i];
+          const int v = (tt < ntiles && zr < N1) ? w1_src[i] + (zc * 64 * Cout + tt * 64) * 2 : kSmOOB;
+          kv_lds_dma16(rw1, d, v);
+        }
+      }
   };
   auto issue_R = [&](int tt) __attribute__((always_inline)) {
     char* dst = lds + R_OFF + (tt % RD) * R_SLOT;
@@ -208,16 +227,16 @@ __global__ __launch_bounds__(kSmNT, 1) void conv_seam_kernel(const KvConvParams 
   };
 
   // ---- prologue ---------------------------------------------------------------
-  for (int i = 0; i < (Cout * 4 + 8191) / 8192; ++i) {
-    const int off = (i * kSmNW + wv) * 1024;
+  for (int i = 0; i < (Cout * 4 + BIAS_ROUND - 1) / BIAS_ROUND; ++i) {
+    const int off = (i * NW + wv) * 1024;
     kv_lds_dma16(rb3, lds + BIAS_OFF + off, off + lane * 16);
   }
-  for (int i = 0; i < (N1 * 4 + 8191) / 8192; ++i) {
-    const int off = (i * kSmNW + wv) * 1024;
+  for (int i = 0; i < (N1 * 4 + BIAS_ROUND - 1) / BIAS_ROUND; ++i) {
+    const int off = (i * NW + wv) * 1024;
     kv_lds_dma16(rb1, lds + b1_off + off, off + lane * 16);
   }
 #pragma unroll
-  for (int kc = 0; kc < NK3; ++kc)
+  for (int kc = 0; kc < NC3; ++kc)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       char* dst = lds + kc * (BM * 128) + (wv * 2 + i) * 1024;
@@ -233,15 +252,15 @@ __global__ __launch_bounds__(kSmNT, 1) void conv_seam_kernel(const KvConvParams 
 
   const int fr = lane & 15, fh = lane >> 4;
   floatx4 acc[2][2];
-  floatx4 accz[NZ][2][2];
+  floatx4 accz[NZC][2][2];
 #pragma unroll
-  for (int zc = 0; zc < NZ; ++zc)
+  for (int zc = 0; zc < NZC; ++zc)
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b) accz[zc][a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // one 64-deep K step: acc[tn][tm] += Bs[wn*32 + tn*16 ..] . As[wm*32 + tm*16 ..]^T
+  // one 64-deep K chunk: acc[tn][tm] += Bs[wn*32 + tn*16 ..] . As[wm*32 + tm*16 ..]^T
   auto mma64 = [&](const char* As, const char* Bs, floatx4 (&c)[2][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -273,13 +292,11 @@ __global__ __launch_bounds__(kSmNT, 1) void conv_seam_kernel(const KvConvParams 
       sm_static_for<SPT>([&](auto JC) __attribute__((always_inline)) {
         constexpr int j = decltype(JC)::value;
         const int s = t * SPT + j;
-        if constexpr (j == NK3) {
+        if constexpr (j == SY) {
           // ---- y epilogue of tile t: residual slot t % RD holds R(t); y overwrites it
           if (warm) sm_wait_vm<S::safe_E()>();
           else sm_wait_vm<S::wE(S::kFar)>();
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-          asm volatile("" ::: "memory");
+          sm_lds_barrier();
           const float* bias_t = reinterpret_cast<const float*>(lds + BIAS_OFF) + t * 64;
 #pragma unroll
           for (int tn = 0; tn < 2; ++tn) {
@@ -302,7 +319,7 @@ __global__ __launch_bounds__(kSmNT, 1) void conv_seam_kernel(const KvConvParams 
           sm_lds_barrier();
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
-            const int idx = tid + kSmNT * i;
+            const int idx = tid + NT * i;
             const int row = idx >> 3, c = idx & 7;
             const bf16x8 v = *reinterpret_cast<const bf16x8*>(Rs + row * 128 + ((c ^ sm_sw(row)) << 4));
             const int m = m0 + row, n = t * 64 + c * 8;
@@ -318,17 +335,15 @@ __global__ __launch_bounds__(kSmNT, 1) void conv_seam_kernel(const KvConvParams 
         }
         if (warm) sm_wait_vm<S::safe_B(j)>();
         else sm_wait_vm<S::wB(S::kFar, j)>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // WAR: last step's reads retired
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
+        sm_lds_barrier();  // WAR: every wave's reads of the slot about to be refilled retired
         constexpr int jn = (j + D - 1) % SPT, tadv = (j + D - 1) / SPT;
         issue_B(t + tadv, SmIC<jn>{});
         if constexpr (j == 0) issue_R(t + RD - 1);
         const char* Bs = lds + B_OFF + (s % D) * B_STAGE;
-        if constexpr (j < NK3) {
-          mma64(lds + j * (BM * 128), Bs, acc);
-        } else {
-          mma64(Rs, Bs, accz[j - NK3]);
+#pragma unroll
+        for (int c = 0; c < KS2; ++c) {
+          if constexpr (j < SY) mma64(lds + (j * KS2 + c) * (BM * 128), Bs + c * B_CHUNK, acc);
+          else mma64(Rs, Bs + c * B_CHUNK, accz[(j - SY) * KS2 + c]);
         }
       });
     }
@@ -339,7 +354,7 @@ __global__ __launch_bounds__(kSmNT, 1) void conv_seam_kernel(const KvConvParams 
   __syncthreads();
   const float* b1 = reinterpret_cast<const float*>(lds + b1_off);
   const bool relu_z = p.act_t == 1;
-  sm_static_for<NZ>([&](auto ZC) __attribute__((always_inline)) {
+  sm_static_for<NZC>([&](auto ZC) __attribute__((always_inline)) {
     constexpr int zc = decltype(ZC)::value;
     char* Zs = lds + R_OFF + (zc % RD) * R_SLOT;
     if constexpr (zc > 0 && zc % RD == 0) __syncthreads();  // previous group's stores read it
@@ -360,7 +375,7 @@ __global__ __launch_bounds__(kSmNT, 1) void conv_seam_kernel(const KvConvParams 
         *reinterpret_cast<bf16x4*>(Zs + row * 128 + (((c0 >> 3) ^ sm_sw(row)) << 4) + (c0 & 7) * 2) = o;
       }
     }
-    if constexpr (zc % RD == RD - 1 || zc == NZ - 1) {
+    if constexpr (zc % RD == RD - 1 || zc == NZC - 1) {
       __syncthreads();
       constexpr int z0 = zc - zc % RD;
 #pragma unroll
@@ -368,7 +383,7 @@ __global__ __launch_bounds__(kSmNT, 1) void conv_seam_kernel(const KvConvParams 
         const char* Zg = lds + R_OFF + (g % RD) * R_SLOT;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const int idx = tid + kSmNT * i;
+          const int idx = tid + NT * i;
           const int row = idx >> 3, c = idx & 7;
           const bf16x8 v = *reinterpret_cast<const bf16x8*>(Zg + row * 128 + ((c ^ sm_sw(row)) << 4));
           const int m = m0 + row, n = g * 64 + c * 8;
@@ -383,29 +398,34 @@ __global__ __launch_bounds__(kSmNT, 1) void conv_seam_kernel(const KvConvParams 
 typedef void (*SmFn)(const KvConvParams, int);
 
 struct SmTile {
-  int nk3, nz, d, rd;
+  int nc3, nzc, d, rd, nw, ks2;
   SmFn fn;
 };
 
-template <int NK3, int NZ, int D, int RD>
+template <int NC3, int NZC, int D, int RD, int NW = 8, int KS2 = 1>
 constexpr SmTile sm_tile() {
-  return SmTile{NK3, NZ, D, RD, &conv_seam_kernel<NK3, NZ, D, RD>};
+  return SmTile{NC3, NZC, D, RD, NW, KS2, &conv_seam_kernel<NC3, NZC, D, RD, NW, KS2>};
 }
 
-// LDS = A (K3 x 128 x 2) + d x 8 KB ring + rd x 16 KB residual ring + bias tables.
+// LDS = A (K3 x BM x 2) + d x ks2 x 8 KB ring + rd x BM x 128 B residual ring + bias tables.
+// Batch 640, same box (profiles/r4_seam_probe.md): the 8-wave 8-KB-stage forms
+// run ~0.44 us per ring step, latency-bound on the one shared weight ring; the 4-wave forms
+// put two workgroups on a CU, the KS2 = 2 forms halve the waits and barriers per MFMA.
 static const SmTile kSmTiles[] = {
-    sm_tile<2, 2, 6, 3>(),  // stage 2: K3 128, Cout 512 -> N1 128
-    sm_tile<2, 2, 4, 4>(),
-    sm_tile<2, 4, 6, 3>(),  // stage 2 -> 3: N1 256
-    sm_tile<4, 4, 5, 2>(),  // stage 3: K3 256, Cout 1024 -> N1 256
-    sm_tile<4, 4, 3, 3>(),
-    sm_tile<4, 4, 4, 3>(),
-    sm_tile<4, 8, 4, 3>(),  // stage 3 -> 4: N1 512
+    sm_tile<2, 2, 6, 3>(),        // stage 2: K3 128, Cout 512 -> N1 128
+    sm_tile<2, 2, 4, 3, 4>(),     //   4 waves, 2 workgroups per CU (80 KB)
+    sm_tile<2, 2, 4, 3, 8, 2>(),  //   16-KB stages
+    sm_tile<2, 4, 6, 3>(),        // stage 2 -> 3: N1 256
+    sm_tile<4, 4, 5, 2>(),        // stage 3: K3 256, Cout 1024 -> N1 256
+    sm_tile<4, 4, 3, 2, 4>(),     //   4 waves, 2 workgroups per CU (80 KB)
+    sm_tile<4, 4, 3, 2, 8, 2>(),  //   16-KB stages
+    sm_tile<4, 8, 4, 3>(),        // stage 3 -> 4: N1 512
 };
 
 int sm_lds_bytes(const SmTile& e, int cout, int n1) {
-  return e.nk3 * kSmBM * 128 + e.d * 64 * 128 + e.rd * kSmBM * 128 +
-         ((cout * 4 + 8191) / 8192) * 8192 + ((n1 * 4 + 8191) / 8192) * 8192;
+  const int bm = 16 * e.nw, round = e.nw * 1024;
+  return e.nc3 * bm * 128 + e.d * e.ks2 * 64 * 128 + e.rd * bm * 128 +
+         ((cout * 4 + round - 1) / round) * round + ((n1 * 4 + round - 1) / round) * round;
 }
 
 }  // namespace
@@ -416,7 +436,7 @@ int seam_num_tiles() { return (int)(sizeof(kSmTiles) / sizeof(kSmTiles[0])); }
 int seam_pick_tile(const KvConvParams* p) {
   for (int i = 0; i < seam_num_tiles(); ++i) {
     const SmTile& e = kSmTiles[i];
-    if (p->Kpad == e.nk3 * 64 && p->n_t == e.nz * 64 && sm_lds_bytes(e, p->Cout, p->n_t) <= kSmLdsMax)
+    if (p->Kpad == e.nc3 * 64 && p->n_t == e.nzc * 64 && sm_lds_bytes(e, p->Cout, p->n_t) <= kSmLdsMax)
       return i;
   }
   return -1;
@@ -427,7 +447,7 @@ int seam_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   const SmTile& e = kSmTiles[tile];
   // plain conv3 + residual only (the dual conv3 + downsample form keeps too much A resident)
   if (p->mode != 1 || !p->res || p->x2 || !p->w_t || !p->z || p->in_u8 || p->pair_1x1) return -8;
-  if (p->Kpad != e.nk3 * 64 || p->Cin > p->Kpad || p->n_t != e.nz * 64 || p->Cout % 64) return -8;
+  if (p->Kpad != e.nc3 * 64 || p->Cin > p->Kpad || p->n_t != e.nzc * 64 || p->Cout % 64) return -8;
   if (p->ldx % 8 || p->x_coff % 8 || p->ldy % 8 || p->y_coff % 8 || p->ldr % 8 || p->r_coff % 8 ||
       p->ldz % 8 || p->z_coff % 8 || p->x_coff + p->Cin > p->ldx || p->y_coff + p->Cout > p->ldy ||
       p->r_coff + p->Cout > p->ldr || p->z_coff + p->n_t > p->ldz)
@@ -438,12 +458,12 @@ int seam_launch(const KvConvParams* p, int tile, hipStream_t stream) {
     return -9;
   const int lds = sm_lds_bytes(e, p->Cout, p->n_t);
   if (lds > kSmLdsMax) return -11;
-  const int nbm = (p->M + kSmBM - 1) / kSmBM, ntiles = p->Cout / 64;
+  const int nbm = (p->M + 16 * e.nw - 1) / (16 * e.nw), ntiles = p->Cout / 64;
   if (nbm <= 0 || ntiles <= 0) return 0;
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(e.fn),
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
     return -7;
-  hipLaunchKernelGGL(e.fn, dim3((unsigned)nbm), dim3(kSmNT), (unsigned)lds, stream, *p, ntiles);
+  hipLaunchKernelGGL(e.fn, dim3((unsigned)nbm), dim3(64 * e.nw), (unsigned)lds, stream, *p, ntiles);
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }
 

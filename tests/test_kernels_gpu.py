@@ -150,7 +150,14 @@ def test_tile_count():
 ])
 def test_conv_every_tile(tile, case):
     N, H, W, cin, cout, k, s, p, act, res, lx, xc = case
-    if DIRECT0 <= tile < XP0:
+    if NLOOP0 <= tile < XP0:
+        # each v6 tile is compiled for one Kpad (128 / 256 / 384 / 768, 1x1 or dual only):
+        # none of these cases is one of them
+        with pytest.raises(RuntimeError):
+            _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
+                       tile=tile)
+        return
+    if DIRECT0 <= tile < NLOOP0:
         # the direct family takes only its instantiated shapes; of these cases exactly the
         # 1x1 64 -> 128 from a channel slice is one (two Cout slices of the 64 -> 64 form,
         # every direct tile).  The others must be refused (3x3 + residual before the act, no
