@@ -343,10 +343,6 @@ int xp_launch(const KvConvParams* p, int tile, hipStream_t stream);
 // v8 split-K (conv_glds.hip SK kernels + finalize): indices after v7
 int sk_num_tiles();
 int sk_launch(const KvConvParams* p, int tile, hipStream_t stream);
-// v10 persistent LDS-DMA GEMM, epilogue overlapped by the next tile (conv_pde.hip): indices
-// after v7, before v8 (the split-K tiles stay the LAST indices)
-int pde_num_tiles();
-int pde_launch(const KvConvParams* p, int tile, hipStream_t stream);
 // v9 bottleneck seam, conv3 + residual -> next conv1 (conv_seam.hip): tail calls only, tile
 // indices after the whole table above (kv_conv_num_tiles() + i)
 int seam_num_tiles();
@@ -360,7 +356,7 @@ extern "C" int kv_nloop_sched_check(void) { return kvedge::nloop_sched_check(); 
 
 extern "C" int kv_conv_num_tiles(void) {
   return kNumTiles + glds_num_tiles() + stream_num_tiles() + direct_num_tiles() +
-         nloop_num_tiles() + xp_num_tiles() + pde_num_tiles() + sk_num_tiles();
+         nloop_num_tiles() + xp_num_tiles() + sk_num_tiles();
 }
 
 extern "C" int kv_conv_pick_tile(const KvConvParams* p) {
@@ -510,11 +506,9 @@ static int kv_conv2d_one(const KvConvParams* p, int tile, hipStream_t stream) {
   const int v4 = v3 + stream_num_tiles();
   const int v6 = v4 + direct_num_tiles();
   const int v7 = v6 + nloop_num_tiles();
-  const int v10 = v7 + xp_num_tiles();
-  const int v8 = v10 + pde_num_tiles();
+  const int v8 = v7 + xp_num_tiles();
   if (tile >= v8 + sk_num_tiles()) return -6;
   if (tile >= v8) return sk_launch(p, tile - v8, stream);
-  if (tile >= v10) return pde_launch(p, tile - v10, stream);
   if (tile >= v7) return xp_launch(p, tile - v7, stream);
   if (tile >= v6) return nloop_launch(p, tile - v6, stream);
   if (tile >= v4) return direct_launch(p, tile - v4, stream);

@@ -63,10 +63,10 @@ __device__ __forceinline__ void sm_wait_vm() {
 //     WAIT(B(s)) | barrier | B(s + D - 1) | j == 0: R(t + RD - 1) | MFMAs
 // vmcnt counts in issue order, so "X landed" = vmcnt(#ops issued after X).  The waits are
 // computed by replaying that sequence at compile time.
-template <int SY, int SZ, int D, int RD, int KB, int NC3>
+template <int SY, int SZ, int D, int RD, int KB, int NA>
 struct SmSched {
   static constexpr int SPT = SY + SZ;
-  static constexpr int kB = KB, kR = 2, kS = 2, kA = 2 * NC3;
+  static constexpr int kB = KB, kR = 2, kS = 2, kA = NA;  // NA: A-chunk DMAs per wave
   static constexpr int kFar = 12;
   static constexpr int kTiles = kFar + 2;
   // kind 0: wait before reading ring stage s; kind 1: wait before tile t's epilogue
@@ -137,15 +137,19 @@ __device__ __forceinline__ void sm_lds_barrier() {
 // NW waves (BM = 16 NW rows, (NW / 2) x 2 waves of 32 x 32); KS2 64-chunks per ring stage
 // (2 = 16-KB stages: half the waits and barriers per MFMA).  NW = 4 tiles fit 80 KB of LDS,
 // so two workgroups share a CU and one's ring waits hide under the other's MFMAs.
-template <int NC3, int NZC, int D, int RD, int NW = 8, int KS2 = 1>
+// AREG: each wave keeps its 32 rows of A (conv3's input) in VGPRs (NC3 x 16 registers)
+// instead of LDS: the conv3 steps then read only weight fragments from LDS (0.5 ds_read_b128
+// per MFMA instead of 1.0 -- the LDS-bound part of the step), and the freed LDS deepens the
+// weight ring.
+template <int NC3, int NZC, int D, int RD, int NW = 8, int KS2 = 1, bool AREG = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(const KvConvParams p, int ntiles) {
   static_assert(NW == 4 || NW == 8, "waves");
   static_assert(NC3 % KS2 == 0 && NZC % KS2 == 0, "whole chunks per ring stage");
   constexpr int SY = NC3 / KS2, SZ = NZC / KS2, BPW = 8 / NW;  // BPW: DMAs per wave per chunk
-  using S = SmSched<SY, SZ, D, RD, KS2 * BPW, NC3>;
+  using S = SmSched<SY, SZ, D, RD, KS2 * BPW, AREG ? 0 : 2 * NC3>;
   static_assert(S::ok(), "counted-wait schedule out of range or not periodic");
   constexpr int SPT = S::SPT, BM = 16 * NW, NT = 64 * NW;
-  constexpr int A_BYTES = NC3 * BM * 128, B_CHUNK = 64 * 128, B_STAGE = KS2 * B_CHUNK;
+  constexpr int A_BYTES = AREG ? 0 : NC3 * BM * 128, B_CHUNK = 64 * 128, B_STAGE = KS2 * B_CHUNK;
   constexpr int R_SLOT = BM * 64 * 2;
   constexpr int B_OFF = A_BYTES, R_OFF = B_OFF + D * B_STAGE, BIAS_OFF = R_OFF + RD * R_SLOT;
   constexpr int BIAS_ROUND = NW * 1024;  // bias DMAs: 1 KB per wave-instruction
@@ -235,22 +239,59 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(con
     const int off = (i * NW + wv) * 1024;
     kv_lds_dma16(rb1, lds + b1_off + off, off + lane * 16);
   }
+  // AREG: the wave's A fragments straight from global memory into VGPRs, in MFMA operand
+  // layout (lane (fr, fh) holds 8 consecutive K values of row wm*32 + tm*16 + fr).  Opaque
+  // loads issued BEFORE the ring prologue, then one counted wait that leaves the prologue
+  // DMAs in flight (an ordinary load would make hipcc drain everything at its first use,
+  // and -- loop-carried -- again at every tile: the conv3 MFMAs read these every tile)
+  typedef unsigned int sm_u32x4 __attribute__((ext_vector_type(4)));
+  sm_u32x4 araw[AREG ? NC3 : 1][2][2];
+  const int fr = lane & 15, fh = lane >> 4;
+  if constexpr (AREG) {
 #pragma unroll
-  for (int kc = 0; kc < NC3; ++kc)
+    for (int kc = 0; kc < NC3; ++kc)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      char* dst = lds + kc * (BM * 128) + (wv * 2 + i) * 1024;
-      const int v = (arow_off[i] != kSmOOB && kc * 64 + lc8[i] < p.Cin) ? arow_off[i] + kc * 128 : kSmOOB;
-      kv_lds_dma16(rx, dst, v);
-    }
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm) {
+          const int m = m0 + wm * 32 + tm * 16 + fr;
+          const int k = kc * 64 + ks * 32 + fh * 8;
+          const int off = (m < p.M && k < p.Cin) ? (m * p.ldx + p.x_coff + k) * 2 : kSmOOB;
+          asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen"
+                       : "=v"(araw[kc][ks][tm]) : "v"(off), "s"(rx) : "memory");
+        }
+  }
+  if constexpr (!AREG) {
+#pragma unroll
+    for (int kc = 0; kc < NC3; ++kc)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        char* dst = lds + kc * (BM * 128) + (wv * 2 + i) * 1024;
+        const int v = (arow_off[i] != kSmOOB && kc * 64 + lc8[i] < p.Cin) ? arow_off[i] + kc * 128 : kSmOOB;
+        kv_lds_dma16(rx, dst, v);
+      }
+  }
 #pragma unroll
   for (int t = 0; t < RD - 1; ++t) issue_R(t);
   sm_static_for<D - 1>([&](auto JJ) __attribute__((always_inline)) {
     constexpr int s = decltype(JJ)::value;
     issue_B(s / SPT, SmIC<s % SPT>{});
   });
+  bf16x8 areg[AREG ? NC3 : 1][2][2];
+  if constexpr (AREG) {
+    // A landed: every op issued after it is a ring-prologue DMA (R(0 .. RD-2), B(0 .. D-2))
+    sm_wait_vm<(RD - 1) * S::kR + (D - 1) * S::kB>();
+#pragma unroll
+    for (int kc = 0; kc < NC3; ++kc)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm) {
+          asm volatile("" : "+v"(araw[kc][ks][tm]));  // no consumer above the wait
+          areg[kc][ks][tm] = __builtin_bit_cast(bf16x8, araw[kc][ks][tm]);
+        }
+  }
 
-  const int fr = lane & 15, fh = lane >> 4;
   floatx4 acc[2][2];
   floatx4 accz[NZC][2][2];
 #pragma unroll
@@ -281,6 +322,26 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(con
 #pragma unroll
         for (int tm = 0; tm < 2; ++tm)
           c[tn][tm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[tn], af[tm], c[tn][tm], 0, 0, 0);
+    }
+  };
+
+  // conv3 K chunk kc with A from registers: acc[tn][tm] += Bs[wn*32 + tn*16 ..] . A^T
+  auto mma64r = [&](int kc_unused, const bf16x8 (&a)[2][2], const char* Bs, floatx4 (&c)[2][2])
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int q = ks * 4 + fh;
+      bf16x8 bfg[2];
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn) {
+        const int row = wn * 32 + tn * 16 + fr;
+        bfg[tn] = *reinterpret_cast<const bf16x8*>(Bs + row * 128 + ((q ^ sm_sw(row)) << 4));
+      }
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+          c[tn][tm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfg[tn], a[ks][tm], c[tn][tm], 0, 0, 0);
     }
   };
 
@@ -342,7 +403,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(con
         const char* Bs = lds + B_OFF + (s % D) * B_STAGE;
 #pragma unroll
         for (int c = 0; c < KS2; ++c) {
-          if constexpr (j < SY) mma64(lds + (j * KS2 + c) * (BM * 128), Bs + c * B_CHUNK, acc);
+          if constexpr (j < SY && AREG) mma64r(0, areg[j * KS2 + c], Bs + c * B_CHUNK, acc);
+          else if constexpr (j < SY) mma64(lds + (j * KS2 + c) * (BM * 128), Bs + c * B_CHUNK, acc);
           else mma64(Rs, Bs + c * B_CHUNK, accz[(j - SY) * KS2 + c]);
         }
       });
@@ -398,13 +460,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(con
 typedef void (*SmFn)(const KvConvParams, int);
 
 struct SmTile {
-  int nc3, nzc, d, rd, nw, ks2;
+  int nc3, nzc, d, rd, nw, ks2, areg;
   SmFn fn;
 };
 
-template <int NC3, int NZC, int D, int RD, int NW = 8, int KS2 = 1>
+template <int NC3, int NZC, int D, int RD, int NW = 8, int KS2 = 1, bool AREG = false>
 constexpr SmTile sm_tile() {
-  return SmTile{NC3, NZC, D, RD, NW, KS2, &conv_seam_kernel<NC3, NZC, D, RD, NW, KS2>};
+  return SmTile{NC3, NZC, D, RD, NW, KS2, AREG ? 1 : 0, &conv_seam_kernel<NC3, NZC, D, RD, NW, KS2, AREG>};
 }
 
 // LDS = A (K3 x BM x 2) + d x ks2 x 8 KB ring + rd x BM x 128 B residual ring + bias tables.
@@ -412,19 +474,29 @@ constexpr SmTile sm_tile() {
 // run ~0.44 us per ring step, latency-bound on the one shared weight ring; the 4-wave forms
 // put two workgroups on a CU, the KS2 = 2 forms halve the waits and barriers per MFMA.
 static const SmTile kSmTiles[] = {
-    sm_tile<2, 2, 6, 3>(),        // stage 2: K3 128, Cout 512 -> N1 128
-    sm_tile<2, 2, 4, 3, 4>(),     //   4 waves, 2 workgroups per CU (80 KB)
-    sm_tile<2, 2, 4, 3, 8, 2>(),  //   16-KB stages
-    sm_tile<2, 4, 6, 3>(),        // stage 2 -> 3: N1 256
-    sm_tile<4, 4, 5, 2>(),        // stage 3: K3 256, Cout 1024 -> N1 256
-    sm_tile<4, 4, 3, 2, 4>(),     //   4 waves, 2 workgroups per CU (80 KB)
-    sm_tile<4, 4, 3, 2, 8, 2>(),  //   16-KB stages
-    sm_tile<4, 8, 4, 3>(),        // stage 3 -> 4: N1 512
+    // stage 2 (K3 128, Cout 512 -> N1 128): 4 waves, two workgroups per CU first
+    // (profiles/r4_v2_seam_probe_b640.md: 305 us vs 337 for the 8-wave form, 358 unfused)
+    sm_tile<2, 2, 4, 3, 4>(),
+    sm_tile<2, 2, 6, 3>(),
+    sm_tile<2, 2, 4, 3, 8, 2>(),
+    sm_tile<2, 2, 6, 3, 4, 1, true>(),   // A in VGPRs (4 waves: 80 KB)
+    sm_tile<2, 2, 6, 3, 8, 2, true>(),   // A in VGPRs, 16-KB stages
+    // stage 2 -> 3 (N1 256)
+    sm_tile<2, 4, 6, 3>(),
+    sm_tile<2, 4, 6, 3, 8, 2, true>(),
+    // stage 3 (K3 256, Cout 1024 -> N1 256): 16-KB stages first (204 vs 217 us, 220 unfused)
+    sm_tile<4, 4, 3, 2, 8, 2>(),
+    sm_tile<4, 4, 5, 2>(),
+    sm_tile<4, 4, 3, 2, 4>(),
+    sm_tile<4, 4, 6, 2, 8, 2, true>(),   // A in VGPRs, 5 x 16 KB of weights in flight
+    sm_tile<4, 4, 8, 3, 8, 1, true>(),
+    // stage 3 -> 4 (N1 512): not taken by the model (level with unfused at b640)
+    sm_tile<4, 8, 4, 3>(),
 };
 
 int sm_lds_bytes(const SmTile& e, int cout, int n1) {
   const int bm = 16 * e.nw, round = e.nw * 1024;
-  return e.nc3 * bm * 128 + e.d * e.ks2 * 64 * 128 + e.rd * bm * 128 +
+  return (e.areg ? 0 : e.nc3 * bm * 128) + e.d * e.ks2 * 64 * 128 + e.rd * bm * 128 +
          ((cout * 4 + round - 1) / round) * round + ((n1 * 4 + round - 1) / round) * round;
 }
 

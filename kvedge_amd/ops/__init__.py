@@ -318,8 +318,10 @@ def conv_tail(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], ac
 
 
 # v9 bottleneck seams (csrc/kernels/conv_seam.hip) the tail path takes: (conv3 K3, conv3
-# Cout, next conv1 Cout) -- ResNet-50 stage 2, 2 -> 3, 3 and 3 -> 4
-SEAM_SHAPES = {(128, 512, 128), (128, 512, 256), (256, 1024, 256), (256, 1024, 512)}
+# Cout, next conv1 Cout) -- ResNet-50 stage 2, 2 -> 3 and 3.  The 3 -> 4 boundary seam
+# (N1 = 512) is level with the two unfused launches at batch 640 and stays unfused
+# (profiles/r4_v2_seam_probe_b640.md)
+SEAM_SHAPES = {(128, 512, 128), (128, 512, 256), (256, 1024, 256)}
 SEAM_ENABLED = os.environ.get("KVEDGE_SEAM", "1") != "0"
 # ... only when the layer gives every CU a 128-row workgroup (edge batches: split-K instead)
 SEAM_MIN_WGS = int(os.environ.get("KVEDGE_SEAM_MIN_WGS", "256"))

@@ -103,13 +103,12 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale
 
 
-N_TILES = 108  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue / N-160 (68-85) + v10 persistent DE (86-88) + v8 split-K (89-107)
+N_TILES = 105  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue / N-160 (68-85) + v8 split-K (86-104)
 # + v6 A-resident N-loop 1x1 GEMM (58-67, conv_nloop.hip kNlTiles: one Kpad per tile;
 # 63-65 are the fused-downsample (dual) forms, 66-67 step 128 K at a time)
 NLOOP0 = 58
 XP0 = 68  # v7: the v2 kernel's cross-stage pipelined loop (BK 32 rings, 8 waves)
-PDE0 = 86  # v10: persistent LDS-DMA tiles, epilogue overlapped by the next tile (conv_pde.hip)
-SK0 = 89  # v8: split-K (conv_sk.hip kSkTiles): K slices per tile (clamped to the K steps)
+SK0 = 86  # v8: split-K (conv_sk.hip kSkTiles): K slices per tile (clamped to the K steps)
 NLOOP_KPAD = [128, 256, 256, 256, 256, 384, 384, 768, 256, 256]
 NLOOP_DUAL = {63, 64, 65}
 STREAM0 = 32  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
@@ -171,11 +170,6 @@ def test_conv_every_tile(tile, case):
             with pytest.raises(RuntimeError):
                 _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
                            tile=tile)
-        return
-    if PDE0 <= tile < SK0 and (res or cin % 64 or k not in (1, 3)):
-        with pytest.raises(RuntimeError):  # v10: Cin % 64 == 0 KxK / 1x1, no residual
-            _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
-                       tile=tile)
         return
     if STREAM0 <= tile < DIRECT0 and (k != 1 or s != 1 or not _stream_fits(tile, (cin * k * k + 63) // 64 * 64, res)):
         with pytest.raises(RuntimeError):
@@ -440,7 +434,7 @@ def test_conv_dual_rejects_v1_tiles():
 
 
 @pytest.mark.parametrize("tile", [-1, 1, 6, 7, 12, 13, STREAM0, STREAM0 + 1, STREAM0 + 5, DIRECT0,
-                                  DIRECT0 + 1, XP0, XP0 + 4, PDE0, PDE0 + 2, SK0, SK0 + 9])
+                                  DIRECT0 + 1, XP0, XP0 + 4, SK0, SK0 + 9])
 @pytest.mark.parametrize("k", [1, 3])
 def test_conv_poisoned_canary(tile, k):
     """SURVEY §5.2 poisoned-buffer check: the output buffer is NaN-filled, with a NaN
@@ -741,20 +735,3 @@ def test_conv_seam(case):
             assert not torch.isnan(got.float()).any(), ("seam nan", case, st)
             _assert_close(got.cpu(), ref, ("seam", case, st))
     assert ran >= 2, "the default pick and at least one explicit seam tile must run"
-
-
-@pytest.mark.parametrize("tile", list(range(PDE0, SK0)))
-@pytest.mark.parametrize("case", [
-    # (N, H, W, cin, cout, k, stride) -- more tiles than CUs: every workgroup walks 2+ tiles,
-    # each epilogue overlapping the next tile's first K stage
-    (80, 28, 28, 128, 512, 3, 1),
-    (40, 28, 28, 256, 256, 3, 2),     # stride 2, M tail
-    (70, 28, 28, 512, 256, 1, 1),     # 1x1 reduce
-    (3, 7, 7, 512, 136, 3, 1),        # fewer tiles than CUs, N tail
-])
-def test_conv_pde_persistent(tile, case):
-    """v10 persistent direct-epilogue tiles (conv_pde.hip) vs the fp32 reference, with
-    several tiles per workgroup, stride 2, M / N tails."""
-    N, H, W, cin, cout, k, s = case
-    err, scale = _conv_case(N, H, W, cin, cout, k, s, k // 2, ops.ACT_RELU, tile=tile, seed=tile)
-    assert err <= 0.02 * scale, (tile, case, err, scale)

@@ -27,9 +27,9 @@ def load(path):
     return d, meta
 
 
-def main(root="gpurun_out/pmc", top=40):
+def main(root="gpurun_out/pmc", top=40, pattern="p*/p*_counter_collection.csv"):
     groups = collections.defaultdict(dict)
-    for p in sorted(glob.glob(f"{root}/p*/p*_counter_collection.csv")):
+    for p in sorted(glob.glob(f"{root}/{pattern}")):
         d, meta = load(p)
         for k, cs in d.items():
             name, grid, dur, vg, ag, lds = meta[k]
@@ -74,4 +74,4 @@ def main(root="gpurun_out/pmc", top=40):
 
 
 if __name__ == "__main__":
-    main(*(sys.argv[1:2] or []))
+    main(*(sys.argv[1:2] or []), *([40, sys.argv[2]] if len(sys.argv) > 2 else []))

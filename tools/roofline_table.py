@@ -14,6 +14,10 @@ its 7x7x3 taps).  Floors: HBM at --hbm TB/s, MFMA at --peak PF/s; 'floor' is the
 """
 import argparse
 import csv
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def layers(B, seam=False):
@@ -43,7 +47,7 @@ def layers(B, seam=False):
                   gemm(m1, 64 + (64 if dual else 0), 256) + gemm(m1, 256, nt)))
     # stages 2-4; with seam=True the v9 seam kernel (conv_seam.hip) runs a plain
     # conv3 + residual together with the NEXT block's conv1 (stages 2, 2->3, 3, 3->4)
-    seam_shapes = {(128, 512, 128), (128, 512, 256), (256, 1024, 256), (256, 1024, 512)}
+    from kvedge_amd.ops import SEAM_SHAPES as seam_shapes
     stages = [  # (stage, hw_in, hw, width, blocks)
         (2, 56, 28, 128, 4), (3, 28, 14, 256, 6), (4, 14, 7, 512, 3)]
     pending_c1 = 128  # conv1 of the next block already computed (stage-1 tail, or a seam)
