@@ -85,6 +85,39 @@ __device__ __forceinline__ void kv_settle(T& v) {
   v = __builtin_bit_cast(T, u);
 }
 
+// Compile-time loop: f(IC<I>{}) for I in [B, E) (IC below), so a body can use its index as an
+// immediate (asm "n"/"i" operands, constexpr ring slots).
+template <int I>
+struct IC;
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(IC<B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// ds_read_b128 that hipcc can neither sink nor merge: the caller owns the wait (a counted
+// s_waitcnt lgkmcnt tied to the destination, lds_wait below).  hipcc's scheduler sank every
+// fragment read of conv_direct.hip's ring to just before its MFMA under register pressure,
+// so each MFMA waited out a full LDS round trip (an lgkmcnt(0) in front of 100 % of them).
+template <int OFF, class T>
+__device__ __forceinline__ void lds_read16(T& dst, unsigned addr) {
+  static_assert(sizeof(T) == 16 && OFF >= 0 && OFF < 65536, "ds_read_b128 immediate offset");
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "n"(OFF) : "memory");
+}
+// wait until at most N LDS ops are outstanding; dst is threaded through so that its consumer
+// cannot be scheduled above the wait
+template <int N, class T>
+__device__ __forceinline__ void lds_wait(T& dst) {
+  static_assert(N >= 0 && N <= 15, "lgkmcnt field");
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(dst) : "n"(N) : "memory");
+}
+template <class T>
+__device__ __forceinline__ unsigned lds_addr(const T* p) {
+  return (unsigned)(unsigned long long)(const __attribute__((address_space(3))) void*)p;
+}
+
 __device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
 __device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }  // v_cvt_pk_bf16_f32, NaN-safe
 

@@ -43,6 +43,20 @@ constexpr int kOOB = 0x7ffffff0;
 constexpr int kLds = 160 * 1024;
 constexpr int kBiasBytes = 4 * 128;  // bias slot at the top of the LDS allocation
 
+// s_waitcnt vmcnt(k) for the largest k <= n in {0, 4, ..., 60}: at most n of the wave's
+// youngest vector-memory ops stay outstanding (rounding down only waits for more).  n must
+// be wave-uniform (an SGPR): the cascade is scalar branches around immediates.
+template <int K>
+__device__ __forceinline__ void direct_wait_vm_le_(int n) {
+  if constexpr (K == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    if (n >= K) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K) : "memory");
+    else direct_wait_vm_le_<K - 4>(n);
+  }
+}
+__device__ __forceinline__ void direct_wait_vm_le(int n) { direct_wait_vm_le_<60>(n); }
+
 template <int CIN, int KK>
 struct DirectCfg {
   static constexpr int PB = CIN * 2 + 16;         // patch bytes per pixel
@@ -60,7 +74,7 @@ struct DirectCfg {
 // (dy*2+dx)*4 + c, channel 3 zero) is built on the fly from raw bytes (exact in bf16; the
 // 1/255 scale is folded into the weights), fusing the preprocess pass away.
 #ifndef KV_DIRECT_PD
-#define KV_DIRECT_PD 2
+#define KV_DIRECT_PD 4
 #endif
 constexpr int KPD = KV_DIRECT_PD;
 
@@ -80,8 +94,17 @@ __host__ __device__ constexpr int direct_patch_alloc(int patch_bytes, bool dma) 
 // (bf16, as the unfused layer would have stored it) and the 1x1 runs on it from there:
 // z = t . W2^T + b2 goes to p.z [M][ldz] at z_coff and t never reaches HBM -- one launch and
 // one tensor round trip less per Detect branch.  W2 [C2][COUT] and b2 sit in LDS.
+// DE (direct epilogue, v10 tiles): each 32-pixel block's accumulators go straight to HBM (8-B
+// buffer stores, out-of-range lanes dropped by the descriptor) instead of through the LDS
+// output tile and a store pass behind a second barrier.  The band's stores then overlap the
+// next blocks' MFMAs, the output tile's LDS goes to taller bands (less halo re-staging), and
+// a band ends with ONE barrier after a counted vmcnt that waits for the next patch's DMAs
+// only -- never for this band's stores (vmcnt retires in issue order, the DMAs are older).
+// The plain-tile form spent ~64 % of wave cycles waiting at 31 % MFMA busy on the Detect P3
+// stem (profiles/r3_v10_yolo_detect_p3_direct_tiles_b192.txt): MFMA phase, store pass and
+// patch wait ran back to back on the only workgroup of the CU.
 template <int CIN, int COUT, int S, int KK, int ACT, bool RES, bool U8 = false, bool DMA = false,
-          bool PAIRS = false, int OCC = 1, int NT = kNT, int C2 = 0>
+          bool PAIRS = false, int OCC = 1, int NT = kNT, int C2 = 0, bool DE = false>
 // OCC = workgroups per CU the launch plans for (1 or 2); the second launch-bounds argument
 // is HIP's minimum waves per SIMD (512 threads = 2 per SIMD per workgroup).  The narrow
 // (16/32-channel) layers are latency-bound at one workgroup per CU -- one band in flight,
@@ -111,6 +134,7 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
   constexpr int NCB2 = (C2 + 31) / 32;   // pair: 32-channel blocks of the 1x1's output
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   static_assert(!(DMA && U8), "DMA patch fetch: bf16 NHWC inputs only");
+  static_assert(!DE || (DMA && !RES && C2 == 0 && !U8), "direct epilogue: plain DMA forms");
   const int psz = direct_patch_alloc(patch_rows * PW * C::PB, DMA);
   unsigned char* patch = lds;
   bf16* otile = reinterpret_cast<bf16*>(lds + (DMA ? 2 * psz : psz));
@@ -118,7 +142,8 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
   const int H = p.H, W = p.W, Ho = p.Ho, Wo = p.Wo;
   const int nbands = (Ho + kR - 1) / kR;
   const int total = p.N * nbands;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loops
   const int fr = lane & 31, fh = lane >> 5;
   const int cb = wv % NCB, ph = wv / NCB;
 
@@ -132,23 +157,35 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
     if (wrow < COUT) v = *reinterpret_cast<const bf16x8*>(wp + wrow * p.Kpad + kk * 16 + fh * 8);
     wreg[kk] = v;
   }
-  // bias staged once in LDS (not 16 live VGPRs: the CIN = 64 forms sit at the 256 cap)
+  // bias staged once in LDS; the DMA forms (no prefetch registers) then hold their 16 bias
+  // values in VGPRs for the whole kernel (the VGPR-prefetch forms sit at the 256 cap)
   float* lbias = reinterpret_cast<float*>(
-      reinterpret_cast<unsigned char*>(otile) + ((kR * p.Wo * OS * 2 + 15) & ~15));
+      reinterpret_cast<unsigned char*>(otile) + (DE ? 0 : ((kR * p.Wo * OS * 2 + 15) & ~15)));
   if (tid < NCB * 32) lbias[tid] = (p.bias && tid < COUT) ? p.bias[tid] : 0.f;
-  // pair: b2 [NCB2 * 32] then W2 [NCB2 * 32][OS] (rows past C2 zero) above the bias slot;
-  // the W2 row pitch equals the output tile's (conflict-free ds_read_b128 of 16 rows)
+  constexpr bool BREG = DMA && OCC == 1;  // bias in VGPRs (OCC = 2 forms: 128-VGPR cap)
+  floatx16 breg = {};
+  if constexpr (BREG) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = cb * 32 + g * 8 + fh * 4 + e;
+        breg[4 * g + e] = (p.bias && c < COUT) ? p.bias[c] : 0.f;
+      }
+  }
+  // pair: b2 [NCB2 * 32] then W2 [C2][OS] above the bias slot (the MFMA rows past C2 read
+  // row C2 - 1 again and are discarded: with 96 rows the C2 = 80 pair missed a 2-row band by
+  // 1.6 KB of LDS); the W2 row pitch equals the output tile's (conflict-free ds_read_b128)
   float* lbias2 = lbias + 128;
   bf16* w2s = reinterpret_cast<bf16*>(lbias2 + 128);
   if constexpr (C2 > 0) {
     static_assert(NCB2 * 32 <= 128 && NCB * 32 <= 128, "pair bias slots");
     if (tid < NCB2 * 32) lbias2[tid] = (p.bias_t && tid < C2) ? p.bias_t[tid] : 0.f;
     const bf16* w2 = reinterpret_cast<const bf16*>(p.w_t);
-    for (int q = tid; q < NCB2 * 32 * (COUT / 8); q += NT) {
+    for (int q = tid; q < C2 * (COUT / 8); q += NT) {
       const int r = q / (COUT / 8), c = (q - r * (COUT / 8)) * 8;
-      bf16x8 v = {};
-      if (r < C2) v = *reinterpret_cast<const bf16x8*>(w2 + (size_t)r * COUT + c);
-      *reinterpret_cast<bf16x8*>(w2s + r * OS + c) = v;
+      *reinterpret_cast<bf16x8*>(w2s + r * OS + c) =
+          *reinterpret_cast<const bf16x8*>(w2 + (size_t)r * COUT + c);
     }
   }
 
@@ -287,7 +324,7 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
   // its stores to be acknowledged -- one HBM write latency per band on every CU.  Split, the
   // DMA waves have no stores outstanding and the store waves never wait on vmcnt.
   constexpr int NWV = NT / 64;
-  constexpr bool SPLIT = DMA && !RES && NWV >= 4 && C2 == 0;
+  constexpr bool SPLIT = DMA && !RES && NWV >= 4 && C2 == 0 && !DE;
   constexpr int NWD = SPLIT ? NWV / 2 : NWV;  // waves issuing the patch DMA
   auto dma_fetch = [&](int item, unsigned char* dst) __attribute__((always_inline)) {
     const int n = item / nbands, band = item - n * nbands;
@@ -309,6 +346,10 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
   };
 
   bf16* __restrict__ Y = reinterpret_cast<bf16*>(p.y);
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+      p.y, (short)0, DE ? p.N * Ho * Wo * p.ldy * 2 : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
+      C2 > 0 ? p.z : p.y, (short)0, C2 > 0 ? p.N * Ho * Wo * p.ldz * 2 : 0, 0x00020000);
   const bf16* __restrict__ R = reinterpret_cast<const bf16*>(p.res);
   const int npix = kR * Wo;
   const int nblk = (npix + 31) / 32;
@@ -376,42 +417,68 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
         po[r] = pa[r] + (S == 2 ? HALF * C::PB : 0);
       }
       floatx16 acc;
+      if constexpr (BREG) {
+        acc = breg;
+      } else {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 bv = *reinterpret_cast<const float4*>(lbias + cb * 32 + g * 8 + fh * 4);
-        acc[4 * g + 0] = bv.x;
-        acc[4 * g + 1] = bv.y;
-        acc[4 * g + 2] = bv.z;
-        acc[4 * g + 3] = bv.w;
+        for (int g = 0; g < 4; ++g) {
+          const float4 bv = *reinterpret_cast<const float4*>(lbias + cb * 32 + g * 8 + fh * 4);
+          acc[4 * g + 0] = bv.x;
+          acc[4 * g + 1] = bv.y;
+          acc[4 * g + 2] = bv.z;
+          acc[4 * g + 3] = bv.w;
+        }
+        // the bias reads retire here, before the counted fragment ring below starts
+        asm volatile("" : "+v"(acc));
       }
-      // fragment ring: the read for step kk + PD is issued before the MFMA of step kk, so
-      // PD LDS reads are in flight behind the MFMA pipe (PD = 1 left the MFMAs waiting on
-      // ds_read latency: 29 % MFMA busy in PMC)
-      constexpr int PD = NT == kNT ? KPD : 6;  // one wave per SIMD: a deeper read ring
+      // fragment ring (asm reads, common.h): the read for step kk + PD is issued before the
+      // MFMA of step kk and each MFMA waits for its own read only -- PD reads stay in flight
+      // behind the MFMA pipe.  Tap offsets are ds_read immediates off KK (stride 2: 2 KK) row
+      // bases; no VALU per MFMA.
+      constexpr int PD = NT == kNT ? (OCC == 2 ? 2 : CIN >= 80 ? 3 : KPD) : 6;
       bf16x8 af[PD + 1];
-      auto load = [&](int buf, int kk) __attribute__((always_inline)) {
-        const int tap = kk / C::KPT, s4 = kk - (kk / C::KPT) * C::KPT;
-        const int r = tap / KK, s = tap - (tap / KK) * KK;
-        if (S == 2 && s == 1)
-          af[buf] = *reinterpret_cast<const bf16x8*>(po[r] + s4 * 32);
+      unsigned ba[KK], bo[KK];
+#pragma unroll
+      for (int r = 0; r < KK; ++r) {
+        ba[r] = lds_addr(pa[r]);
+        bo[r] = lds_addr(po[r]);
+      }
+      auto rd = [&](auto kc) __attribute__((always_inline)) {
+        constexpr int kk = decltype(kc)::value;
+        constexpr int tap = kk / C::KPT, s4 = kk % C::KPT;
+        constexpr int r = tap / KK, s = tap % KK;
+        if constexpr (S == 2 && s == 1)
+          lds_read16<s4 * 32>(af[kk % (PD + 1)], bo[r]);
         else
-          af[buf] = *reinterpret_cast<const bf16x8*>(pa[r] + (S == 2 ? s / 2 : s) * C::PB + s4 * 32);
+          lds_read16<(S == 2 ? s / 2 : s) * C::PB + s4 * 32>(af[kk % (PD + 1)], ba[r]);
       };
-#pragma unroll
-      for (int kk = 0; kk < PD; ++kk) load(kk, kk);
-#pragma unroll
-      for (int kk = 0; kk < C::KS; ++kk) {
-        if (kk + PD < C::KS) load((kk + PD) % (PD + 1), kk + PD);
+      static_for<0, (PD < C::KS ? PD : C::KS)>(rd);
+      static_for<0, C::KS>([&](auto kc) __attribute__((always_inline)) {
+        constexpr int kk = decltype(kc)::value;
+        if constexpr (kk + PD < C::KS) rd(IC<kk + PD>{});
+        constexpr int younger = (C::KS - 1 - kk) < PD ? (C::KS - 1 - kk) : PD;
+        lds_wait<younger>(af[kk % (PD + 1)]);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wreg[kk], af[kk % (PD + 1)], acc, 0, 0, 0);
-      }
-      // reads(0..PD-1) | reads(k+PD) MFMA(k) ...
-      __builtin_amdgcn_sched_group_barrier(0x100, PD, 0);
-#pragma unroll
-      for (int kk = 0; kk < C::KS; ++kk) {
-        if (kk + PD < C::KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      }
+      });
       const int jr = b * 32 + fr;
+      if constexpr (DE) {
+        // lanes fr / fr + 32 write channels [g*8, g*8+4) / [g*8+4, g*8+8) of pixel jr: 16
+        // contiguous bytes per pixel and instruction; L2 merges the 4 groups' lines
+        const int oy = oy0 + yl;
+        const bool ok = jr < npix && oy < Ho;
+        const int base = (((n * Ho + oy) * Wo + xc) * p.ldy + p.y_coff + cb * 32 + fh * 4) * 2;
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          if (cb * 32 + g * 8 >= COUT) continue;  // wave-uniform; counted in nst below
+          bf16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = f2bf(act_c<ACT>(acc[4 * g + e]));
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ry,
+                                                ok ? base + g * 16 : kOOB, 0, 0);
+        }
+        continue;
+      }
       if (jr < npix) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -424,6 +491,18 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
           *reinterpret_cast<bf16x4*>(otile + jr * OS + cb * 32 + g * 8 + fh * 4) = o;
         }
       }
+    }
+    if constexpr (DE) {
+      // this wave's stores of the band (nbw blocks x ng groups) are its youngest vector-memory
+      // ops: wait for everything older -- the next band's patch DMAs -- and leave them in flight
+      const int nbw = ph < NPH ? (nblk - ph + NPH - 1) / NPH : 0;
+      const int ng = min(4, (COUT - cb * 32 + 7) / 8);
+      direct_wait_vm_le(__builtin_amdgcn_readfirstlane(nbw * ng));
+      cur ^= 1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // next patch visible; this patch's reads all retired
+      asm volatile("" ::: "memory");
+      continue;
     }
     __syncthreads();  // output tile complete; patch no longer read
     // next band's patch BEFORE this band's stores: on gfx9 vmcnt counts stores too, so a
@@ -453,7 +532,6 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
     if constexpr (C2 > 0) {
       // ---- pair: z = t . W2^T + b2 from the output tile, 32 pixels x 32 channels per unit,
       // stored straight from the accumulators (a lane: 4 consecutive channels of a pixel)
-      bf16* __restrict__ Z = reinterpret_cast<bf16*>(p.z);
       for (int u = wv; u < nblk * NCB2; u += NWV) {
         const int b = u / NCB2, cb2 = u - b * NCB2;
         floatx16 acc2;
@@ -466,28 +544,45 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
           acc2[4 * g + 3] = bv.w;
         }
         const bf16* tp = otile + (b * 32 + fr) * OS + fh * 8;  // rows past npix: discarded
-        const bf16* wp2 = w2s + (cb2 * 32 + fr) * OS + fh * 8;
+        const bf16* wp2 = w2s + min(cb2 * 32 + fr, C2 - 1) * OS + fh * 8;
 #pragma unroll
         for (int ks = 0; ks < COUT / 16; ++ks)
           acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
               *reinterpret_cast<const bf16x8*>(wp2 + ks * 16),
               *reinterpret_cast<const bf16x8*>(tp + ks * 16), acc2, 0, 0, 0);
+        // buffer stores, out-of-range lanes dropped by the descriptor: every wave issues
+        // exactly ng2(cb2) stores per unit, so the band end can count them (below)
         const int jr = b * 32 + fr;
-        if (jr < npix) {
-          const int yl = fdiv(jr, fWo), xc = jr - yl * Wo;
-          const int oy = oy0 + yl;
-          if (oy < Ho) {
-            bf16* zp = Z + ((long long)(n * Ho + oy) * Wo + xc) * p.ldz + p.z_coff + cb2 * 32 + fh * 4;
+        const int jc = min(jr, npix - 1);
+        const int yl = fdiv(jc, fWo), xc = jc - yl * Wo;
+        const int oy = oy0 + yl;
+        const bool ok = jr < npix && oy < Ho;
+        const int base = (((n * Ho + oy) * Wo + xc) * p.ldz + p.z_coff + cb2 * 32 + fh * 4) * 2;
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              if (cb2 * 32 + g * 8 >= C2) continue;  // compile-time for C2 % 32 == 0
-              bf16x4 o;
+        for (int g = 0; g < 4; ++g) {
+          if (cb2 * 32 + g * 8 >= C2) continue;  // wave-uniform
+          bf16x4 o;
 #pragma unroll
-              for (int e = 0; e < 4; ++e) o[e] = f2bf(acc2[4 * g + e]);
-              *reinterpret_cast<bf16x4*>(zp + g * 8) = o;
-            }
-          }
+          for (int e = 0; e < 4; ++e) o[e] = f2bf(acc2[4 * g + e]);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), rz,
+                                                ok ? base + g * 16 : kOOB, 0, 0);
         }
+      }
+      if constexpr (DMA) {
+        // the z stores are this wave's youngest vector-memory ops: wait for the next patch's
+        // DMAs only, then an LDS-only barrier (__syncthreads' fence would drain the stores)
+        int nz = 0;
+        for (int u = wv; u < nblk * NCB2; u += NWV) {
+          const int cb2 = u - (u / NCB2) * NCB2;
+          nz += min(4, (C2 - cb2 * 32 + 7) / 8);
+        }
+        direct_wait_vm_le(__builtin_amdgcn_readfirstlane(nz));
+        cur ^= 1;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // next patch visible; output tile and patch free
+        asm volatile("" ::: "memory");
+        continue;
       }
     }
     constexpr int SB = SPLIT ? NWD * 64 : 0;  // first storing thread
@@ -529,6 +624,7 @@ struct DirectEntry {
   int occ = 1;         // workgroups per CU (launch bounds, LDS budget, grid)
   int nt = kNT;        // threads per workgroup
   int c2 = 0;          // fused 1x1 pair: its output channels (0 = plain conv)
+  bool de = false;     // direct epilogue (v10 tiles; DMA forms only)
 };
 
 #define KV_DIRECT(CI, CO, S, A, R) {CI, CO, S, 3, A, R, conv3x3_direct_kernel<CI, CO, S, 3, A, R>}
@@ -540,6 +636,15 @@ struct DirectEntry {
 #define KV_DIRECT_OCC2(CI, CO, S, KK, A, R)                                                       \
   {CI, CO, S, KK, A, R, conv3x3_direct_kernel<CI, CO, S, KK, A, R, false, true, false, 2>, false, \
    true, false, 2}
+// v10: the direct-epilogue forms (one or two workgroups per CU)
+#define KV_DIRECT_DE(CI, CO, S, KK, A)                                                          \
+  {CI, CO, S, KK, A, false,                                                                    \
+   conv3x3_direct_kernel<CI, CO, S, KK, A, false, false, true, false, 1, kNT, 0, true>, false,  \
+   true, false, 1, kNT, 0, true}
+#define KV_DIRECT_DE2(CI, CO, S, KK, A)                                                         \
+  {CI, CO, S, KK, A, false,                                                                    \
+   conv3x3_direct_kernel<CI, CO, S, KK, A, false, false, true, false, 2, kNT, 0, true>, false,  \
+   true, false, 2, kNT, 0, true}
 #define KV_DIRECT1(CI, CO, A)                                                        \
   {CI, CO, 1, 1, A, false, conv3x3_direct_kernel<CI, CO, 1, 1, A, false>},           \
   {CI, CO, 1, 1, A, false, conv3x3_direct_kernel<CI, CO, 1, 1, A, false, false, true>, false, true}
@@ -593,8 +698,29 @@ static const DirectEntry kDirect[] = {
     {80, 80, 1, 3, kActSilu, false,
      conv3x3_direct_kernel<80, 80, 1, 3, kActSilu, false, false, true, false, 1, kNT, 80>, false,
      true, false, 1, kNT, 80},
+    // v10 direct-epilogue forms (listed last: the v4 tiles' any-form fallback never lands here)
+    KV_DIRECT_DE(64, 64, 1, 3, kActRelu),     // ResNet-50 layer1 conv2
+    KV_DIRECT_DE(64, 128, 1, 3, kActSilu),    // Detect P3 merged stem 64 -> 144 = 128 + 16
+    KV_DIRECT_DE(64, 16, 1, 3, kActSilu),
+    KV_DIRECT_DE(64, 64, 1, 3, kActSilu),     // bottleneck cv1 / Detect a1
+    KV_DIRECT_DE(80, 80, 1, 3, kActSilu),
+    KV_DIRECT_DE(64, 128, 2, 3, kActSilu),    // b5
+    KV_DIRECT_DE(64, 64, 2, 3, kActSilu),     // h16
+    KV_DIRECT_DE(32, 64, 2, 3, kActSilu),     // b3
+    KV_DIRECT_DE(16, 32, 2, 3, kActSilu),     // b1
+    KV_DIRECT_DE(32, 32, 1, 3, kActSilu),
+    KV_DIRECT_DE(16, 16, 1, 3, kActSilu),
+    KV_DIRECT_DE(32, 32, 1, 1, kActSilu), KV_DIRECT_DE(48, 32, 1, 1, kActSilu),
+    KV_DIRECT_DE(64, 64, 1, 1, kActSilu), KV_DIRECT_DE(128, 64, 1, 1, kActSilu),
+    KV_DIRECT_DE(192, 64, 1, 1, kActSilu), KV_DIRECT_DE(96, 64, 1, 1, kActSilu),
+    KV_DIRECT_DE(64, 64, 1, 1, kActNone), KV_DIRECT_DE(80, 80, 1, 1, kActNone),
+    KV_DIRECT_DE2(16, 32, 2, 3, kActSilu), KV_DIRECT_DE2(16, 16, 1, 3, kActSilu),
+    KV_DIRECT_DE2(32, 64, 2, 3, kActSilu), KV_DIRECT_DE2(32, 32, 1, 3, kActSilu),
+    KV_DIRECT_DE2(32, 32, 1, 1, kActSilu), KV_DIRECT_DE2(48, 32, 1, 1, kActSilu),
 };
 #undef KV_DIRECT2
+#undef KV_DIRECT_DE
+#undef KV_DIRECT_DE2
 #undef KV_DIRECT1
 #undef KV_DIRECT_OCC2
 #undef KV_DIRECT_DMA
@@ -606,8 +732,11 @@ int direct_max_patch(int cin) { return (cin >= 80 ? 6 : cin >= 64 ? 7 : 10) * kN
 }  // namespace
 
 // tile 0: the VGPR-prefetch form where one exists; tile 1: the DMA form where one exists
-// tile bit 0: DMA patch fetch; bit 1: two workgroups per CU (the OCC = 2 forms)
+// tile bit 0: DMA patch fetch; bit 1: two workgroups per CU (the OCC = 2 forms).
+// Internal codes 4..7 (bit 2) are the direct-epilogue forms, exposed as the v10 tiles
+// (direct_de_launch): they take only their own instantiations, no fallback.
 int direct_num_tiles() { return 4; }
+int direct_de_num_tiles() { return 2; }
 
 // Returns the instantiation index for p (or < 0), and the band geometry it would use.
 static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* rows, int* lds) {
@@ -623,13 +752,13 @@ static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* r
   const bool res = p->res != nullptr;
   if (res && !(p->act & 4) && act != kActNone) return -8;  // only x + act(conv)
   int idx = -1;
-  for (int pass = 0; pass < 2 && idx < 0; ++pass) {  // the tile's form first, then any
+  for (int pass = 0; pass < ((tile & 4) ? 1 : 2) && idx < 0; ++pass) {  // the tile's form, then any
     for (int i = 0; i < (int)(sizeof(kDirect) / sizeof(kDirect[0])); ++i) {
       const DirectEntry& e = kDirect[i];
       if (e.cin == p->Cin && e.cout == p->Cout && e.stride == p->stride && e.kk == kk &&
           e.act == act && e.res == res && e.u8 == (p->in_u8 != 0) &&
           (!e.u8 || e.pairs == (p->W % 2 == 0)) &&
-          e.c2 == (p->pair_1x1 ? p->n_t : 0) &&
+          e.c2 == (p->pair_1x1 ? p->n_t : 0) && e.de == ((tile & 4) != 0) &&
           (pass == 1 || (e.dma == ((tile & 1) != 0) && e.occ == 1 + ((tile >> 1) & 1)))) {
         idx = i;
         break;
@@ -642,6 +771,8 @@ static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* r
   if (kk == 3 && (p->Ho != (p->H - 1) / p->stride + 1 || p->Wo != (p->W - 1) / p->stride + 1))
     return -8;
   if (!p->in_u8 && (long long)p->N * p->H * p->W * p->ldx * 2 >= kOOB) return -9;
+  if ((long long)p->N * p->Ho * p->Wo * p->ldy * 2 >= kOOB) return -9;
+  if (p->pair_1x1 && (long long)p->N * p->Ho * p->Wo * p->ldz * 2 >= kOOB) return -9;
   const int S = p->stride;
   *PW = (p->Wo - 1) * S + kk;
   const int pb = direct_pb(p->Cin);
@@ -651,9 +782,10 @@ static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* r
   const bool dma = kDirect[idx].dma;
   auto lds_of = [&](int prows, int r) {
     const int np = dma ? 2 : 1;
-    const int c2p = (kDirect[idx].c2 + 31) / 32 * 32;  // pair: b2 slot + W2 [c2p][os]
-    return np * direct_patch_alloc(prows * *PW * pb, dma) + ((r * p->Wo * os * 2 + 15) & ~15) +
-           kBiasBytes + (c2p ? kBiasBytes + c2p * os * 2 : 0);
+    const int c2p = kDirect[idx].c2;  // pair: b2 slot + W2 [c2][os]
+    const int ot = kDirect[idx].de ? 0 : ((r * p->Wo * os * 2 + 15) & ~15);  // output tile
+    return np * direct_patch_alloc(prows * *PW * pb, dma) + ot + kBiasBytes +
+           (c2p ? kBiasBytes + c2p * os * 2 : 0);
   };
   // band height: the tallest that fits (<= 8).  (A "fewest pixel-block rounds" rule was
   // measured slower on YOLO's 32-channel layers at 160^2: the extra halo rows and per-band
@@ -697,7 +829,7 @@ static int direct_launch_one(const KvConvParams* p, int tile, hipStream_t stream
 // that have one (largest first), e.g. YOLO's merged Detect stem 64 -> 144 = 128 + 16: each
 // slice re-reads the input (cheap: the layer is MFMA-bound) and writes its y_coff range.
 int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
-  if (tile < 0 || tile >= direct_num_tiles()) return -6;
+  if (tile < 0 || tile >= 8) return -6;
   int kR, PW, rows, lds;
   if (direct_plan(p, tile, &kR, &PW, &rows, &lds) >= 0) return direct_launch_one(p, tile, stream);
   if (p->res || p->Cout % 16 || p->pair_1x1) return -8;
@@ -728,6 +860,12 @@ int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
     off += cuts[i];
   }
   return 0;
+}
+
+// v10 tile i: the DMA direct-epilogue form at 1 + i workgroups per CU
+int direct_de_launch(const KvConvParams* p, int tile, hipStream_t stream) {
+  if (tile < 0 || tile >= direct_de_num_tiles() || p->res || p->pair_1x1) return -8;
+  return direct_launch(p, 4 | 1 | (tile << 1), stream);
 }
 
 }  // namespace kvedge

@@ -343,6 +343,9 @@ int xp_launch(const KvConvParams* p, int tile, hipStream_t stream);
 // v8 split-K (conv_glds.hip SK kernels + finalize): indices after v7
 int sk_num_tiles();
 int sk_launch(const KvConvParams* p, int tile, hipStream_t stream);
+// v10 direct-epilogue forms of the v4 family (conv_direct.hip): indices after v8
+int direct_de_num_tiles();
+int direct_de_launch(const KvConvParams* p, int tile, hipStream_t stream);
 // v9 bottleneck seam, conv3 + residual -> next conv1 (conv_seam.hip): tail calls only, tile
 // indices after the whole table above (kv_conv_num_tiles() + i)
 int seam_num_tiles();
@@ -356,7 +359,7 @@ extern "C" int kv_nloop_sched_check(void) { return kvedge::nloop_sched_check(); 
 
 extern "C" int kv_conv_num_tiles(void) {
   return kNumTiles + glds_num_tiles() + stream_num_tiles() + direct_num_tiles() +
-         nloop_num_tiles() + xp_num_tiles() + sk_num_tiles();
+         nloop_num_tiles() + xp_num_tiles() + sk_num_tiles() + direct_de_num_tiles();
 }
 
 extern "C" int kv_conv_pick_tile(const KvConvParams* p) {
@@ -507,7 +510,9 @@ static int kv_conv2d_one(const KvConvParams* p, int tile, hipStream_t stream) {
   const int v6 = v4 + direct_num_tiles();
   const int v7 = v6 + nloop_num_tiles();
   const int v8 = v7 + xp_num_tiles();
-  if (tile >= v8 + sk_num_tiles()) return -6;
+  const int v10 = v8 + sk_num_tiles();
+  if (tile >= v10 + direct_de_num_tiles()) return -6;
+  if (tile >= v10) return direct_de_launch(p, tile - v10, stream);
   if (tile >= v8) return sk_launch(p, tile - v8, stream);
   if (tile >= v7) return xp_launch(p, tile - v7, stream);
   if (tile >= v6) return nloop_launch(p, tile - v6, stream);

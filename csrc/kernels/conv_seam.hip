@@ -484,12 +484,17 @@ static const SmTile kSmTiles[] = {
     // stage 2 -> 3 (N1 256): A in VGPRs, 16-KB stages first (388 vs 408 us, 414 unfused)
     sm_tile<2, 4, 6, 3, 8, 2, true>(),
     sm_tile<2, 4, 6, 3>(),
-    // stage 3 (K3 256, Cout 1024 -> N1 256): 16-KB stages first (204 vs 217 us, 220 unfused)
+    // stage 3 (K3 256, Cout 1024 -> N1 256): A in VGPRs with a 4-slot residual ring first --
+    // 3 tiles (48 KB) of residual in flight per CU: 197.5 vs 202.8 us for the 16-KB-stage
+    // form and 216 unfused (profiles/r4_v3_seam_probe_b640.md; the same deeper ring lost
+    // on stage 2, whose 4-wave form already holds two workgroups' rings per CU)
+    sm_tile<4, 4, 4, 4, 8, 2, true>(),
     sm_tile<4, 4, 3, 2, 8, 2>(),
     sm_tile<4, 4, 5, 2>(),
     sm_tile<4, 4, 3, 2, 4>(),
     sm_tile<4, 4, 6, 2, 8, 2, true>(),   // A in VGPRs, 5 x 16 KB of weights in flight
     sm_tile<4, 4, 8, 3, 8, 1, true>(),
+    sm_tile<4, 4, 3, 5, 8, 2, true>(),
     // stage 3 -> 4 (N1 512): not taken by the model (level with unfused at b640)
     sm_tile<4, 8, 4, 3>(),
 };

@@ -63,7 +63,7 @@ def load(build_if_missing: bool = False) -> bool:
         return False
     _check_single_hip_runtime()
     global SPLITK0
-    SPLITK0 = int(torch.ops.kvedge.conv_num_tiles()) - N_SPLITK_TILES
+    SPLITK0 = int(torch.ops.kvedge.conv_num_tiles()) - N_DE_TILES - N_SPLITK_TILES
     _loaded = True
     return True
 
@@ -206,8 +206,13 @@ def unpack_conv_weight(wp: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
 _WS: dict = {}
 SPLITK_MAX_ELEMS = 32 << 20  # 128 MB of fp32 per stream at most
 SPLITK_MAX_SPLIT = 32        # largest split of conv_sk.hip kSkTiles
-N_SPLITK_TILES = 19          # conv_sk.hip kSkTiles: the LAST tile indices
+N_SPLITK_TILES = 19          # conv_sk.hip kSkTiles
+N_DE_TILES = 2               # v10 direct-epilogue tiles (conv_direct.hip): after split-K, last
 SPLITK0 = 1 << 30            # first split-K tile index, set by load()
+
+
+def is_splitk(tile: int) -> bool:
+    return SPLITK0 <= tile < SPLITK0 + N_SPLITK_TILES
 
 
 def splitk_workspace(device: torch.device, elems: int) -> Optional[torch.Tensor]:
@@ -241,7 +246,7 @@ def conv2d(x: torch.Tensor, spec: ConvSpec, w: torch.Tensor, bias: Optional[torc
     ldy = out.shape[3]
     ldr = res.shape[-1] if res is not None else 0
     if x.is_cuda:
-        ws = splitk_workspace(x.device, N * Ho * Wo * spec.cout) if tile >= SPLITK0 else None
+        ws = splitk_workspace(x.device, N * Ho * Wo * spec.cout) if is_splitk(tile) else None
         _native().conv(x, w, bias, res, out, N, H, W, spec.cin_eff, ldx, x_coff, Ho, Wo,
                        spec.cout, spec.kh, spec.kw, spec.stride, spec.pad, spec.K, ldy, y_coff,
                        ldr, r_coff, spec.act, spec.mode, tile, ws)
@@ -282,7 +287,7 @@ def conv_dual(x1: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, bias: Optiona
     if out is None:
         out = empty(N, Ho, Wo, cout, dtype=torch.bfloat16, device=x1.device)
     if x1.is_cuda:
-        ws = splitk_workspace(x1.device, N * Ho * Wo * cout) if tile >= SPLITK0 else None
+        ws = splitk_workspace(x1.device, N * Ho * Wo * cout) if is_splitk(tile) else None
         _native().conv_dual(x1, x2, w, bias, out, stride2, act, tile, ws)
     else:
         _ref.conv_dual(x1, x2, w, bias, act, stride2, out)

@@ -103,12 +103,45 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale
 
 
-N_TILES = 105  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue / N-160 (68-85) + v8 split-K (86-104)
+N_TILES = 107  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue / N-160 (68-85) + v8 split-K (86-104) + v10 (105-106)
 # + v6 A-resident N-loop 1x1 GEMM (58-67, conv_nloop.hip kNlTiles: one Kpad per tile;
 # 63-65 are the fused-downsample (dual) forms, 66-67 step 128 K at a time)
 NLOOP0 = 58
 XP0 = 68  # v7: the v2 kernel's cross-stage pipelined loop (BK 32 rings, 8 waves)
 SK0 = 86  # v8: split-K (conv_sk.hip kSkTiles): K slices per tile (clamped to the K steps)
+DE0 = 105  # v10: the direct family's direct-epilogue forms (conv_direct.hip), 1 / 2 workgroups per CU
+# (cin, cout, k, stride, act) instantiated as v10 tile 0 / tile 1 (no residual, no fallback)
+DE_SHAPES = {
+    0: {(64, 64, 3, 1, ops.ACT_RELU), (64, 128, 3, 1, ops.ACT_SILU), (64, 16, 3, 1, ops.ACT_SILU),
+        (64, 64, 3, 1, ops.ACT_SILU), (80, 80, 3, 1, ops.ACT_SILU), (64, 128, 3, 2, ops.ACT_SILU),
+        (64, 64, 3, 2, ops.ACT_SILU), (32, 64, 3, 2, ops.ACT_SILU), (16, 32, 3, 2, ops.ACT_SILU),
+        (32, 32, 3, 1, ops.ACT_SILU), (16, 16, 3, 1, ops.ACT_SILU), (32, 32, 1, 1, ops.ACT_SILU),
+        (48, 32, 1, 1, ops.ACT_SILU), (64, 64, 1, 1, ops.ACT_SILU), (128, 64, 1, 1, ops.ACT_SILU),
+        (192, 64, 1, 1, ops.ACT_SILU), (96, 64, 1, 1, ops.ACT_SILU), (64, 64, 1, 1, ops.ACT_NONE),
+        (80, 80, 1, 1, ops.ACT_NONE)},
+    1: {(16, 32, 3, 2, ops.ACT_SILU), (16, 16, 3, 1, ops.ACT_SILU), (32, 64, 3, 2, ops.ACT_SILU),
+        (32, 32, 3, 1, ops.ACT_SILU), (32, 32, 1, 1, ops.ACT_SILU), (48, 32, 1, 1, ops.ACT_SILU)},
+}
+
+
+def _de_takes(tile, cin, cout, k, s, act, res):
+    """Mirror of direct_plan() for a v10 tile: an instantiated shape, or a Cout covered by
+    instantiated slices (largest first, e.g. 144 = 128 + 16), never a residual."""
+    if res:
+        return False
+    shapes = DE_SHAPES[tile - DE0]
+    if (cin, cout, k, s, act) in shapes:
+        return True
+    if cout % 16:
+        return False
+    done = 0
+    while done < cout:
+        best = max((c for (ci, c, kk, ss, a) in shapes
+                    if (ci, kk, ss, a) == (cin, k, s, act) and c <= cout - done), default=0)
+        if best == 0:
+            return False
+        done += best
+    return True
 NLOOP_KPAD = [128, 256, 256, 256, 256, 384, 384, 768, 256, 256]
 NLOOP_DUAL = {63, 64, 65}
 STREAM0 = 32  # v3 tiles take 1x1 stride-1 GEMMs and dual-source convs only
@@ -149,6 +182,16 @@ def test_tile_count():
 ])
 def test_conv_every_tile(tile, case):
     N, H, W, cin, cout, k, s, p, act, res, lx, xc = case
+    if tile >= DE0:
+        if _de_takes(tile, cin, cout, k, s, act, res) and p == k // 2:
+            err, scale = _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx,
+                                    x_coff=xc, tile=tile)
+            assert err <= 0.02 * scale, (tile, case, err, scale)
+        else:
+            with pytest.raises(RuntimeError):
+                _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
+                           tile=tile)
+        return
     if NLOOP0 <= tile < XP0:
         # each v6 tile is compiled for one Kpad (128 / 256 / 384 / 768, 1x1 or dual only):
         # none of these cases is one of them
@@ -434,7 +477,7 @@ def test_conv_dual_rejects_v1_tiles():
 
 
 @pytest.mark.parametrize("tile", [-1, 1, 6, 7, 12, 13, STREAM0, STREAM0 + 1, STREAM0 + 5, DIRECT0,
-                                  DIRECT0 + 1, XP0, XP0 + 4, SK0, SK0 + 9])
+                                  DIRECT0 + 1, XP0, XP0 + 4, SK0, SK0 + 9, DE0])
 @pytest.mark.parametrize("k", [1, 3])
 def test_conv_poisoned_canary(tile, k):
     """SURVEY §5.2 poisoned-buffer check: the output buffer is NaN-filled, with a NaN
@@ -443,10 +486,10 @@ def test_conv_poisoned_canary(tile, k):
     (a kernel that writes past M/N tails or outside [y_coff, y_coff+cout) fails here)."""
     if STREAM0 <= tile < DIRECT0 and k != 1:
         pytest.skip("v3 tiles take 1x1 GEMMs only")
-    if DIRECT0 <= tile < XP0 and k != 3:
-        pytest.skip("v4 takes 3x3 only")
+    if (DIRECT0 <= tile < XP0 or tile >= DE0) and k != 3:
+        pytest.skip("v4 / v10 take 3x3 only here")
     N, H, W, cin, cout, ldy, y_coff = 3, 13, 11, 64, 72, 104, 16
-    if DIRECT0 <= tile < XP0:
+    if DIRECT0 <= tile < XP0 or tile >= DE0:
         cout = 64  # an instantiated direct shape (64 -> 64 ReLU)
     spec = ConvSpec.auto(cin, cout, k, 1, k // 2, ops.ACT_RELU)
     g = torch.Generator().manual_seed(3)
@@ -490,16 +533,24 @@ def test_conv_poisoned_canary(tile, k):
     (3, 28, 28, 128, 128, 1, ops.ACT_RELU, False, 0, 0, 0, 0),   # ResNet stage-2 conv2 (4 waves)
     (2, 13, 11, 128, 128, 1, ops.ACT_RELU, False, 0, 0, 8, 8),   # band / pixel-block tails
 ])
-@pytest.mark.parametrize("dtile", [0, 1, 3])
+@pytest.mark.parametrize("dtile", [0, 1, 3, "de0", "de1"])
 def test_conv_direct3x3(case, dtile):
     """v4 persistent direct 3x3 conv (csrc/kernels/conv_direct.hip) vs the fp32 reference:
     both strides, odd sizes, channel slices in/out, residual after the activation.
     dtile 0: VGPR-prefetched band patch; 1: the DMA (buffer_load ... lds) double buffer;
-    3: the DMA form at two workgroups per CU (narrow shapes; others fall back to 0/1)."""
+    3: the DMA form at two workgroups per CU (narrow shapes; others fall back to 0/1);
+    de0 / de1: the v10 direct-epilogue forms (accumulators straight to HBM), which refuse
+    every shape they do not instantiate."""
     N, H, W, cin, cout, s, act, res, lx, xc, ly, yc = case
     a = act | (ops.RES_AFTER_ACT if res and act != ops.ACT_NONE else 0)
+    tile = DE0 + int(dtile[2]) if isinstance(dtile, str) else DIRECT0 + dtile
+    if tile >= DE0 and not _de_takes(tile, cin, cout, 3, s, act, res):
+        with pytest.raises(RuntimeError):
+            _conv_case(N, H, W, cin, cout, 3, s, 1, a, res=res, ldx_extra=lx, x_coff=xc,
+                       ldy_extra=ly, y_coff=yc, tile=tile)
+        return
     err, scale = _conv_case(N, H, W, cin, cout, 3, s, 1, a, res=res, ldx_extra=lx, x_coff=xc,
-                            ldy_extra=ly, y_coff=yc, tile=DIRECT0 + dtile)
+                            ldy_extra=ly, y_coff=yc, tile=tile)
     assert err <= 0.02 * scale, (case, err, scale)
 
 
@@ -516,13 +567,19 @@ def test_conv_direct3x3(case, dtile):
     (3, 13, 11, 32, 32, ops.ACT_SILU, 0, 0, 0, 0),       # pixel-block / band tails
     (1, 1, 1, 48, 32, ops.ACT_SILU, 0, 0, 0, 0),
 ])
-@pytest.mark.parametrize("dtile", [0, 1, 3])
+@pytest.mark.parametrize("dtile", [0, 1, 3, "de0", "de1"])
 def test_conv_direct1x1(case, dtile):
     """v4 direct family in its 1x1 form (KK = 1, pad 0) vs the fp32 reference: channel
-    slices in and out, tails, both patch-fetch forms."""
+    slices in and out, tails, both patch-fetch forms, the v10 direct-epilogue forms."""
     N, H, W, cin, cout, act, lx, xc, ly, yc = case
+    tile = DE0 + int(dtile[2]) if isinstance(dtile, str) else DIRECT0 + dtile
+    if tile >= DE0 and not _de_takes(tile, cin, cout, 1, 1, act, False):
+        with pytest.raises(RuntimeError):
+            _conv_case(N, H, W, cin, cout, 1, 1, 0, act, ldx_extra=lx, x_coff=xc,
+                       ldy_extra=ly, y_coff=yc, tile=tile)
+        return
     err, scale = _conv_case(N, H, W, cin, cout, 1, 1, 0, act, ldx_extra=lx, x_coff=xc,
-                            ldy_extra=ly, y_coff=yc, tile=DIRECT0 + dtile)
+                            ldy_extra=ly, y_coff=yc, tile=tile)
     assert err <= 0.02 * scale, (case, err, scale)
 
 
@@ -617,7 +674,7 @@ def test_conv_tail_fused(case, mf):
 
 
 
-@pytest.mark.parametrize("tile", list(range(SK0, N_TILES)))
+@pytest.mark.parametrize("tile", list(range(SK0, DE0)))
 @pytest.mark.parametrize("case", [
     # (N, H, W, cin, cout, k, stride, act, res) -- ResNet-50 edge-batch shapes
     (1, 14, 14, 256, 256, 3, 1, ops.ACT_RELU, False),     # s3 3x3 at batch 1: M 196
