@@ -74,7 +74,7 @@ struct DirectCfg {
 // (dy*2+dx)*4 + c, channel 3 zero) is built on the fly from raw bytes (exact in bf16; the
 // 1/255 scale is folded into the weights), fusing the preprocess pass away.
 #ifndef KV_DIRECT_PD
-#define KV_DIRECT_PD 4
+#define KV_DIRECT_PD 8
 #endif
 constexpr int KPD = KV_DIRECT_PD;
 
@@ -104,7 +104,12 @@ __host__ __device__ constexpr int direct_patch_alloc(int patch_bytes, bool dma) 
 // stem (profiles/r3_v10_yolo_detect_p3_direct_tiles_b192.txt): MFMA phase, store pass and
 // patch wait ran back to back on the only workgroup of the CU.
 template <int CIN, int COUT, int S, int KK, int ACT, bool RES, bool U8 = false, bool DMA = false,
-          bool PAIRS = false, int OCC = 1, int NT = kNT, int C2 = 0, bool DE = false>
+          bool PAIRS = false, int OCC = 1, int NT = kNT, int C2 = 0, bool DE = false,
+          bool SB = false>
+// SB (single patch buffer, DE forms at NT = 256 and two workgroups per CU): each band DMAs
+// its own patch, waits, computes.  No prefetch within a workgroup; the CU's other workgroup
+// runs its MFMA phase meanwhile, so the two band pipelines are not in lockstep (one
+// workgroup of 8 waves syncs every wave of the CU at each band end).
 // OCC = workgroups per CU the launch plans for (1 or 2); the second launch-bounds argument
 // is HIP's minimum waves per SIMD (512 threads = 2 per SIMD per workgroup).  The narrow
 // (16/32-channel) layers are latency-bound at one workgroup per CU -- one band in flight,
@@ -113,9 +118,10 @@ template <int CIN, int COUT, int S, int KK, int ACT, bool RES, bool U8 = false, 
 // pipelines share every CU.  Only the DMA forms fit 128 VGPRs without spilling.
 // NT = 256 (4 waves, one workgroup per CU, one wave per SIMD): the whole 512-entry register
 // file per lane, for weight blocks that do not fit 256 (CIN = 128: 288 weight VGPRs)
-__global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_kernel(const KvConvParams p, int kR,
+__global__ __launch_bounds__(NT, (NT / 256) * OCC) void conv3x3_direct_kernel(const KvConvParams p, int kR,
                                                                 int PW, int patch_rows,
-                                                                FastDiv fPW, FastDiv fWo) {
+                                                                FastDiv fPW, FastDiv fWo,
+                                                                int diag) {
   static_assert(!U8 || (CIN == 16 && KK == 2 && S == 1), "frames-in form: the 2x2 s2d stem");
   static_assert(!PAIRS || U8, "paired raw-row loads: frames-in form only");
   // KK = 1: a 1x1 conv through the same band machinery (pad 0): YOLO's narrow C2f / Detect
@@ -135,9 +141,10 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   static_assert(!(DMA && U8), "DMA patch fetch: bf16 NHWC inputs only");
   static_assert(!DE || (DMA && !RES && C2 == 0 && !U8), "direct epilogue: plain DMA forms");
+  static_assert(!SB || DE, "single patch buffer: direct-epilogue forms");
   const int psz = direct_patch_alloc(patch_rows * PW * C::PB, DMA);
   unsigned char* patch = lds;
-  bf16* otile = reinterpret_cast<bf16*>(lds + (DMA ? 2 * psz : psz));
+  bf16* otile = reinterpret_cast<bf16*>(lds + (DMA && !SB ? 2 * psz : psz));
 
   const int H = p.H, W = p.W, Ho = p.Ho, Wo = p.Wo;
   const int nbands = (Ho + kR - 1) / kR;
@@ -362,7 +369,9 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
         *reinterpret_cast<uint4*>(patch + (q >> 1) * PW * C::PB + (q & 1) * 16) =
             make_uint4(0u, 0u, 0u, 0u);
   }
-  if constexpr (DMA) {
+  if constexpr (SB) {
+    // per band, below
+  } else if constexpr (DMA) {
     dma_fetch(item, patch);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
@@ -375,8 +384,18 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
     const int oy0 = band * kR;
     // next band: in flight during this band's MFMAs (DMA: into the other patch buffer,
     // last read in the previous band, before the barrier that ended it)
-    if constexpr (DMA) dma_fetch(item + gridDim.x, patch + (cur ^ 1) * psz);
-    else fetch(item + gridDim.x);
+    if constexpr (SB) {
+      dma_fetch(item, patch);  // this band's patch (the last band's readers passed the barrier)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else if constexpr (DMA) {
+      // diag bit 1 (KVEDGE_DIRECT_DIAG, timing experiments only: wrong results): no prefetch
+      if (!(DE && (diag & 2))) dma_fetch(item + gridDim.x, patch + (cur ^ 1) * psz);
+    } else {
+      fetch(item + gridDim.x);
+    }
     const unsigned char* pbase = patch + cur * psz;
     // residual of THIS band, loaded now so its HBM latency hides under the MFMA phase
     // (a load in the store pass stalled every band: 69 % of wave cycles waiting on the
@@ -435,7 +454,7 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
       // MFMA of step kk and each MFMA waits for its own read only -- PD reads stay in flight
       // behind the MFMA pipe.  Tap offsets are ds_read immediates off KK (stride 2: 2 KK) row
       // bases; no VALU per MFMA.
-      constexpr int PD = NT == kNT ? (OCC == 2 ? 2 : CIN >= 80 ? 3 : KPD) : 6;
+      constexpr int PD = NT == kNT ? (OCC == 2 ? 2 : CIN >= 80 ? 3 : DMA ? KPD : 4) : 6;
       bf16x8 af[PD + 1];
       unsigned ba[KK], bo[KK];
 #pragma unroll
@@ -458,7 +477,8 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
         if constexpr (kk + PD < C::KS) rd(IC<kk + PD>{});
         constexpr int younger = (C::KS - 1 - kk) < PD ? (C::KS - 1 - kk) : PD;
         lds_wait<younger>(af[kk % (PD + 1)]);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wreg[kk], af[kk % (PD + 1)], acc, 0, 0, 0);
+        if (!(DE && (diag & 4)))  // diag bit 2: no MFMAs
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wreg[kk], af[kk % (PD + 1)], acc, 0, 0, 0);
       });
       const int jr = b * 32 + fr;
       if constexpr (DE) {
@@ -467,6 +487,7 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
         const int oy = oy0 + yl;
         const bool ok = jr < npix && oy < Ho;
         const int base = (((n * Ho + oy) * Wo + xc) * p.ldy + p.y_coff + cb * 32 + fh * 4) * 2;
+        if (diag & 1) continue;  // diag bit 0: no stores (the band-end wait then under-waits)
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -492,7 +513,12 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
         }
       }
     }
-    if constexpr (DE) {
+    if constexpr (SB) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave done reading the patch: the next DMA may land
+      asm volatile("" ::: "memory");
+      continue;
+    } else if constexpr (DE) {
       // this wave's stores of the band (nbw blocks x ng groups) are its youngest vector-memory
       // ops: wait for everything older -- the next band's patch DMAs -- and leave them in flight
       const int nbw = ph < NPH ? (nblk - ph + NPH - 1) / NPH : 0;
@@ -585,9 +611,9 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
         continue;
       }
     }
-    constexpr int SB = SPLIT ? NWD * 64 : 0;  // first storing thread
-    for (int q = C2 > 0 ? npix * OCH : RPF > 0 && rpre ? npix * OCH : tid - SB; q < npix * OCH;
-         q += NT - SB) {
+    constexpr int ST0 = SPLIT ? NWD * 64 : 0;  // first storing thread
+    for (int q = C2 > 0 ? npix * OCH : RPF > 0 && rpre ? npix * OCH : tid - ST0; q < npix * OCH;
+         q += NT - ST0) {
       if (SPLIT && q < 0) break;  // a DMA wave
       const int px = q / OCH, c = q - (q / OCH) * OCH;
       const int yl = fdiv(px, fWo), xc = px - yl * Wo;
@@ -612,7 +638,7 @@ __global__ __launch_bounds__(NT, NT == kNT ? 2 * OCC : 1) void conv3x3_direct_ke
   }
 }
 
-typedef void (*DirectFn)(const KvConvParams, int, int, int, FastDiv, FastDiv);
+typedef void (*DirectFn)(const KvConvParams, int, int, int, FastDiv, FastDiv, int);
 
 struct DirectEntry {
   int cin, cout, stride, kk, act;
@@ -625,6 +651,7 @@ struct DirectEntry {
   int nt = kNT;        // threads per workgroup
   int c2 = 0;          // fused 1x1 pair: its output channels (0 = plain conv)
   bool de = false;     // direct epilogue (v10 tiles; DMA forms only)
+  bool sb = false;     // single patch buffer, 4 waves, two workgroups per CU (v10 tile 2)
 };
 
 #define KV_DIRECT(CI, CO, S, A, R) {CI, CO, S, 3, A, R, conv3x3_direct_kernel<CI, CO, S, 3, A, R>}
@@ -645,6 +672,14 @@ struct DirectEntry {
   {CI, CO, S, KK, A, false,                                                                    \
    conv3x3_direct_kernel<CI, CO, S, KK, A, false, false, true, false, 2, kNT, 0, true>, false,  \
    true, false, 2, kNT, 0, true}
+#define KV_DIRECT_SB(CI, CO, S, KK, A)                                                          \
+  {CI, CO, S, KK, A, false,                                                                    \
+   conv3x3_direct_kernel<CI, CO, S, KK, A, false, false, true, false, 2, 256, 0, true, true>,   \
+   false, true, false, 2, 256, 0, true, true}
+#define KV_DIRECT_DE4(CI, CO, S, KK, A)                                                         \
+  {CI, CO, S, KK, A, false,                                                                    \
+   conv3x3_direct_kernel<CI, CO, S, KK, A, false, false, true, false, 1, 256, 0, true>, false,  \
+   true, false, 1, 256, 0, true}
 #define KV_DIRECT1(CI, CO, A)                                                        \
   {CI, CO, 1, 1, A, false, conv3x3_direct_kernel<CI, CO, 1, 1, A, false>},           \
   {CI, CO, 1, 1, A, false, conv3x3_direct_kernel<CI, CO, 1, 1, A, false, false, true>, false, true}
@@ -717,10 +752,21 @@ static const DirectEntry kDirect[] = {
     KV_DIRECT_DE2(16, 32, 2, 3, kActSilu), KV_DIRECT_DE2(16, 16, 1, 3, kActSilu),
     KV_DIRECT_DE2(32, 64, 2, 3, kActSilu), KV_DIRECT_DE2(32, 32, 1, 3, kActSilu),
     KV_DIRECT_DE2(32, 32, 1, 1, kActSilu), KV_DIRECT_DE2(48, 32, 1, 1, kActSilu),
+    KV_DIRECT_SB(64, 64, 1, 3, kActRelu), KV_DIRECT_SB(64, 128, 1, 3, kActSilu),
+    KV_DIRECT_SB(64, 16, 1, 3, kActSilu), KV_DIRECT_SB(64, 64, 1, 3, kActSilu),
+    KV_DIRECT_SB(64, 128, 2, 3, kActSilu), KV_DIRECT_SB(64, 64, 2, 3, kActSilu),
+    KV_DIRECT_SB(32, 64, 2, 3, kActSilu), KV_DIRECT_SB(32, 32, 1, 3, kActSilu),
+    KV_DIRECT_SB(80, 80, 1, 3, kActSilu),
+    // CIN = 128 at 4 waves, one workgroup per CU (288 weight VGPRs per wave): ResNet-50
+    // stage-2 conv2 and YOLO's 128-channel 3x3s, as v10 tile 0
+    KV_DIRECT_DE4(128, 128, 1, 3, kActRelu), KV_DIRECT_DE4(128, 128, 1, 3, kActSilu),
+    KV_DIRECT_DE4(128, 128, 2, 3, kActSilu),
 };
 #undef KV_DIRECT2
 #undef KV_DIRECT_DE
 #undef KV_DIRECT_DE2
+#undef KV_DIRECT_SB
+#undef KV_DIRECT_DE4
 #undef KV_DIRECT1
 #undef KV_DIRECT_OCC2
 #undef KV_DIRECT_DMA
@@ -736,7 +782,7 @@ int direct_max_patch(int cin) { return (cin >= 80 ? 6 : cin >= 64 ? 7 : 10) * kN
 // Internal codes 4..7 (bit 2) are the direct-epilogue forms, exposed as the v10 tiles
 // (direct_de_launch): they take only their own instantiations, no fallback.
 int direct_num_tiles() { return 4; }
-int direct_de_num_tiles() { return 2; }
+int direct_de_num_tiles() { return 3; }
 
 // Returns the instantiation index for p (or < 0), and the band geometry it would use.
 static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* rows, int* lds) {
@@ -759,6 +805,7 @@ static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* r
           e.act == act && e.res == res && e.u8 == (p->in_u8 != 0) &&
           (!e.u8 || e.pairs == (p->W % 2 == 0)) &&
           e.c2 == (p->pair_1x1 ? p->n_t : 0) && e.de == ((tile & 4) != 0) &&
+          e.sb == ((tile & 8) != 0) &&
           (pass == 1 || (e.dma == ((tile & 1) != 0) && e.occ == 1 + ((tile >> 1) & 1)))) {
         idx = i;
         break;
@@ -781,7 +828,7 @@ static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* r
   // (DMA form: two patch buffers in LDS, no VGPR prefetch budget)
   const bool dma = kDirect[idx].dma;
   auto lds_of = [&](int prows, int r) {
-    const int np = dma ? 2 : 1;
+    const int np = dma && !kDirect[idx].sb ? 2 : 1;
     const int c2p = kDirect[idx].c2;  // pair: b2 slot + W2 [c2][os]
     const int ot = kDirect[idx].de ? 0 : ((r * p->Wo * os * 2 + 15) & ~15);  // output tile
     return np * direct_patch_alloc(prows * *PW * pb, dma) + ot + kBiasBytes +
@@ -805,6 +852,13 @@ static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* r
   return idx;
 }
 
+// KVEDGE_DIRECT_DIAG (timing experiments on the direct-epilogue forms only; outputs are
+// wrong): bit 0 drops the stores, bit 1 the next-band patch prefetch, bit 2 the MFMAs.
+static int direct_diag() {
+  const char* e = getenv("KVEDGE_DIRECT_DIAG");
+  return e ? atoi(e) : 0;
+}
+
 static int direct_launch_one(const KvConvParams* p, int tile, hipStream_t stream) {
   int kR, PW, rows, lds;
   const int idx = direct_plan(p, tile, &kR, &PW, &rows, &lds);
@@ -821,7 +875,7 @@ static int direct_launch_one(const KvConvParams* p, int tile, hipStream_t stream
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
     return -7;
   hipLaunchKernelGGL(fn, dim3(g), dim3(kDirect[idx].nt), (unsigned)lds, stream, *p, kR, PW, rows,
-                     make_fastdiv(PW), make_fastdiv(p->Wo));
+                     make_fastdiv(PW), make_fastdiv(p->Wo), direct_diag());
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }
 
@@ -829,7 +883,7 @@ static int direct_launch_one(const KvConvParams* p, int tile, hipStream_t stream
 // that have one (largest first), e.g. YOLO's merged Detect stem 64 -> 144 = 128 + 16: each
 // slice re-reads the input (cheap: the layer is MFMA-bound) and writes its y_coff range.
 int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
-  if (tile < 0 || tile >= 8) return -6;
+  if (tile < 0 || tile >= 16) return -6;
   int kR, PW, rows, lds;
   if (direct_plan(p, tile, &kR, &PW, &rows, &lds) >= 0) return direct_launch_one(p, tile, stream);
   if (p->res || p->Cout % 16 || p->pair_1x1) return -8;
@@ -862,10 +916,11 @@ int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   return 0;
 }
 
-// v10 tile i: the DMA direct-epilogue form at 1 + i workgroups per CU
+// v10 tile 0 / 1: the DMA direct-epilogue form at 1 / 2 workgroups per CU (8 waves);
+// tile 2: its single-buffer 4-wave form, two workgroups per CU
 int direct_de_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   if (tile < 0 || tile >= direct_de_num_tiles() || p->res || p->pair_1x1) return -8;
-  return direct_launch(p, 4 | 1 | (tile << 1), stream);
+  return direct_launch(p, tile == 2 ? (4 | 8 | 2 | 1) : (4 | 1 | (tile << 1)), stream);
 }
 
 }  // namespace kvedge

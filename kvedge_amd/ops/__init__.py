@@ -207,7 +207,7 @@ _WS: dict = {}
 SPLITK_MAX_ELEMS = 32 << 20  # 128 MB of fp32 per stream at most
 SPLITK_MAX_SPLIT = 32        # largest split of conv_sk.hip kSkTiles
 N_SPLITK_TILES = 19          # conv_sk.hip kSkTiles
-N_DE_TILES = 2               # v10 direct-epilogue tiles (conv_direct.hip): after split-K, last
+N_DE_TILES = 3               # v10 direct-epilogue tiles (conv_direct.hip): after split-K, last
 SPLITK0 = 1 << 30            # first split-K tile index, set by load()
 
 

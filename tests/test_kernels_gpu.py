@@ -103,14 +103,15 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale
 
 
-N_TILES = 107  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue / N-160 (68-85) + v8 split-K (86-104) + v10 (105-106)
+N_TILES = 108  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue / N-160 (68-85) + v8 split-K (86-104) + v10 (105-107)
 # + v6 A-resident N-loop 1x1 GEMM (58-67, conv_nloop.hip kNlTiles: one Kpad per tile;
 # 63-65 are the fused-downsample (dual) forms, 66-67 step 128 K at a time)
 NLOOP0 = 58
 XP0 = 68  # v7: the v2 kernel's cross-stage pipelined loop (BK 32 rings, 8 waves)
 SK0 = 86  # v8: split-K (conv_sk.hip kSkTiles): K slices per tile (clamped to the K steps)
-DE0 = 105  # v10: the direct family's direct-epilogue forms (conv_direct.hip), 1 / 2 workgroups per CU
-# (cin, cout, k, stride, act) instantiated as v10 tile 0 / tile 1 (no residual, no fallback)
+DE0 = 105  # v10: the direct family's direct-epilogue forms (conv_direct.hip): 8 waves at 1 / 2
+# workgroups per CU, then the single-patch-buffer 4-wave form at 2 per CU
+# (cin, cout, k, stride, act) instantiated as v10 tile 0 / 1 / 2 (no residual, no fallback)
 DE_SHAPES = {
     0: {(64, 64, 3, 1, ops.ACT_RELU), (64, 128, 3, 1, ops.ACT_SILU), (64, 16, 3, 1, ops.ACT_SILU),
         (64, 64, 3, 1, ops.ACT_SILU), (80, 80, 3, 1, ops.ACT_SILU), (64, 128, 3, 2, ops.ACT_SILU),
@@ -118,9 +119,13 @@ DE_SHAPES = {
         (32, 32, 3, 1, ops.ACT_SILU), (16, 16, 3, 1, ops.ACT_SILU), (32, 32, 1, 1, ops.ACT_SILU),
         (48, 32, 1, 1, ops.ACT_SILU), (64, 64, 1, 1, ops.ACT_SILU), (128, 64, 1, 1, ops.ACT_SILU),
         (192, 64, 1, 1, ops.ACT_SILU), (96, 64, 1, 1, ops.ACT_SILU), (64, 64, 1, 1, ops.ACT_NONE),
-        (80, 80, 1, 1, ops.ACT_NONE)},
+        (80, 80, 1, 1, ops.ACT_NONE), (128, 128, 3, 1, ops.ACT_RELU), (128, 128, 3, 1, ops.ACT_SILU),
+        (128, 128, 3, 2, ops.ACT_SILU)},
     1: {(16, 32, 3, 2, ops.ACT_SILU), (16, 16, 3, 1, ops.ACT_SILU), (32, 64, 3, 2, ops.ACT_SILU),
         (32, 32, 3, 1, ops.ACT_SILU), (32, 32, 1, 1, ops.ACT_SILU), (48, 32, 1, 1, ops.ACT_SILU)},
+    2: {(64, 64, 3, 1, ops.ACT_RELU), (64, 128, 3, 1, ops.ACT_SILU), (64, 16, 3, 1, ops.ACT_SILU),
+        (64, 64, 3, 1, ops.ACT_SILU), (64, 128, 3, 2, ops.ACT_SILU), (64, 64, 3, 2, ops.ACT_SILU),
+        (32, 64, 3, 2, ops.ACT_SILU), (32, 32, 3, 1, ops.ACT_SILU), (80, 80, 3, 1, ops.ACT_SILU)},
 }
 
 
@@ -477,7 +482,7 @@ def test_conv_dual_rejects_v1_tiles():
 
 
 @pytest.mark.parametrize("tile", [-1, 1, 6, 7, 12, 13, STREAM0, STREAM0 + 1, STREAM0 + 5, DIRECT0,
-                                  DIRECT0 + 1, XP0, XP0 + 4, SK0, SK0 + 9, DE0])
+                                  DIRECT0 + 1, XP0, XP0 + 4, SK0, SK0 + 9, DE0, DE0 + 2])
 @pytest.mark.parametrize("k", [1, 3])
 def test_conv_poisoned_canary(tile, k):
     """SURVEY §5.2 poisoned-buffer check: the output buffer is NaN-filled, with a NaN
@@ -532,8 +537,10 @@ def test_conv_poisoned_canary(tile, k):
     (2, 40, 40, 80, 80, 1, ops.ACT_SILU, False, 64, 64, 0, 0),   # Detect P4 cls
     (3, 28, 28, 128, 128, 1, ops.ACT_RELU, False, 0, 0, 0, 0),   # ResNet stage-2 conv2 (4 waves)
     (2, 13, 11, 128, 128, 1, ops.ACT_RELU, False, 0, 0, 8, 8),   # band / pixel-block tails
+    (2, 20, 20, 128, 128, 1, ops.ACT_SILU, False, 0, 0, 0, 0),   # YOLO P5 3x3 (v10 only)
+    (2, 41, 39, 128, 128, 2, ops.ACT_SILU, False, 0, 0, 8, 8),   # YOLO PAN downsample (v10 only)
 ])
-@pytest.mark.parametrize("dtile", [0, 1, 3, "de0", "de1"])
+@pytest.mark.parametrize("dtile", [0, 1, 3, "de0", "de1", "de2"])
 def test_conv_direct3x3(case, dtile):
     """v4 persistent direct 3x3 conv (csrc/kernels/conv_direct.hip) vs the fp32 reference:
     both strides, odd sizes, channel slices in/out, residual after the activation.
@@ -544,7 +551,8 @@ def test_conv_direct3x3(case, dtile):
     N, H, W, cin, cout, s, act, res, lx, xc, ly, yc = case
     a = act | (ops.RES_AFTER_ACT if res and act != ops.ACT_NONE else 0)
     tile = DE0 + int(dtile[2]) if isinstance(dtile, str) else DIRECT0 + dtile
-    if tile >= DE0 and not _de_takes(tile, cin, cout, 3, s, act, res):
+    v10_only = (cin, cout, s, act) in {(128, 128, 1, ops.ACT_SILU), (128, 128, 2, ops.ACT_SILU)}
+    if (tile >= DE0 and not _de_takes(tile, cin, cout, 3, s, act, res)) or (tile < DE0 and v10_only):
         with pytest.raises(RuntimeError):
             _conv_case(N, H, W, cin, cout, 3, s, 1, a, res=res, ldx_extra=lx, x_coff=xc,
                        ldy_extra=ly, y_coff=yc, tile=tile)
@@ -567,7 +575,7 @@ def test_conv_direct3x3(case, dtile):
     (3, 13, 11, 32, 32, ops.ACT_SILU, 0, 0, 0, 0),       # pixel-block / band tails
     (1, 1, 1, 48, 32, ops.ACT_SILU, 0, 0, 0, 0),
 ])
-@pytest.mark.parametrize("dtile", [0, 1, 3, "de0", "de1"])
+@pytest.mark.parametrize("dtile", [0, 1, 3, "de0", "de1", "de2"])
 def test_conv_direct1x1(case, dtile):
     """v4 direct family in its 1x1 form (KK = 1, pad 0) vs the fp32 reference: channel
     slices in and out, tails, both patch-fetch forms, the v10 direct-epilogue forms."""
