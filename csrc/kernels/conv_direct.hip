@@ -142,6 +142,7 @@ __global__ __launch_bounds__(NT, (NT / 256) * OCC) void conv3x3_direct_kernel(co
   static_assert(!(DMA && U8), "DMA patch fetch: bf16 NHWC inputs only");
   static_assert(!DE || (DMA && !RES && C2 == 0 && !U8), "direct epilogue: plain DMA forms");
   static_assert(!SB || DE, "single patch buffer: direct-epilogue forms");
+  static_assert(!DE || COUT % 16 == 0, "direct epilogue: 16-channel store pairs");
   const int psz = direct_patch_alloc(patch_rows * PW * C::PB, DMA);
   unsigned char* patch = lds;
   bf16* otile = reinterpret_cast<bf16*>(lds + (DMA && !SB ? 2 * psz : psz));
@@ -482,21 +483,49 @@ __global__ __launch_bounds__(NT, (NT / 256) * OCC) void conv3x3_direct_kernel(co
       });
       const int jr = b * 32 + fr;
       if constexpr (DE) {
-        // lanes fr / fr + 32 write channels [g*8, g*8+4) / [g*8+4, g*8+8) of pixel jr: 16
-        // contiguous bytes per pixel and instruction; L2 merges the 4 groups' lines
         const int oy = oy0 + yl;
         const bool ok = jr < npix && oy < Ho;
-        const int base = (((n * Ho + oy) * Wo + xc) * p.ldy + p.y_coff + cb * 32 + fh * 4) * 2;
         if (diag & 1) continue;  // diag bit 0: no stores (the band-end wait then under-waits)
+        const int pix = (((n * Ho + oy) * Wo + xc) * p.ldy + p.y_coff + cb * 32) * 2;
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        if (diag & 8) {
+          // diag bit 3: the first DE store form, 4 x 8 B per lane (lanes fr / fr + 32: channels
+          // [g*8, g*8+4) / [g*8+4, g*8+8)), 32 16-B segments per instruction
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          if (cb * 32 + g * 8 >= COUT) continue;  // wave-uniform; counted in nst below
-          bf16x4 o;
+          for (int g = 0; g < 4; ++g) {
+            if (cb * 32 + g * 8 >= COUT) continue;
+            bf16x4 o;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = f2bf(act_c<ACT>(acc[4 * g + e]));
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ry,
-                                                ok ? base + g * 16 : kOOB, 0, 0);
+            for (int e = 0; e < 4; ++e) o[e] = f2bf(act_c<ACT>(acc[4 * g + e]));
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), ry,
+                                                  ok ? pix + (g * 8 + fh * 4) * 2 : kOOB, 0, 0);
+          }
+          continue;
+        }
+        // Half-wave exchange, then 16 B per lane: for the group pair (2q, 2q+1) lane fr ends
+        // with channels [16q, 16q+8) of pixel jr and lane fr + 32 with [16q+8, 16q+16).  One
+        // store instruction writes 32 pixels x 32 contiguous bytes (the 4 x 8-B form: 32 x 16 B).
+        // Same box, 2-5 % faster than the 8-B form; the stores still cost ~80 of 250 us on the
+        // Detect P3 stem slice (profiles/r4_v3_direct_diag.txt).
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if (cb * 32 + q * 16 >= COUT) continue;  // wave-uniform (COUT % 16 == 0); counted below
+          bf16x4 lo, hi;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            lo[e] = f2bf(act_c<ACT>(acc[8 * q + e]));      // group 2q: channels 16q + fh*4 + e
+            hi[e] = f2bf(act_c<ACT>(acc[8 * q + 4 + e]));  // group 2q+1: 16q + 8 + fh*4 + e
+          }
+          // v_permlane32_swap(a, b): a's lanes 32-63 <-> b's lanes 0-31.  Lane fr then holds
+          // (a: own [16q, +4), b: partner's [16q+4, +4)), lane fr + 32 (a: partner's
+          // [16q+8, +4), b: own [16q+12, +4)) -- 8 consecutive channels each, no LDS trip
+          const u32x2 a0 = __builtin_bit_cast(u32x2, lo), a1 = __builtin_bit_cast(u32x2, hi);
+          const auto s0 = __builtin_amdgcn_permlane32_swap(a0[0], a1[0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane32_swap(a0[1], a1[1], false, false);
+          const u32x4 v = u32x4{s0[0], s1[0], s0[1], s1[1]};
+          __builtin_amdgcn_raw_buffer_store_b128(v, ry, ok ? pix + (q * 16 + fh * 8) * 2 : kOOB, 0,
+                                                 0);
         }
         continue;
       }
@@ -522,7 +551,7 @@ __global__ __launch_bounds__(NT, (NT / 256) * OCC) void conv3x3_direct_kernel(co
       // this wave's stores of the band (nbw blocks x ng groups) are its youngest vector-memory
       // ops: wait for everything older -- the next band's patch DMAs -- and leave them in flight
       const int nbw = ph < NPH ? (nblk - ph + NPH - 1) / NPH : 0;
-      const int ng = min(4, (COUT - cb * 32 + 7) / 8);
+      const int ng = (diag & 8) ? min(4, (COUT - cb * 32 + 7) / 8) : min(2, (COUT - cb * 32 + 15) / 16);
       direct_wait_vm_le(__builtin_amdgcn_readfirstlane(nbw * ng));
       cur ^= 1;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -852,8 +881,9 @@ static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* r
   return idx;
 }
 
-// KVEDGE_DIRECT_DIAG (timing experiments on the direct-epilogue forms only; outputs are
-// wrong): bit 0 drops the stores, bit 1 the next-band patch prefetch, bit 2 the MFMAs.
+// KVEDGE_DIRECT_DIAG (timing experiments on the direct-epilogue forms only; bits 0-2 make
+// the outputs wrong): bit 0 drops the stores, bit 1 the next-band patch prefetch, bit 2 the
+// MFMAs; bit 3 selects the first (4 x 8-B) store form, for same-box A/B.
 static int direct_diag() {
   const char* e = getenv("KVEDGE_DIRECT_DIAG");
   return e ? atoi(e) : 0;
@@ -920,7 +950,8 @@ int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
 // tile 2: its single-buffer 4-wave form, two workgroups per CU
 int direct_de_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   if (tile < 0 || tile >= direct_de_num_tiles() || p->res || p->pair_1x1) return -8;
-  return direct_launch(p, tile == 2 ? (4 | 8 | 2 | 1) : (4 | 1 | (tile << 1)), stream);
+  static const int code[3] = {4 | 1, 4 | 2 | 1, 4 | 8 | 2 | 1};
+  return direct_launch(p, code[tile], stream);
 }
 
 }  // namespace kvedge

@@ -110,7 +110,7 @@ NLOOP0 = 58
 XP0 = 68  # v7: the v2 kernel's cross-stage pipelined loop (BK 32 rings, 8 waves)
 SK0 = 86  # v8: split-K (conv_sk.hip kSkTiles): K slices per tile (clamped to the K steps)
 DE0 = 105  # v10: the direct family's direct-epilogue forms (conv_direct.hip): 8 waves at 1 / 2
-# workgroups per CU, then the single-patch-buffer 4-wave form at 2 per CU
+# workgroups per CU, the single-patch-buffer 4-wave form at 2 per CU
 # (cin, cout, k, stride, act) instantiated as v10 tile 0 / 1 / 2 (no residual, no fallback)
 DE_SHAPES = {
     0: {(64, 64, 3, 1, ops.ACT_RELU), (64, 128, 3, 1, ops.ACT_SILU), (64, 16, 3, 1, ops.ACT_SILU),
