@@ -69,7 +69,9 @@ struct SmSched {
   static constexpr int kB = KB, kR = 2, kS = 2, kA = NA;  // NA: A-chunk DMAs per wave
   static constexpr int kFar = 12;
   static constexpr int kTiles = kFar + 2;
-  // kind 0: wait before reading ring stage s; kind 1: wait before tile t's epilogue
+  // kind 0: wait before reading ring stage s; kind 1: wait before tile t's epilogue;
+  // kind 2 (XP): the wait at step s that covers stage s + 1 (its fragments are read during
+  // step s, one step ahead of their MFMAs)
   static constexpr int wait(int kind, int idx) {
     long endB[kTiles * SPT + D + 2] = {};
     long endR[kTiles + RD + 2] = {};
@@ -84,6 +86,7 @@ struct SmSched {
           pos += kS;
         }
         if (kind == 0 && idx == s) return (int)(pos - endB[s]);
+        if (kind == 2 && idx == s) return D >= 3 ? (int)(pos - endB[s + 1]) : -1;
         endB[s + D - 1] = (pos += kB);
         if (j == 0) endR[t + RD - 1] = (pos += kR);
       }
@@ -92,11 +95,13 @@ struct SmSched {
   }
   static constexpr int wB(int t, int j) { return wait(0, t * SPT + j); }
   static constexpr int wE(int t) { return wait(1, t); }
+  static constexpr int wXB(int t, int j) { return wait(2, t * SPT + j); }
   static constexpr int steady_from() {
     int t0 = 0;
     for (int t = 0; t < kFar; ++t) {
       bool same = wE(t) == wE(kFar);
-      for (int j = 0; j < SPT; ++j) same = same && wB(t, j) == wB(kFar, j);
+      for (int j = 0; j < SPT; ++j)
+        same = same && wB(t, j) == wB(kFar, j) && wXB(t, j) == wXB(kFar, j);
       if (!same) t0 = t + 1;
     }
     return t0;
@@ -107,16 +112,23 @@ struct SmSched {
     for (int t = 0; t <= kSteady; ++t) m = wB(t, j) < m ? wB(t, j) : m;
     return m;
   }
+  static constexpr int safe_XB(int j) {
+    int m = wXB(kFar, j);
+    for (int t = 0; t <= kSteady; ++t) m = wXB(t, j) < m ? wXB(t, j) : m;
+    return m;
+  }
   static constexpr int safe_E() {
     int m = wE(kFar);
     for (int t = 0; t <= kSteady; ++t) m = wE(t) < m ? wE(t) : m;
     return m;
   }
-  static constexpr bool ok() {
+  static constexpr bool ok(bool xp = false) {
     for (int t = 0; t <= kFar; ++t) {
       if (wE(t) < 0 || wE(t) > 63) return false;
-      for (int j = 0; j < SPT; ++j)
+      for (int j = 0; j < SPT; ++j) {
         if (wB(t, j) < 0 || wB(t, j) > 63) return false;
+        if (xp && (wXB(t, j) < 0 || wXB(t, j) > 63)) return false;
+      }
     }
     return kSteady < kFar;
   }
@@ -141,14 +153,22 @@ __device__ __forceinline__ void sm_lds_barrier() {
 // instead of LDS: the conv3 steps then read only weight fragments from LDS (0.5 ds_read_b128
 // per MFMA instead of 1.0 -- the LDS-bound part of the step), and the freed LDS deepens the
 // weight ring.
-template <int NC3, int NZC, int D, int RD, int NW = 8, int KS2 = 1, bool AREG = false>
+// XP (AREG forms): cross-step fragment prefetch.  The wait + barrier at step s covers ring
+// stage s + 1, and step s reads stage s + 1's weight fragments into the other register set
+// while its own MFMAs consume the set read during step s - 1: no step starts with an LDS
+// round trip behind the barrier (the conv1 steps' y-tile A reads stay in-step: y is written
+// by the epilogue at the start of the tile's first conv1 step).
+template <int NC3, int NZC, int D, int RD, int NW = 8, int KS2 = 1, bool AREG = false,
+          bool XP = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(const KvConvParams p, int ntiles) {
   static_assert(NW == 4 || NW == 8, "waves");
   static_assert(NC3 % KS2 == 0 && NZC % KS2 == 0, "whole chunks per ring stage");
   constexpr int SY = NC3 / KS2, SZ = NZC / KS2, BPW = 8 / NW;  // BPW: DMAs per wave per chunk
   using S = SmSched<SY, SZ, D, RD, KS2 * BPW, AREG ? 0 : 2 * NC3>;
-  static_assert(S::ok(), "counted-wait schedule out of range or not periodic");
+  static_assert(S::ok(XP), "counted-wait schedule out of range or not periodic");
   constexpr int SPT = S::SPT, BM = 16 * NW, NT = 64 * NW;
+  static_assert(!XP || (AREG && D >= 3 && SPT % 2 == 0),
+                "XP: A in VGPRs, stage s + 1 issued before step s, register sets by step parity");
   constexpr int A_BYTES = AREG ? 0 : NC3 * BM * 128, B_CHUNK = 64 * 128, B_STAGE = KS2 * B_CHUNK;
   constexpr int R_SLOT = BM * 64 * 2;
   constexpr int B_OFF = A_BYTES, R_OFF = B_OFF + D * B_STAGE, BIAS_OFF = R_OFF + RD * R_SLOT;
@@ -345,6 +365,50 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(con
     }
   };
 
+  // XP: weight fragments of one ring stage, [c][ks][tn], two sets by step parity
+  bf16x8 bset[XP ? 2 : 1][XP ? KS2 : 1][2][2];
+  auto read_B = [&](bf16x8 (&dst)[XP ? KS2 : 1][2][2], const char* Bs) __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < (XP ? KS2 : 1); ++c)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {
+          const int row = wn * 32 + tn * 16 + fr, q = ks * 4 + fh;
+          dst[c][ks][tn] =
+              *reinterpret_cast<const bf16x8*>(Bs + c * B_CHUNK + row * 128 + ((q ^ sm_sw(row)) << 4));
+        }
+  };
+  // one 64-deep K chunk with B from registers: A from VGPRs (conv3) or from LDS (conv1: y)
+  auto mma_xr = [&](const bf16x8 (&b)[2][2], const bf16x8 (&a)[2][2], floatx4 (&c)[2][2])
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+          c[tn][tm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][tn], a[ks][tm], c[tn][tm], 0, 0, 0);
+  };
+  auto mma_xl = [&](const bf16x8 (&b)[2][2], const char* As, floatx4 (&c)[2][2])
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int q = ks * 4 + fh;
+      bf16x8 af[2];
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm) {
+        const int row = wm * 32 + tm * 16 + fr;
+        af[tm] = *reinterpret_cast<const bf16x8*>(As + row * 128 + ((q ^ sm_sw(row)) << 4));
+      }
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+          c[tn][tm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[ks][tn], af[tm], c[tn][tm], 0, 0, 0);
+    }
+  };
+
   dispatch_act(p.act, true, [&](auto A1, auto A2) __attribute__((always_inline)) {
     constexpr int act1 = decltype(A1)::value, act2 = decltype(A2)::value;
     for (int t = 0; t < ntiles; ++t) {
@@ -394,18 +458,36 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(con
 #pragma unroll
             for (int b = 0; b < 2; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
         }
-        if (warm) sm_wait_vm<S::safe_B(j)>();
-        else sm_wait_vm<S::wB(S::kFar, j)>();
+        if constexpr (XP) {
+          if (warm) sm_wait_vm<S::safe_XB(j)>();
+          else sm_wait_vm<S::wXB(S::kFar, j)>();
+        } else {
+          if (warm) sm_wait_vm<S::safe_B(j)>();
+          else sm_wait_vm<S::wB(S::kFar, j)>();
+        }
         sm_lds_barrier();  // WAR: every wave's reads of the slot about to be refilled retired
         constexpr int jn = (j + D - 1) % SPT, tadv = (j + D - 1) / SPT;
         issue_B(t + tadv, SmIC<jn>{});
         if constexpr (j == 0) issue_R(t + RD - 1);
         const char* Bs = lds + B_OFF + (s % D) * B_STAGE;
+        if constexpr (XP) {
+          constexpr int cur = j & 1, nxt = cur ^ 1;  // SPT even: parity of s == parity of j
+          if constexpr (j == 0) {
+            if (t == 0) read_B(bset[cur], Bs);  // the first step has no predecessor
+          }
+          read_B(bset[nxt], lds + B_OFF + ((s + 1) % D) * B_STAGE);  // stage s + 1 landed
 #pragma unroll
-        for (int c = 0; c < KS2; ++c) {
-          if constexpr (j < SY && AREG) mma64r(0, areg[j * KS2 + c], Bs + c * B_CHUNK, acc);
-          else if constexpr (j < SY) mma64(lds + (j * KS2 + c) * (BM * 128), Bs + c * B_CHUNK, acc);
-          else mma64(Rs, Bs + c * B_CHUNK, accz[(j - SY) * KS2 + c]);
+          for (int c = 0; c < KS2; ++c) {
+            if constexpr (j < SY) mma_xr(bset[cur][c], areg[j * KS2 + c], acc);
+            else mma_xl(bset[cur][c], Rs, accz[(j - SY) * KS2 + c]);
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < KS2; ++c) {
+            if constexpr (j < SY && AREG) mma64r(0, areg[j * KS2 + c], Bs + c * B_CHUNK, acc);
+            else if constexpr (j < SY) mma64(lds + (j * KS2 + c) * (BM * 128), Bs + c * B_CHUNK, acc);
+            else mma64(Rs, Bs + c * B_CHUNK, accz[(j - SY) * KS2 + c]);
+          }
         }
       });
     }
@@ -464,9 +546,11 @@ struct SmTile {
   SmFn fn;
 };
 
-template <int NC3, int NZC, int D, int RD, int NW = 8, int KS2 = 1, bool AREG = false>
+template <int NC3, int NZC, int D, int RD, int NW = 8, int KS2 = 1, bool AREG = false,
+          bool XP = false>
 constexpr SmTile sm_tile() {
-  return SmTile{NC3, NZC, D, RD, NW, KS2, AREG ? 1 : 0, &conv_seam_kernel<NC3, NZC, D, RD, NW, KS2, AREG>};
+  return SmTile{NC3, NZC, D, RD, NW, KS2, AREG ? 1 : 0,
+                &conv_seam_kernel<NC3, NZC, D, RD, NW, KS2, AREG, XP>};
 }
 
 // LDS = A (K3 x BM x 2) + d x ks2 x 8 KB ring + rd x BM x 128 B residual ring + bias tables.
@@ -497,6 +581,11 @@ static const SmTile kSmTiles[] = {
     sm_tile<4, 4, 3, 5, 8, 2, true>(),
     // stage 3 -> 4 (N1 512): not taken by the model (level with unfused at b640)
     sm_tile<4, 8, 4, 3>(),
+    // XP: cross-step weight-fragment prefetch (A in VGPRs)
+    sm_tile<2, 2, 6, 3, 4, 1, true, true>(),
+    sm_tile<2, 2, 6, 3, 8, 2, true, true>(),
+    sm_tile<2, 4, 6, 3, 8, 1, true, true>(),
+    sm_tile<4, 4, 4, 4, 8, 2, true, true>(),
 };
 
 int sm_lds_bytes(const SmTile& e, int cout, int n1) {
