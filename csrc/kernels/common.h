@@ -90,10 +90,10 @@ __device__ __forceinline__ void kv_settle(T& v) {
 template <int I>
 struct IC;
 template <int B, int E, class F>
-__device__ __forceinline__ void static_for(F&& f) {
+__device__ __forceinline__ void static_range(F&& f) {
   if constexpr (B < E) {
     f(IC<B>{});
-    static_for<B + 1, E>(f);
+    static_range<B + 1, E>(f);
   }
 }
 

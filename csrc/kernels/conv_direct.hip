@@ -472,8 +472,8 @@ __global__ __launch_bounds__(NT, (NT / 256) * OCC) void conv3x3_direct_kernel(co
         else
           lds_read16<(S == 2 ? s / 2 : s) * C::PB + s4 * 32>(af[kk % (PD + 1)], ba[r]);
       };
-      static_for<0, (PD < C::KS ? PD : C::KS)>(rd);
-      static_for<0, C::KS>([&](auto kc) __attribute__((always_inline)) {
+      static_range<0, (PD < C::KS ? PD : C::KS)>(rd);
+      static_range<0, C::KS>([&](auto kc) __attribute__((always_inline)) {
         constexpr int kk = decltype(kc)::value;
         if constexpr (kk + PD < C::KS) rd(IC<kk + PD>{});
         constexpr int younger = (C::KS - 1 - kk) < PD ? (C::KS - 1 - kk) : PD;

@@ -301,7 +301,7 @@ void conv_stream_kernel(const KvConvParams p) {
     // right before its MFMAs, and an lgkmcnt(0) sat in front of most of them (tools/isa_lint.py:
     // 59 % of this kernel's MFMAs at NT1 = 128)
     constexpr int KK2 = BN / 16, RPS = 1 + TN1;          // steps, reads per step
-    constexpr int PD2 = (15 / RPS) < 4 ? (15 / RPS) : 4;  // lgkmcnt holds at most 15
+    constexpr int PD2 = TN1 == 1 ? 2 : 3;  // RPS x PD2 <= 15 (lgkmcnt); NT1 = 64 sits at 512 VGPRs
     bf16x8 ar[PD2 + 1], br[PD2 + 1][TN1];
     const unsigned a_base = lds_addr(Cs + (wm2 * 32 + fr32) * CS + fh32 * 8);
     unsigned b_base[TN1][4];  // per (tn, kk & 3): the swizzled 16-B column of this lane's row
@@ -319,8 +319,8 @@ void conv_stream_kernel(const KvConvParams p) {
       for (int tn = 0; tn < TN1; ++tn)  // kt = kk / 4 blocks of [NT1][64] bf16 apart
         lds_read16<0>(br[sl][tn], b_base[tn][kk & 3] + (kk >> 2) * NT1 * BK * 2);
     };
-    static_for<0, (PD2 < KK2 ? PD2 : KK2)>(rd2);
-    static_for<0, KK2>([&](auto kc) __attribute__((always_inline)) {
+    static_range<0, (PD2 < KK2 ? PD2 : KK2)>(rd2);
+    static_range<0, KK2>([&](auto kc) __attribute__((always_inline)) {
       constexpr int kk = decltype(kc)::value, sl = kk % (PD2 + 1);
       if constexpr (kk + PD2 < KK2) rd2(IC<kk + PD2>{});
       constexpr int later = (KK2 - 1 - kk) < PD2 ? (KK2 - 1 - kk) : PD2;
