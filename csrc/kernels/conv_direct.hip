@@ -789,7 +789,7 @@ static const DirectEntry kDirect[] = {
     // CIN = 128 at 4 waves, one workgroup per CU (288 weight VGPRs per wave): ResNet-50
     // stage-2 conv2 and YOLO's 128-channel 3x3s, as v10 tile 0
     KV_DIRECT_DE4(128, 128, 1, 3, kActRelu), KV_DIRECT_DE4(128, 128, 1, 3, kActSilu),
-    KV_DIRECT_DE4(128, 128, 2, 3, kActSilu), KV_DIRECT_DE4(128, 128, 2, 3, kActRelu),
+    KV_DIRECT_DE4(128, 128, 2, 3, kActSilu),
 };
 #undef KV_DIRECT2
 #undef KV_DIRECT_DE

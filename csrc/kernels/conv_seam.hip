@@ -568,10 +568,12 @@ static const SmTile kSmTiles[] = {
     // stage 2 -> 3 (N1 256): A in VGPRs, 16-KB stages first (388 vs 408 us, 414 unfused)
     sm_tile<2, 4, 6, 3, 8, 2, true>(),
     sm_tile<2, 4, 6, 3>(),
-    // stage 3 (K3 256, Cout 1024 -> N1 256): A in VGPRs with a 4-slot residual ring first --
-    // 3 tiles (48 KB) of residual in flight per CU: 197.5 vs 202.8 us for the 16-KB-stage
-    // form and 216 unfused (profiles/r4_v3_seam_probe_b640.md; the same deeper ring lost
-    // on stage 2, whose 4-wave form already holds two workgroups' rings per CU)
+    // stage 3 (K3 256, Cout 1024 -> N1 256): A in VGPRs with a 4-slot residual ring (3 tiles,
+    // 48 KB, of residual in flight per CU) and the cross-step weight-fragment prefetch first:
+    // 193.4 us vs 198.6 without the prefetch, 224 unfused (profiles/r4_v4_seam_probe_b640.md).
+    // The prefetch lost on the stage-2 forms (327 vs 321 us, 401 vs 385 at 2 -> 3) and was
+    // dropped there; the deeper residual ring lost on stage 2 too (r4_v3 probe)
+    sm_tile<4, 4, 4, 4, 8, 2, true, true>(),
     sm_tile<4, 4, 4, 4, 8, 2, true>(),
     sm_tile<4, 4, 3, 2, 8, 2>(),
     sm_tile<4, 4, 5, 2>(),
@@ -581,11 +583,6 @@ static const SmTile kSmTiles[] = {
     sm_tile<4, 4, 3, 5, 8, 2, true>(),
     // stage 3 -> 4 (N1 512): not taken by the model (level with unfused at b640)
     sm_tile<4, 8, 4, 3>(),
-    // XP: cross-step weight-fragment prefetch (A in VGPRs)
-    sm_tile<2, 2, 6, 3, 4, 1, true, true>(),
-    sm_tile<2, 2, 6, 3, 8, 2, true, true>(),
-    sm_tile<2, 4, 6, 3, 8, 1, true, true>(),
-    sm_tile<4, 4, 4, 4, 8, 2, true, true>(),
 };
 
 int sm_lds_bytes(const SmTile& e, int cout, int n1) {

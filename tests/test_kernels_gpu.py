@@ -120,7 +120,7 @@ DE_SHAPES = {
         (48, 32, 1, 1, ops.ACT_SILU), (64, 64, 1, 1, ops.ACT_SILU), (128, 64, 1, 1, ops.ACT_SILU),
         (192, 64, 1, 1, ops.ACT_SILU), (96, 64, 1, 1, ops.ACT_SILU), (64, 64, 1, 1, ops.ACT_NONE),
         (80, 80, 1, 1, ops.ACT_NONE), (128, 128, 3, 1, ops.ACT_RELU), (128, 128, 3, 1, ops.ACT_SILU),
-        (128, 128, 3, 2, ops.ACT_SILU), (128, 128, 3, 2, ops.ACT_RELU)},
+        (128, 128, 3, 2, ops.ACT_SILU)},
     1: {(16, 32, 3, 2, ops.ACT_SILU), (16, 16, 3, 1, ops.ACT_SILU), (32, 64, 3, 2, ops.ACT_SILU),
         (32, 32, 3, 1, ops.ACT_SILU), (32, 32, 1, 1, ops.ACT_SILU), (48, 32, 1, 1, ops.ACT_SILU)},
     2: {(64, 64, 3, 1, ops.ACT_RELU), (64, 128, 3, 1, ops.ACT_SILU), (64, 16, 3, 1, ops.ACT_SILU),
@@ -539,7 +539,6 @@ def test_conv_poisoned_canary(tile, k):
     (2, 13, 11, 128, 128, 1, ops.ACT_RELU, False, 0, 0, 8, 8),   # band / pixel-block tails
     (2, 20, 20, 128, 128, 1, ops.ACT_SILU, False, 0, 0, 0, 0),   # YOLO P5 3x3 (v10 only)
     (2, 41, 39, 128, 128, 2, ops.ACT_SILU, False, 0, 0, 8, 8),   # YOLO PAN downsample (v10 only)
-    (2, 56, 56, 128, 128, 2, ops.ACT_RELU, False, 0, 0, 0, 0),   # ResNet stage-2 b0 conv2 (v10 only)
 ])
 @pytest.mark.parametrize("dtile", [0, 1, 3, "de0", "de1", "de2"])
 def test_conv_direct3x3(case, dtile):
@@ -552,8 +551,7 @@ def test_conv_direct3x3(case, dtile):
     N, H, W, cin, cout, s, act, res, lx, xc, ly, yc = case
     a = act | (ops.RES_AFTER_ACT if res and act != ops.ACT_NONE else 0)
     tile = DE0 + int(dtile[2]) if isinstance(dtile, str) else DIRECT0 + dtile
-    v10_only = (cin, cout, s, act) in {(128, 128, 1, ops.ACT_SILU), (128, 128, 2, ops.ACT_SILU),
-                                       (128, 128, 2, ops.ACT_RELU)}
+    v10_only = (cin, cout, s, act) in {(128, 128, 1, ops.ACT_SILU), (128, 128, 2, ops.ACT_SILU)}
     if (tile >= DE0 and not _de_takes(tile, cin, cout, 3, s, act, res)) or (tile < DE0 and v10_only):
         with pytest.raises(RuntimeError):
             _conv_case(N, H, W, cin, cout, 3, s, 1, a, res=res, ldx_extra=lx, x_coff=xc,
