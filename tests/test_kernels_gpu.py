@@ -460,6 +460,10 @@ def test_conv_dual_fused_downsample(tile, geom):
     w = (torch.randn(cout, K1 + K2, generator=g) * 0.05).to(torch.bfloat16)
     b = torch.randn(cout, generator=g)
     ref = ops.conv_dual(x1, x2, w, b, ops.ACT_RELU, s)
+    if tile >= DE0:
+        with pytest.raises(RuntimeError):  # the v10 direct forms take no dual-source GEMM
+            ops.conv_dual(x1.cuda(), x2.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, s, tile=tile)
+        return
     if NLOOP0 <= tile < XP0 and (tile not in NLOOP_DUAL or K1 + K2 != NLOOP_KPAD[tile - NLOOP0]):
         with pytest.raises(RuntimeError):  # each v6 dual tile is compiled for one K
             ops.conv_dual(x1.cuda(), x2.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, s, tile=tile)
