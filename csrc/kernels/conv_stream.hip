@@ -296,41 +296,18 @@ void conv_stream_kernel(const KvConvParams p) {
         acc2[tn][4 * g + 2] = bias1_r[tn][g].z;
         acc2[tn][4 * g + 3] = bias1_r[tn][g].w;
       }
-    // fragment ring (asm reads, common.h: lds_read16 / lds_wait): the reads of step kk + PD2
-    // are issued before the MFMAs of step kk.  With plain loads hipcc issued each step's reads
-    // right before its MFMAs, and an lgkmcnt(0) sat in front of most of them (tools/isa_lint.py:
-    // 59 % of this kernel's MFMAs at NT1 = 128)
-    constexpr int KK2 = BN / 16, RPS = 1 + TN1;          // steps, reads per step
-    constexpr int PD2 = TN1 == 1 ? 2 : 3;  // RPS x PD2 <= 15 (lgkmcnt); NT1 = 64 sits at 512 VGPRs
-    bf16x8 ar[PD2 + 1], br[PD2 + 1][TN1];
-    const unsigned a_base = lds_addr(Cs + (wm2 * 32 + fr32) * CS + fh32 * 8);
-    unsigned b_base[TN1][4];  // per (tn, kk & 3): the swizzled 16-B column of this lane's row
 #pragma unroll
-    for (int tn = 0; tn < TN1; ++tn) {
-      const int row = wn2 * (NT1 / 2) + tn * 32 + fr32;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        b_base[tn][j] = lds_addr(W1s + row * BK + (((j * 2 + fh32) ^ ((row >> 1) & 7)) << 3));
-    }
-    auto rd2 = [&](auto kc) __attribute__((always_inline)) {
-      constexpr int kk = decltype(kc)::value, sl = kk % (PD2 + 1);
-      lds_read16<kk * 32>(ar[sl], a_base);
-#pragma unroll
-      for (int tn = 0; tn < TN1; ++tn)  // kt = kk / 4 blocks of [NT1][64] bf16 apart
-        lds_read16<0>(br[sl][tn], b_base[tn][kk & 3] + (kk >> 2) * NT1 * BK * 2);
-    };
-    static_range<0, (PD2 < KK2 ? PD2 : KK2)>(rd2);
-    static_range<0, KK2>([&](auto kc) __attribute__((always_inline)) {
-      constexpr int kk = decltype(kc)::value, sl = kk % (PD2 + 1);
-      if constexpr (kk + PD2 < KK2) rd2(IC<kk + PD2>{});
-      constexpr int later = (KK2 - 1 - kk) < PD2 ? (KK2 - 1 - kk) : PD2;
-      lds_wait<later * RPS>(ar[sl]);
+    for (int kk = 0; kk < BN / 16; ++kk) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(Cs + (wm2 * 32 + fr32) * CS + kk * 16 + fh32 * 8);
+      const int kt = kk >> 2, q = (kk & 3) * 2 + fh32;
 #pragma unroll
       for (int tn = 0; tn < TN1; ++tn) {
-        asm volatile("" : "+v"(br[sl][tn]));  // after the wait above
-        acc2[tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(br[sl][tn], ar[sl], acc2[tn], 0, 0, 0);
+        const int row = wn2 * (NT1 / 2) + tn * 32 + fr32;
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(
+            W1s + kt * NT1 * BK + row * BK + ((q ^ ((row >> 1) & 7)) << 3));
+        acc2[tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, a, acc2[tn], 0, 0, 0);
       }
-    });
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave done reading the y tile: reuse Cs for z
     asm volatile("" ::: "memory");

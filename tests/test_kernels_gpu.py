@@ -653,6 +653,7 @@ def test_stem_pool_fused(shape):
     (2, 56, 56, 64, 0, 1, 64),     # layer1 conv3 + res -> next conv1 (64)
     (2, 56, 56, 64, 0, 1, 128),    # layer1 -> layer2 conv1 (128)
     (3, 13, 11, 64, 0, 1, 64),     # M tail (M % 64 != 0)
+    (12, 56, 56, 64, 0, 1, 64),    # more 64-row tiles than CUs: workgroups walk several tiles
     (2, 28, 28, 64, 64, 1, 64),    # fused downsample dual form (layer1 block 0)
     (1, 9, 7, 64, 64, 2, 64),      # dual with a strided second source
 ])
