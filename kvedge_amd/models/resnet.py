@@ -270,7 +270,9 @@ class KvResNet50:
                 for j in range(nb):
                     b, nxt = self.blocks[j], self.blocks[j + 1]
                     last = j == nb - 1
-                    fuse = self.fuse_tail and y.is_cuda and b.can_tail(nxt)
+                    # the same batch gate as the whole-batch path below: a seam at micro-batch
+                    # size where the whole batch runs the pair unfused changes y's bf16 rounding
+                    fuse = self.fuse_tail and y.is_cuda and b.can_tail(nxt) and b.tail_fits(y)
                     if last and full is None:
                         shp = b.out_shape(y.shape)
                         full = ops.empty((B,) + shp[1:], dtype=y.dtype, device=y.device)
