@@ -170,11 +170,22 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   // wave-aggregated compaction: one LDS atomic per wave and pass (popcount of the ballot)
   // instead of one per candidate -- with random-init heads nearly all 8400 anchors pass
   // conf, and 8400 atomics on one LDS word serialise (key order does not matter: sorted next)
+  // All of this thread's scores are loaded up front (A <= kMaxCand: at most kIt per thread),
+  // so the HBM latency is paid once, not once per pass of the ballot loop below.
+  constexpr int kIt = kMaxCand / (64 * kNmsWaves);
   {
     const int ln = tid & 63;
-    for (int a0 = 0; a0 < A; a0 += blockDim.x) {  // uniform trip count: whole waves ballot
-      const int a = a0 + tid;
-      const float s = a < A ? sc[a] : 0.f;
+    float sv[kIt];
+#pragma unroll
+    for (int i = 0; i < kIt; ++i) {
+      const int a = i * 64 * kNmsWaves + tid;
+      sv[i] = a < A ? sc[a] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < kIt; ++i) {  // uniform trip count: whole waves ballot
+      if (i * 64 * kNmsWaves >= A) break;
+      const int a = i * 64 * kNmsWaves + tid;
+      const float s = sv[i];
       const bool take = a < A && s > conf;
       const unsigned long long m = __ballot(take);
       int base = 0;
@@ -261,9 +272,16 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
     __syncthreads();
     if (s_nsel <= kSelMax) {
       const int T = s_T;
-      for (int i = tid; i < cnt; i += blockDim.x) {
-        const unsigned long long key = keys[i];
-        if (bin_of(key) >= T) sel[atomicAdd(&s_n2, 1)] = key;
+      const int ln = tid & 63;
+      for (int i0 = 0; i0 < cnt; i0 += blockDim.x) {  // wave-aggregated, as the compaction
+        const int i = i0 + tid;
+        const unsigned long long key = i < cnt ? keys[i] : 0ull;
+        const bool take = i < cnt && bin_of(key) >= T;
+        const unsigned long long m = __ballot(take);
+        int base = 0;
+        if (ln == 0 && m) base = atomicAdd(&s_n2, (int)__popcll(m));
+        base = __shfl(base, 0);
+        if (take) sel[base + (int)__popcll(m & ((1ull << ln) - 1ull))] = key;
       }
       __syncthreads();
       K = sel;
