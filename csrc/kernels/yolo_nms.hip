@@ -1,3 +1,4 @@
+#include <stdlib.h>
 // K9 YOLOv8 decode and K10 class-aware NMS for gfx950.  SURVEY.md §2.5, §7.3(2).
 //
 // Decode: one workgroup per 64 consecutive anchors of one (image, level): the
@@ -146,13 +147,14 @@ constexpr int kNmsWaves = 8;
 constexpr int kSel = 1024;     // top-set target size
 constexpr int kSelMax = 2048;  // top-set capacity (a wider threshold bin -> full sort)
 constexpr int kBins = 2048;    // score-bit histogram bins
+constexpr int kRankSortMax = 1024;  // rank sort up to here (<= 2 keys per thread), bitonic above
 
 __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __restrict__ boxes,
                                                   const float* __restrict__ scores,
                                                   const int* __restrict__ cls, int A,
                                                   float conf, float iou_thr, int max_det,
                                                   float* __restrict__ out,
-                                                  int* __restrict__ count) {
+                                                  int* __restrict__ count, int diag) {
   __shared__ unsigned long long keys[kMaxCand];
   __shared__ __attribute__((aligned(16))) float kept[4 * 320];
   __shared__ int kept_c[320];
@@ -164,6 +166,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   __shared__ int s_n2, s_T, s_nsel;
   const int n = blockIdx.x;
   const int tid = threadIdx.x;
+  const unsigned long long t_start = (diag & 4) ? __builtin_amdgcn_s_memrealtime() : 0ull;
   if (tid == 0) ncand = 0;
   __syncthreads();
   const float* sc = scores + (long long)n * A;
@@ -200,6 +203,8 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   }
   __syncthreads();
   const int cnt = min(ncand, kMaxCand);
+  // diag bit 2: per-phase wall-clock stamps (s_memrealtime, 100 MHz) -> the image's output rows
+  unsigned long long t_ph[4] = {t_start, 0, 0, 0};
   // bitonic sort of K[0, n) (padded with zero keys to a power of two), descending
   auto bitonic = [&](unsigned long long* K, int n) __attribute__((always_inline)) {
     int P = 64;
@@ -288,7 +293,29 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
       nsel = s_n2;
     }
   }
-  bitonic(K, nsel);
+  if (diag & 4) t_ph[1] = __builtin_amdgcn_s_memrealtime();
+  // Small sets (random-init heads: ~100 candidates per image) are sorted by rank: each thread
+  // counts the keys above its own with broadcast LDS reads and writes its key to that slot --
+  // one pass and one barrier instead of the bitonic network's log^2 barrier-separated stages
+  // (28 at 128 keys, 42 us per image measured: profiles/r4_v5_nms_probe.txt).  Keys are unique
+  // (the index is in the low word), so the ranks are a permutation.
+  if (!(diag & 2)) {
+    if (K == keys && nsel <= kRankSortMax) {  // (a top set in sel stays bitonic: the
+      unsigned long long* dst = sel;           // full-sort fallback below needs keys intact)
+      for (int i0 = 0; i0 < nsel; i0 += blockDim.x) {
+        const int i = i0 + tid;
+        const unsigned long long key = i < nsel ? K[i] : 0ull;
+        int r = 0;
+        for (int j = 0; j < nsel; ++j) r += K[j] > key;
+        if (i < nsel) dst[r] = key;
+      }
+      __syncthreads();
+      K = dst;
+    } else {
+      bitonic(K, nsel);  // diag bit 1: no top-set sort (timing only)
+    }
+  }
+  if (diag & 4) t_ph[2] = __builtin_amdgcn_s_memrealtime();
   float* o = out + (long long)n * max_det * 6;
   const int lane = tid & 63, wv = tid >> 6;
   const float* bx = boxes + (long long)n * A * 4;
@@ -380,7 +407,8 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
       nk = s_nk;
     }
   };
-  greedy(K, 0, nsel);
+  if (!(diag & 1)) greedy(K, 0, nsel);  // diag bit 0: no suppression (timing only)
+  else nk = max_det;
   if (nk < max_det && nsel < cnt) {
     // the top set ran out: sort everything (its first nsel keys are the top set again,
     // in the same order) and continue after them
@@ -389,6 +417,15 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   }
   for (int i = nk * 6 + tid; i < max_det * 6; i += blockDim.x) o[i] = 0.f;
   if (tid == 0) count[n] = nk;
+  if (diag & 4) {
+    t_ph[3] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    if (tid == 0) {  // phase durations in 10-ns ticks: compaction+select, sort, suppression
+      o[0] = (float)(t_ph[1] - t_ph[0]);
+      o[1] = (float)(t_ph[2] - t_ph[1]);
+      o[2] = (float)(t_ph[3] - t_ph[2]);
+    }
+  }
 }
 
 }  // namespace
@@ -419,7 +456,11 @@ extern "C" int kv_nms(const float* boxes, const float* scores, const int* cls, i
                       hipStream_t s) {
   if (max_det > 300 || max_det <= 0 || A > kMaxCand) return -1;
   if (N <= 0) return 0;
+  // KVEDGE_NMS_DIAG (timing experiments only; outputs wrong): bit 0 skips the greedy
+  // suppression, bit 1 the top-set sort; bit 2 writes per-phase durations into each image's
+  // first output row
+  const char* dg = getenv("KVEDGE_NMS_DIAG");
   hipLaunchKernelGGL(nms_kernel, dim3(N), dim3(64 * kNmsWaves), 0, s, boxes, scores, cls, A, conf_thres,
-                     iou_thres, max_det, out, count);
+                     iou_thres, max_det, out, count, dg ? atoi(dg) : 0);
   return hipGetLastError() == hipSuccess ? 0 : -100;
 }

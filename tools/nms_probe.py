@@ -1,32 +1,58 @@
 #!/usr/bin/env python3
-"""NMS workload at the bench shape: candidates per image over a batch of synthetic
-frames, and the standalone nms kernel time."""
+"""Time the YOLOv8n NMS kernel on the model's own decode output (random-init weights, synthetic
+frames), with KVEDGE_NMS_DIAG switching phases off (timing only; 1 = no greedy suppression,
+2 = no top-set sort) -- where the per-image NMS latency goes.
+
+  python tools/nms_probe.py --batch 192
+"""
+import argparse
 import os
 import sys
 
-import torch
-
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from kvedge_amd import ops  # noqa: E402
-from kvedge_amd.models.yolov8 import STRIDES, KvYoloV8n as M  # noqa: E402
 
-assert ops.load()
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-m = M.build(seed=0, device="cuda")
-fr = torch.empty(B, 640, 640, 3, dtype=torch.uint8, device="cuda")
-ops.synth_frames(fr, 0, 3)
-feats = m.heads(m.preprocess(fr))
-boxes, scores, cls = ops.yolo_decode(feats, STRIDES, m.nc)
-torch.cuda.synchronize()
-cand = (scores > m.conf).sum(1).float()
-print("candidates per image: min %d median %d max %d" % (cand.min(), cand.median(), cand.max()))
-for conf in (m.conf, 0.5, 0.9):
-    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ops.nms(boxes, scores, cls, conf, m.iou, m.max_det)
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=192)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    import torch
+
+    from kvedge_amd import ops
+    from kvedge_amd.models.yolov8 import STRIDES, KvYoloV8n
+
+    assert ops.load()
+    m = KvYoloV8n.build(seed=0, device="cuda")
+    fr = torch.randint(0, 256, (a.batch, 640, 640, 3), dtype=torch.uint8,
+                       generator=torch.Generator().manual_seed(1)).cuda()
+    with torch.no_grad():
+        feats = m.heads(m.stem_b1(fr), b1_done=True)
+        boxes, scores, cls = ops.yolo_decode(feats, STRIDES, m.nc)
     torch.cuda.synchronize()
-    st.record()
-    for _ in range(10):
-        dets, cnt = ops.nms(boxes, scores, cls, conf, m.iou, m.max_det)
-    en.record()
+    print(f"candidates per image > conf {m.conf}: "
+          f"{float((scores > m.conf).sum(1).float().mean()):.0f} of {scores.shape[1]}")
+    os.environ["KVEDGE_NMS_DIAG"] = "4"
+    out, cnt = ops.nms(boxes, scores, cls, m.conf, m.iou, m.max_det)
     torch.cuda.synchronize()
-    print("conf %.2f: nms %.1f us, kept max %d" % (conf, st.elapsed_time(en) / 10 * 1e3, cnt.max()))
+    ph = out[:, 0, :3].float().cpu() / 100.0  # 10-ns ticks -> us
+    print("per-image phase us (median over images): compaction+select %.1f, sort %.1f, "
+          "suppression %.1f" % tuple(float(ph[:, i].median()) for i in range(3)))
+    for d in ("0", "1", "2", "3"):
+        os.environ["KVEDGE_NMS_DIAG"] = d
+        ts = []
+        for _ in range(a.iters):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            out, cnt = ops.nms(boxes, scores, cls, m.conf, m.iou, m.max_det)
+            e.record()
+            torch.cuda.synchronize()
+            ts.append(s.elapsed_time(e) * 1e3)
+        ts.sort()
+        extra = f" kept/image {float(cnt.float().mean()):.0f}" if d == "0" else ""
+        print(f"diag {d}: {ts[len(ts) // 2]:.1f} us{extra}", flush=True)
+    os.environ.pop("KVEDGE_NMS_DIAG")
+
+
+if __name__ == "__main__":
+    main()
