@@ -211,16 +211,32 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
     while (P < n) P <<= 1;
     for (int i = n + tid; i < P; i += blockDim.x) K[i] = 0ull;
     __syncthreads();
+    // one compare-exchange PAIR per thread and pass (pair q -> i = the q-th index with bit j
+    // clear), all of a thread's loads issued before any compare: one LDS latency per stage.
+    // (Looping over elements and skipping half left one dependent load pair per element in
+    // series: 43 us for a 2048-key top set, profiles/r4_v5_nms_probe.txt.)
+    constexpr int kPairs = kMaxCand / 2 / (64 * kNmsWaves);  // pairs per thread, at most
     for (int k = 2; k <= P; k <<= 1) {
       for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = tid; i < P; i += blockDim.x) {
-          const int ixj = i ^ j;
-          if (ixj > i) {
-            const unsigned long long a = K[i], b = K[ixj];
-            const bool desc = (i & k) == 0;
-            if (desc ? (a < b) : (a > b)) {
-              K[i] = b;
-              K[ixj] = a;
+        unsigned long long a[kPairs], b[kPairs];
+        int ia[kPairs];
+#pragma unroll
+        for (int r = 0; r < kPairs; ++r) {
+          const int q = tid + r * 64 * kNmsWaves;
+          ia[r] = ((q & ~(j - 1)) << 1) | (q & (j - 1));  // insert a 0 at bit log2(j)
+          if (2 * q < P) {
+            a[r] = K[ia[r]];
+            b[r] = K[ia[r] | j];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < kPairs; ++r) {
+          const int q = tid + r * 64 * kNmsWaves;
+          if (2 * q < P) {
+            const bool desc = (ia[r] & k) == 0;
+            if (desc ? (a[r] < b[r]) : (a[r] > b[r])) {
+              K[ia[r]] = b[r];
+              K[ia[r] | j] = a[r];
             }
           }
         }
@@ -323,19 +339,34 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   int nk = 0;
   // greedy suppression over the sorted K[from, to), continuing the kept list
   auto greedy = [&](const unsigned long long* K, int from, int to) __attribute__((always_inline)) {
+    // the chunk's class / box gathers (random global reads) are issued one chunk ahead, so
+    // their latency hides under the previous chunk's IoU tests and barriers (the images
+    // with crowded candidate sets walk ~20 chunks: 58 us of suppression at b192,
+    // profiles/r4_v5_nms_probe.txt)
+    int pc = -1;
+    float4 praw = make_float4(0.f, 0.f, 0.f, 0.f);
+    unsigned long long pkey = 0ull;
+    auto fetch = [&](int b) __attribute__((always_inline)) {
+      const int ci = b + lane;
+      pc = -1;
+      if (ci < to) {
+        pkey = K[ci];
+        const int idx = (int)(0xFFFFFFFFu - (unsigned)(pkey & 0xFFFFFFFFull));
+        pc = cl[idx];
+        praw = *reinterpret_cast<const float4*>(bx + idx * 4);
+      }
+    };
+    if (from < to) fetch(from);
     for (int base = from; base < to && nk < max_det; base += 64) {
       // every wave holds the same 64 candidates (lane = candidate)
       const int ci = base + lane;
       const bool valid = ci < to;
       float x1 = 0, y1 = 0, x2 = 0, y2 = 0, s = 0;
-      float4 raw = make_float4(0.f, 0.f, 0.f, 0.f);
-      int c = -1;
+      const float4 raw = valid ? praw : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int c = valid ? pc : -1;
+      if (valid) s = __uint_as_float((unsigned)(pkey >> 32));
+      if (base + 64 < to) fetch(base + 64);
       if (valid) {
-        const unsigned long long key = K[ci];
-        const int idx = (int)(0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull));
-        s = __uint_as_float((unsigned)(key >> 32));
-        c = cl[idx];
-        raw = *reinterpret_cast<const float4*>(bx + idx * 4);
         const float off = (float)c * kMaxWH;
         x1 = raw.x + off;
         y1 = raw.y + off;

@@ -38,6 +38,10 @@ def main():
     ph = out[:, 0, :3].float().cpu() / 100.0  # 10-ns ticks -> us
     print("per-image phase us (median over images): compaction+select %.1f, sort %.1f, "
           "suppression %.1f" % tuple(float(ph[:, i].median()) for i in range(3)))
+    print("per-image phase us (max over images):    compaction+select %.1f, sort %.1f, "
+          "suppression %.1f" % tuple(float(ph[:, i].max()) for i in range(3)))
+    nc = (scores > m.conf).sum(1)
+    print(f"candidates per image: max {int(nc.max())}, images over 1024: {int((nc > 1024).sum())}")
     for d in ("0", "1", "2", "3"):
         os.environ["KVEDGE_NMS_DIAG"] = d
         ts = []
