@@ -211,32 +211,16 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
     while (P < n) P <<= 1;
     for (int i = n + tid; i < P; i += blockDim.x) K[i] = 0ull;
     __syncthreads();
-    // one compare-exchange PAIR per thread and pass (pair q -> i = the q-th index with bit j
-    // clear), all of a thread's loads issued before any compare: one LDS latency per stage.
-    // (Looping over elements and skipping half left one dependent load pair per element in
-    // series: 43 us for a 2048-key top set, profiles/r4_v5_nms_probe.txt.)
-    constexpr int kPairs = kMaxCand / 2 / (64 * kNmsWaves);  // pairs per thread, at most
     for (int k = 2; k <= P; k <<= 1) {
       for (int j = k >> 1; j > 0; j >>= 1) {
-        unsigned long long a[kPairs], b[kPairs];
-        int ia[kPairs];
-#pragma unroll
-        for (int r = 0; r < kPairs; ++r) {
-          const int q = tid + r * 64 * kNmsWaves;
-          ia[r] = ((q & ~(j - 1)) << 1) | (q & (j - 1));  // insert a 0 at bit log2(j)
-          if (2 * q < P) {
-            a[r] = K[ia[r]];
-            b[r] = K[ia[r] | j];
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < kPairs; ++r) {
-          const int q = tid + r * 64 * kNmsWaves;
-          if (2 * q < P) {
-            const bool desc = (ia[r] & k) == 0;
-            if (desc ? (a[r] < b[r]) : (a[r] > b[r])) {
-              K[ia[r]] = b[r];
-              K[ia[r] | j] = a[r];
+        for (int i = tid; i < P; i += blockDim.x) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const unsigned long long a = K[i], b = K[ixj];
+            const bool desc = (i & k) == 0;
+            if (desc ? (a < b) : (a > b)) {
+              K[i] = b;
+              K[ixj] = a;
             }
           }
         }
