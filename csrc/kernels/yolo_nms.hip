@@ -391,15 +391,17 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
           row |= rowp[w][lane];
         }
         const bool alive = valid && !((dead >> lane) & 1ull);
-        unsigned long long live = __ballot(alive);
+        unsigned long long todo = __ballot(alive), live = 0ull;
         const unsigned rlo = (unsigned)row, rhi = (unsigned)(row >> 32);
-        for (int j = 0; j < lim; ++j) {
-          if ((live >> j) & 1ull) {
-            const unsigned long long rj =
-                ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)rhi, j) << 32) |
-                (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)rlo, j);
-            live &= ~rj;
-          }
+        // survivors in rank order: only the set bits are visited (a crowded chunk behind a
+        // full kept list has few), each one striking the later boxes it overlaps
+        while (todo) {
+          const int j = __builtin_ctzll(todo);
+          const unsigned long long rj =
+              ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)rhi, j) << 32) |
+              (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)rlo, j);
+          live |= 1ull << j;
+          todo &= ~(rj | (1ull << j));
         }
         // 3. append survivors in rank order
         const bool keep = (live >> lane) & 1ull;
