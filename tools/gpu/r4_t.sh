@@ -1,0 +1,9 @@
+# Round 4 (t): seam IDR forms (residual as an identity K chunk, bias-seeded accumulators):
+# numerics, same-box probe
+set -o pipefail
+mkdir -p gpurun_out; export TMPDIR=/tmp
+T=${TAG:-r4t}
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "seam" > gpurun_out/${T}_t.txt 2>&1 || { tail -30 gpurun_out/${T}_t.txt; exit 1; }
+tail -1 gpurun_out/${T}_t.txt
+timeout -k 10 300 python -u tools/seam_probe.py --batch 640 > gpurun_out/${T}_seam_probe.md 2> gpurun_out/${T}_probe.err || { tail -5 gpurun_out/${T}_probe.err; exit 1; }
+cut -c1-900 gpurun_out/${T}_seam_probe.md
