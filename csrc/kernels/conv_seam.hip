@@ -158,14 +158,8 @@ __device__ __forceinline__ void sm_lds_barrier() {
 // while its own MFMAs consume the set read during step s - 1: no step starts with an LDS
 // round trip behind the barrier (the conv1 steps' y-tile A reads stay in-step: y is written
 // by the epilogue at the start of the tile's first conv1 step).
-// IDR: the residual joins the conv3 GEMM as one more 64-deep K chunk against an identity
-// block held in registers (acc += R . I), and the bias seeds the accumulators; the y
-// epilogue is then act + pack only.  The seams were VALU-bound in the epilogue: 3.4 (stage 3)
-// and 6.4 (stage 2) VALU instructions per MFMA (profiles/r4_v3_pmc_seam.md), the residual
-// unpack + add and the bias add taking 3 of the ~4.5 per output element.  ResNet's act1 =
-// none only (act2(acc + b + r)); other activation pairs take the plain epilogue.
 template <int NC3, int NZC, int D, int RD, int NW = 8, int KS2 = 1, bool AREG = false,
-          bool XP = false, bool IDR = false>
+          bool XP = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(const KvConvParams p, int ntiles) {
   static_assert(NW == 4 || NW == 8, "waves");
   static_assert(NC3 % KS2 == 0 && NZC % KS2 == 0, "whole chunks per ring stage");
@@ -320,19 +314,6 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(con
 
   floatx4 acc[2][2];
   floatx4 accz[NZC][2][2];
-  // IDR: B fragments of the 64 x 64 identity in MFMA operand layout: lane (fr, fh) holds K
-  // values ks*32 + fh*8 .. +8 of output channel wn*32 + tn*16 + fr
-  bf16x8 ident[IDR ? 2 : 1][2];
-  if constexpr (IDR) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int tn = 0; tn < 2; ++tn) {
-        const int d = (wn * 32 + tn * 16 + fr) - (ks * 32 + fh * 8);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) ident[ks][tn][e] = (bf16)(d == e ? 1.0f : 0.0f);
-      }
-  }
 #pragma unroll
   for (int zc = 0; zc < NZC; ++zc)
 #pragma unroll
@@ -354,12 +335,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(con
 #pragma unroll
       for (int tn = 0; tn < 2; ++tn) {
         const int row = wn * 32 + tn * 16 + fr;
-        if constexpr (IDR) {  // Bs == nullptr: the identity block (IDR residual chunk)
-          bfg[tn] = Bs ? *reinterpret_cast<const bf16x8*>(Bs + row * 128 + ((q ^ sm_sw(row)) << 4))
-                       : ident[ks][tn];
-        } else {
-          bfg[tn] = *reinterpret_cast<const bf16x8*>(Bs + row * 128 + ((q ^ sm_sw(row)) << 4));
-        }
+        bfg[tn] = *reinterpret_cast<const bf16x8*>(Bs + row * 128 + ((q ^ sm_sw(row)) << 4));
       }
 #pragma unroll
       for (int tn = 0; tn < 2; ++tn)
@@ -447,25 +423,6 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(con
           else sm_wait_vm<S::wE(S::kFar)>();
           sm_lds_barrier();
           const float* bias_t = reinterpret_cast<const float*>(lds + BIAS_OFF) + t * 64;
-          if constexpr (IDR && act1 == kActNone) {
-            // acc (seeded with the bias) += R(t) . I: the residual slot's rows are A fragments
-            mma64(Rs, nullptr, acc);
-            sm_lds_barrier();  // every wave's residual reads retired before y overwrites them
-#pragma unroll
-            for (int tn = 0; tn < 2; ++tn) {
-              const int c0 = wn * 32 + tn * 16 + fh * 4;
-#pragma unroll
-              for (int tm = 0; tm < 2; ++tm) {
-                const int row = wm * 32 + tm * 16 + fr;
-                bf16x4* ptr = reinterpret_cast<bf16x4*>(Rs + row * 128 +
-                                                        (((c0 >> 3) ^ sm_sw(row)) << 4) + (c0 & 7) * 2);
-                bf16x4 o;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = f2bf(act_c<act2>(acc[tn][tm][e]));
-                *ptr = o;
-              }
-            }
-          } else
 #pragma unroll
           for (int tn = 0; tn < 2; ++tn) {
             const int c0 = wn * 32 + tn * 16 + fh * 4;
@@ -495,7 +452,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(con
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(kv_i32x4, v), ry, off, 0, 0);
           }
         }
-        if constexpr (j == 0 && !(IDR && act1 == kActNone)) {
+        if constexpr (j == 0) {
 #pragma unroll
           for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -509,15 +466,6 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(con
           else sm_wait_vm<S::wB(S::kFar, j)>();
         }
         sm_lds_barrier();  // WAR: every wave's reads of the slot about to be refilled retired
-        if constexpr (j == 0 && IDR && act1 == kActNone) {  // bias seeds the accumulators
-          const float* bias_t = reinterpret_cast<const float*>(lds + BIAS_OFF) + t * 64;
-#pragma unroll
-          for (int tn = 0; tn < 2; ++tn) {
-            const float4 bv = *reinterpret_cast<const float4*>(bias_t + wn * 32 + tn * 16 + fh * 4);
-#pragma unroll
-            for (int tm = 0; tm < 2; ++tm) acc[tn][tm] = floatx4{bv.x, bv.y, bv.z, bv.w};
-          }
-        }
         constexpr int jn = (j + D - 1) % SPT, tadv = (j + D - 1) / SPT;
         issue_B(t + tadv, SmIC<jn>{});
         if constexpr (j == 0) issue_R(t + RD - 1);
@@ -599,10 +547,10 @@ struct SmTile {
 };
 
 template <int NC3, int NZC, int D, int RD, int NW = 8, int KS2 = 1, bool AREG = false,
-          bool XP = false, bool IDR = false>
+          bool XP = false>
 constexpr SmTile sm_tile() {
   return SmTile{NC3, NZC, D, RD, NW, KS2, AREG ? 1 : 0,
-                &conv_seam_kernel<NC3, NZC, D, RD, NW, KS2, AREG, XP, IDR>};
+                &conv_seam_kernel<NC3, NZC, D, RD, NW, KS2, AREG, XP>};
 }
 
 // LDS = A (K3 x BM x 2) + d x ks2 x 8 KB ring + rd x BM x 128 B residual ring + bias tables.
@@ -635,11 +583,6 @@ static const SmTile kSmTiles[] = {
     sm_tile<4, 4, 3, 5, 8, 2, true>(),
     // stage 3 -> 4 (N1 512): not taken by the model (level with unfused at b640)
     sm_tile<4, 8, 4, 3>(),
-    // IDR forms (residual as an identity K chunk, bias-seeded accumulators), for the probe
-    sm_tile<2, 2, 4, 3, 4, 1, false, false, true>(),
-    sm_tile<2, 4, 6, 3, 8, 2, true, false, true>(),
-    sm_tile<4, 4, 4, 4, 8, 2, true, false, true>(),
-    sm_tile<4, 4, 3, 2, 8, 2, false, false, true>(),
 };
 
 int sm_lds_bytes(const SmTile& e, int cout, int n1) {
