@@ -162,26 +162,10 @@ __global__ __launch_bounds__(kNT, 2) void yolo_stem2_kernel(
       const unsigned char* sa0 = sring + mod3(sy - 1) * SR + q16 * kSP + kq * 16;  // pixel sx-1
       const unsigned char* sa1 = sring + mod3(sy) * SR + q16 * kSP + kq * 16;
       unsigned char* td = tring + mod3(sy) * TR + lslot * kTP + kq * 8;
-      // the next block's two fragments are read (asm, common.h) before this block's MFMAs:
-      // one block of latency ahead instead of an lgkmcnt(0) in front of every MFMA pair
-      // (tools/isa_lint.py: 80 % of this kernel's MFMAs)
-      const unsigned la0 = lds_addr(sa0), la1 = lds_addr(sa1);
-      bf16x8 n0, n1;
-      if (wv < bpr) {
-        lds_read16<0>(n0, la0 + wv * 16 * kSP);
-        lds_read16<0>(n1, la1 + wv * 16 * kSP);
-      }
       for (int b = wv; b < bpr; b += 4) {
         floatx4 acc = {b0v.x, b0v.y, b0v.z, b0v.w};
-        bf16x8 a0 = n0, a1 = n1;
-        if (b + 4 < bpr) {
-          lds_read16<0>(n0, la0 + (b + 4) * 16 * kSP);
-          lds_read16<0>(n1, la1 + (b + 4) * 16 * kSP);
-          lds_wait<2>(a0);  // this block's pair landed; the next pair stays in flight
-        } else {
-          lds_wait<0>(a0);
-        }
-        asm volatile("" : "+v"(a1));
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(sa0 + b * 16 * kSP);
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(sa1 + b * 16 * kSP);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0r[0], a0, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0r[1], a1, acc, 0, 0, 0);
         // lane holds channels kq*4 .. +3 of stem pixel (sy, 16 b + q16)
@@ -196,23 +180,6 @@ __global__ __launch_bounds__(kNT, 2) void yolo_stem2_kernel(
   // ---- b1: output row yo of image n from stem rows 2yo-1 .. 2yo+1 -> global
   auto b1_row = [&](int n, int yo) __attribute__((always_inline)) {
     const int nblk = (W1 + 31) / 32;
-    unsigned rowl[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) rowl[r] = lds_addr(tring + mod3(2 * yo - 1 + r) * TR + fh * 16);
-    // the 9 tap fragments of a block, read (asm) one block ahead of its MFMAs
-    // tap s: stem column 2xo - 1 + s -> s = 0: odd xo-1 (pad slot when xo = 0), s = 1: even
-    // xo, s = 2: odd xo
-    auto rd9 = [&](bf16x8 (&f)[9], int blk) __attribute__((always_inline)) {
-      const int xo = min(blk * 32 + fr, W1 - 1);
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        lds_read16<0>(f[3 * r + 0], rowl[r] + (half + xo) * kTP);
-        lds_read16<0>(f[3 * r + 1], rowl[r] + xo * kTP);
-        lds_read16<0>(f[3 * r + 2], rowl[r] + (half + 1 + xo) * kTP);
-      }
-    };
-    bf16x8 nf[9];
-    if (wv < nblk) rd9(nf, wv);
     for (int blk = wv; blk < nblk; blk += 4) {
       const int xo = min(blk * 32 + fr, W1 - 1);
       floatx16 acc;
@@ -225,15 +192,14 @@ __global__ __launch_bounds__(kNT, 2) void yolo_stem2_kernel(
       }
       bf16x8 af[9];
 #pragma unroll
-      for (int t = 0; t < 9; ++t) af[t] = nf[t];
-      if (blk + 4 < nblk) {
-        rd9(nf, blk + 4);
-        lds_wait<9>(af[0]);  // this block's 9 landed; the next block's 9 stay in flight
-      } else {
-        lds_wait<0>(af[0]);
+      for (int r = 0; r < 3; ++r) {
+        const unsigned char* rowp = tring + mod3(2 * yo - 1 + r) * TR + fh * 16;
+        // tap s: stem column 2xo - 1 + s -> s = 0: odd xo-1 (pad slot when xo = 0),
+        // s = 1: even xo, s = 2: odd xo
+        af[3 * r + 0] = *reinterpret_cast<const bf16x8*>(rowp + (half + xo) * kTP);
+        af[3 * r + 1] = *reinterpret_cast<const bf16x8*>(rowp + xo * kTP);
+        af[3 * r + 2] = *reinterpret_cast<const bf16x8*>(rowp + (half + 1 + xo) * kTP);
       }
-#pragma unroll
-      for (int t = 1; t < 9; ++t) asm volatile("" : "+v"(af[t]));
 #pragma unroll
       for (int t = 0; t < 9; ++t)
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1r[t], af[t], acc, 0, 0, 0);
