@@ -98,7 +98,10 @@ __device__ __forceinline__ void static_range(F&& f) {
 }
 
 // ds_read_b128 that hipcc can neither sink nor merge: the caller owns the wait (a counted
-// s_waitcnt lgkmcnt tied to the destination, lds_wait below).  hipcc's scheduler sank every
+// s_waitcnt lgkmcnt tied to the destination, lds_wait below).  The destination register is
+// written when the data returns, after the asm statement hipcc sees: keep it out of
+// loop-carried values (a back-edge copy may read it before the wait -- the YOLO stem2
+// prefetch produced NaNs that way) and consume it only after its lds_wait.  hipcc's scheduler sank every
 // fragment read of conv_direct.hip's ring to just before its MFMA under register pressure,
 // so each MFMA waited out a full LDS round trip (an lgkmcnt(0) in front of 100 % of them).
 template <int OFF, class T>
