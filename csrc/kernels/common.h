@@ -116,6 +116,19 @@ __device__ __forceinline__ void lds_wait(T& dst) {
   static_assert(N >= 0 && N <= 15, "lgkmcnt field");
   asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(dst) : "n"(N) : "memory");
 }
+// 16-B buffer load that hipcc neither sinks nor waits for: the same contract as lds_read16
+// (not loop-carried, consumed only after vm_wait).  vmcnt counts every vector-memory op of
+// the wave in issue order (loads, stores, LDS DMAs): vm_wait<N> leaves the N youngest in flight.
+template <class T>
+__device__ __forceinline__ void vm_load16(T& dst, kv_i32x4 rs, int voff) {
+  static_assert(sizeof(T) == 16, "buffer_load_dwordx4");
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(dst) : "v"(voff), "s"(rs) : "memory");
+}
+template <int N, class T>
+__device__ __forceinline__ void vm_wait(T& a, T& b) {
+  static_assert(N >= 0 && N <= 63, "vmcnt field");
+  asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
+}
 template <class T>
 __device__ __forceinline__ unsigned lds_addr(const T* p) {
   return (unsigned)(unsigned long long)(const __attribute__((address_space(3))) void*)p;

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(NT, (NT / 256) * OCC) void conv3x3_direct_kernel(co
   constexpr int NCB2 = (C2 + 31) / 32;   // pair: 32-channel blocks of the 1x1's output
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   static_assert(!(DMA && U8), "DMA patch fetch: bf16 NHWC inputs only");
-  static_assert(!DE || (DMA && !RES && C2 == 0 && !U8), "direct epilogue: plain DMA forms");
+  static_assert(!DE || (DMA && C2 == 0 && !U8 && !(RES && SB)), "direct epilogue: plain DMA forms");
   static_assert(!SB || DE, "single patch buffer: direct-epilogue forms");
   static_assert(!DE || COUT % 16 == 0, "direct epilogue: 16-channel store pairs");
   const int psz = direct_patch_alloc(patch_rows * PW * C::PB, DMA);
@@ -359,6 +359,7 @@ __global__ __launch_bounds__(NT, (NT / 256) * OCC) void conv3x3_direct_kernel(co
   const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
       C2 > 0 ? p.z : p.y, (short)0, C2 > 0 ? p.N * Ho * Wo * p.ldz * 2 : 0, 0x00020000);
   const bf16* __restrict__ R = reinterpret_cast<const bf16*>(p.res);
+  const kv_i32x4 rr4 = kv_rsrc4(p.res, DE && RES ? p.N * Ho * Wo * p.ldr * 2 : 0);
   const int npix = kR * Wo;
   const int nblk = (npix + 31) / 32;
   const int rowb = PW * C::PB;
@@ -403,7 +404,7 @@ __global__ __launch_bounds__(NT, (NT / 256) * OCC) void conv3x3_direct_kernel(co
     // 16-channel YOLO bottleneck conv, profiles/r2_v2_yolov8n_b384_pmc.md)
     constexpr int OCH = COUT / 8;
     // VGPR budget: narrow forms only; the VGPR-prefetch form also holds the next patch
-    constexpr int RPF = RES && CIN <= 32 ? (DMA ? 12 : CIN <= 16 ? 6 : 0) : 0;
+    constexpr int RPF = RES && !DE && CIN <= 32 ? (DMA ? 12 : CIN <= 16 ? 6 : 0) : 0;
     uint4 rpf[RPF > 0 ? RPF : 1];
     const bool rpre = RPF > 0 && npix * OCH <= RPF * NT;
     if constexpr (RPF > 0) {
@@ -435,6 +436,18 @@ __global__ __launch_bounds__(NT, (NT / 256) * OCC) void conv3x3_direct_kernel(co
       for (int r = 0; r < KK; ++r) {
         pa[r] = pa0 + r * rowb;
         po[r] = pa[r] + (S == 2 ? HALF * C::PB : 0);
+      }
+      // DE + residual: this block's residual, in the store layout (lane fr: channels
+      // [q*16 + fh*8, +8) of pixel j), issued before the MFMA phase so its latency hides
+      // there; asm loads (common.h), so hipcc can neither sink them nor wait early
+      u32x4 rv[2] = {};
+      if constexpr (DE && RES) {
+        const int oy = oy0 + yl;
+        const bool ok = b * 32 + fr < npix && oy < Ho;
+        const int rp = (((n * Ho + oy) * Wo + xc) * p.ldr + p.r_coff + cb * 32) * 2;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          if (cb * 32 + q * 16 < COUT) vm_load16(rv[q], rr4, ok ? rp + (q * 16 + fh * 8) * 2 : kOOB);
       }
       floatx16 acc;
       if constexpr (BREG) {
@@ -489,7 +502,7 @@ __global__ __launch_bounds__(NT, (NT / 256) * OCC) void conv3x3_direct_kernel(co
         const int pix = (((n * Ho + oy) * Wo + xc) * p.ldy + p.y_coff + cb * 32) * 2;
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        if (diag & 8) {
+        if (!RES && (diag & 8)) {
           // diag bit 3: the first DE store form, 4 x 8 B per lane (lanes fr / fr + 32: channels
           // [g*8, g*8+4) / [g*8+4, g*8+8)), 32 16-B segments per instruction
 #pragma unroll
@@ -508,14 +521,30 @@ __global__ __launch_bounds__(NT, (NT / 256) * OCC) void conv3x3_direct_kernel(co
         // store instruction writes 32 pixels x 32 contiguous bytes (the 4 x 8-B form: 32 x 16 B).
         // Same box, 2-5 % faster than the 8-B form; the stores still cost ~80 of 250 us on the
         // Detect P3 stem slice (profiles/r4_v3_direct_diag.txt).
+        // Residual: the block's loads are this wave's youngest vector-memory ops -> vmcnt(0)
+        // (older: the previous block's stores, issued a whole MFMA phase ago, and the patch DMA).
+        if constexpr (RES) vm_wait<0>(rv[0], rv[1]);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           if (cb * 32 + q * 16 >= COUT) continue;  // wave-uniform (COUT % 16 == 0); counted below
+          float rlo[4] = {}, rhi[4] = {};
+          if constexpr (RES) {
+            // the store exchange below is an involution: applied to the residual (store
+            // layout) it yields the accumulator layout, so x + act(conv) rounds once, in fp32
+            const auto t0 = __builtin_amdgcn_permlane32_swap(rv[q][0], rv[q][2], false, false);
+            const auto t1 = __builtin_amdgcn_permlane32_swap(rv[q][1], rv[q][3], false, false);
+            const unsigned wl[2] = {t0[0], t1[0]}, wh[2] = {t0[1], t1[1]};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              rlo[e] = __uint_as_float(e & 1 ? wl[e >> 1] & 0xffff0000u : wl[e >> 1] << 16);
+              rhi[e] = __uint_as_float(e & 1 ? wh[e >> 1] & 0xffff0000u : wh[e >> 1] << 16);
+            }
+          }
           bf16x4 lo, hi;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            lo[e] = f2bf(act_c<ACT>(acc[8 * q + e]));      // group 2q: channels 16q + fh*4 + e
-            hi[e] = f2bf(act_c<ACT>(acc[8 * q + 4 + e]));  // group 2q+1: 16q + 8 + fh*4 + e
+            lo[e] = f2bf(act_c<ACT>(acc[8 * q + e]) + rlo[e]);      // group 2q: 16q + fh*4 + e
+            hi[e] = f2bf(act_c<ACT>(acc[8 * q + 4 + e]) + rhi[e]);  // group 2q+1: 16q + 8 + fh*4 + e
           }
           // v_permlane32_swap(a, b): a's lanes 32-63 <-> b's lanes 0-31.  Lane fr then holds
           // (a: own [16q, +4), b: partner's [16q+4, +4)), lane fr + 32 (a: partner's
@@ -551,7 +580,7 @@ __global__ __launch_bounds__(NT, (NT / 256) * OCC) void conv3x3_direct_kernel(co
       // this wave's stores of the band (nbw blocks x ng groups) are its youngest vector-memory
       // ops: wait for everything older -- the next band's patch DMAs -- and leave them in flight
       const int nbw = ph < NPH ? (nblk - ph + NPH - 1) / NPH : 0;
-      const int ng = (diag & 8) ? min(4, (COUT - cb * 32 + 7) / 8) : min(2, (COUT - cb * 32 + 15) / 16);
+      const int ng = (!RES && (diag & 8)) ? min(4,(COUT - cb * 32 + 7) / 8) : min(2, (COUT - cb * 32 + 15) / 16);
       direct_wait_vm_le(__builtin_amdgcn_readfirstlane(nbw * ng));
       cur ^= 1;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -697,6 +726,11 @@ struct DirectEntry {
   {CI, CO, S, KK, A, false,                                                                    \
    conv3x3_direct_kernel<CI, CO, S, KK, A, false, false, true, false, 1, kNT, 0, true>, false,  \
    true, false, 1, kNT, 0, true}
+// ... with the residual added after the activation (YOLO C2f bottleneck cv2: x + silu(conv))
+#define KV_DIRECT_DER(CI, CO, OCC)                                                               \
+  {CI, CO, 1, 3, kActSilu, true,                                                                 \
+   conv3x3_direct_kernel<CI, CO, 1, 3, kActSilu, true, false, true, false, OCC, kNT, 0, true>,   \
+   false, true, false, OCC, kNT, 0, true}
 #define KV_DIRECT_DE2(CI, CO, S, KK, A)                                                         \
   {CI, CO, S, KK, A, false,                                                                    \
    conv3x3_direct_kernel<CI, CO, S, KK, A, false, false, true, false, 2, kNT, 0, true>, false,  \
@@ -781,6 +815,8 @@ static const DirectEntry kDirect[] = {
     KV_DIRECT_DE2(16, 32, 2, 3, kActSilu), KV_DIRECT_DE2(16, 16, 1, 3, kActSilu),
     KV_DIRECT_DE2(32, 64, 2, 3, kActSilu), KV_DIRECT_DE2(32, 32, 1, 3, kActSilu),
     KV_DIRECT_DE2(32, 32, 1, 1, kActSilu), KV_DIRECT_DE2(48, 32, 1, 1, kActSilu),
+    KV_DIRECT_DER(16, 16, 1), KV_DIRECT_DER(32, 32, 1), KV_DIRECT_DER(64, 64, 1),
+    KV_DIRECT_DER(16, 16, 2), KV_DIRECT_DER(32, 32, 2),
     KV_DIRECT_SB(64, 64, 1, 3, kActRelu), KV_DIRECT_SB(64, 128, 1, 3, kActSilu),
     KV_DIRECT_SB(64, 16, 1, 3, kActSilu), KV_DIRECT_SB(64, 64, 1, 3, kActSilu),
     KV_DIRECT_SB(64, 128, 2, 3, kActSilu), KV_DIRECT_SB(64, 64, 2, 3, kActSilu),
@@ -794,6 +830,7 @@ static const DirectEntry kDirect[] = {
 #undef KV_DIRECT2
 #undef KV_DIRECT_DE
 #undef KV_DIRECT_DE2
+#undef KV_DIRECT_DER
 #undef KV_DIRECT_SB
 #undef KV_DIRECT_DE4
 #undef KV_DIRECT1
@@ -849,6 +886,7 @@ static int direct_plan(const KvConvParams* p, int tile, int* kR, int* PW, int* r
   if (!p->in_u8 && (long long)p->N * p->H * p->W * p->ldx * 2 >= kOOB) return -9;
   if ((long long)p->N * p->Ho * p->Wo * p->ldy * 2 >= kOOB) return -9;
   if (p->pair_1x1 && (long long)p->N * p->Ho * p->Wo * p->ldz * 2 >= kOOB) return -9;
+  if (res && (long long)p->N * p->Ho * p->Wo * p->ldr * 2 >= kOOB) return -9;
   const int S = p->stride;
   *PW = (p->Wo - 1) * S + kk;
   const int pb = direct_pb(p->Cin);
@@ -949,7 +987,10 @@ int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
 // v10 tile 0 / 1: the DMA direct-epilogue form at 1 / 2 workgroups per CU (8 waves);
 // tile 2: its single-buffer 4-wave form, two workgroups per CU
 int direct_de_launch(const KvConvParams* p, int tile, hipStream_t stream) {
-  if (tile < 0 || tile >= direct_de_num_tiles() || p->res || p->pair_1x1) return -8;
+  if (tile < 0 || tile >= direct_de_num_tiles() || p->pair_1x1) return -8;
+  // KVEDGE_DE_RES=0: the residual forms refuse (same-box A/B against the v1 / v4 picks)
+  static const bool de_res = !getenv("KVEDGE_DE_RES") || atoi(getenv("KVEDGE_DE_RES")) != 0;
+  if (p->res && !de_res) return -8;
   static const int code[3] = {4 | 1, 4 | 2 | 1, 4 | 8 | 2 | 1};
   return direct_launch(p, code[tile], stream);
 }

@@ -129,11 +129,20 @@ DE_SHAPES = {
 }
 
 
+# ... with the residual added after the activation (YOLO C2f bottleneck cv2), tiles 0 / 1
+DE_RES_SHAPES = {
+    0: {(16, 16, 3, 1, ops.ACT_SILU), (32, 32, 3, 1, ops.ACT_SILU), (64, 64, 3, 1, ops.ACT_SILU)},
+    1: {(16, 16, 3, 1, ops.ACT_SILU), (32, 32, 3, 1, ops.ACT_SILU)},
+    2: set(),
+}
+
+
 def _de_takes(tile, cin, cout, k, s, act, res):
     """Mirror of direct_plan() for a v10 tile: an instantiated shape, or a Cout covered by
-    instantiated slices (largest first, e.g. 144 = 128 + 16), never a residual."""
+    instantiated slices (largest first, e.g. 144 = 128 + 16); a residual only for its own
+    instantiations (no slicing)."""
     if res:
-        return False
+        return (cin, cout, k, s, act) in DE_RES_SHAPES[tile - DE0]
     shapes = DE_SHAPES[tile - DE0]
     if (cin, cout, k, s, act) in shapes:
         return True
@@ -532,6 +541,8 @@ def test_conv_poisoned_canary(tile, k):
     (2, 21, 19, 16, 16, 1, ops.ACT_SILU, True, 16, 16, 16, 0),   # C2f bottleneck 16
     (2, 20, 20, 32, 64, 2, ops.ACT_SILU, False, 0, 0, 0, 0),     # YOLO b3
     (2, 20, 20, 32, 32, 1, ops.ACT_SILU, True, 0, 0, 0, 0),
+    (2, 40, 40, 64, 64, 1, ops.ACT_SILU, True, 0, 0, 0, 0),      # C2f bottleneck 64 (+res)
+    (3, 13, 11, 32, 32, 1, ops.ACT_SILU, True, 32, 32, 8, 8),    # +res: tails, x / y slices
     (2, 19, 17, 64, 128, 2, ops.ACT_SILU, False, 0, 0, 0, 0),    # YOLO b5 (odd H, W)
     (2, 10, 10, 64, 64, 2, ops.ACT_SILU, False, 0, 0, 0, 0),     # h16
     (1, 160, 160, 16, 16, 1, ops.ACT_SILU, False, 0, 0, 0, 0),   # full YOLO row width

@@ -23,7 +23,8 @@ def run(a):
     else:
         from kvedge_amd.models.yolov8 import KvYoloV8n as M
     model = M.build(seed=0, device="cuda")
-    eng = InferenceEngine(model, a.batch, M.image_size, device="cuda").prepare(warmup=2)
+    eng = InferenceEngine(model, a.batch, M.image_size, device="cuda",
+                          streams=a.streams).prepare(warmup=2)
     for _ in range(3):
         eng.run()
     torch.cuda.synchronize()
@@ -45,7 +46,7 @@ def summarize(path, reps):
     for r in body:
         name = r["Kernel_Name"].replace("void ", "").replace(
             "kvedge::(anonymous namespace)::", "").split("(")[0]
-        key = (name[:60], r.get("Grid_Size_X", r.get("Grid_Size", "")))
+        key = (name[:110], r.get("Grid_Size_X", r.get("Grid_Size", "")))
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         agg.setdefault(key, []).append(dur)
     total = sum(sum(v) for v in agg.values()) / reps
@@ -63,6 +64,8 @@ if __name__ == "__main__":
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--streams", type=int, default=1,
+                    help="batch slices on HIP streams (the bench uses engine.BENCH_STREAMS)")
     ap.add_argument("--summarize", default=None)
     a = ap.parse_args()
     if a.summarize:
