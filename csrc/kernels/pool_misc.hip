@@ -75,6 +75,21 @@ __global__ __launch_bounds__(kBlock) void maxpool_kernel(const bf16* __restrict_
 // radius-2/4/6 row-max images of the previous version) -> 2.5x the workgroups per CU, and
 // 5 + 5 reads per output per stage instead of 13 + (5 + 9 + 13) for the whole pass.
 constexpr int kSppfCg = 16;  // channels per workgroup
+typedef short sppf_i16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned sppf_key2(unsigned w) {
+  const sppf_i16x2 x = __builtin_bit_cast(sppf_i16x2, w);
+  return __builtin_bit_cast(unsigned, x ^ ((x >> 15) & (short)0x7fff));
+}
+__device__ __forceinline__ uint4 sppf_key4(uint4 v) {
+  return make_uint4(sppf_key2(v.x), sppf_key2(v.y), sppf_key2(v.z), sppf_key2(v.w));
+}
+__device__ __forceinline__ unsigned sppf_max2(unsigned a, unsigned b) {
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(sppf_i16x2, a),
+                                                                __builtin_bit_cast(sppf_i16x2, b)));
+}
+__device__ __forceinline__ uint4 sppf_max4(uint4 a, uint4 b) {
+  return make_uint4(sppf_max2(a.x, b.x), sppf_max2(a.y, b.y), sppf_max2(a.z, b.z), sppf_max2(a.w, b.w));
+}
 __global__ __launch_bounds__(kBlock) void sppf_kernel(bf16* __restrict__ buf, int N, int H,
                                                       int W, int C) {
   extern __shared__ __attribute__((aligned(16))) bf16 sp[];  // 2 x [H*W][16]
@@ -87,51 +102,41 @@ __global__ __launch_bounds__(kBlock) void sppf_kernel(bf16* __restrict__ buf, in
   bf16* base = buf + (long long)n * HW * ld + cg * kSppfCg;
   for (int q = threadIdx.x; q < HW * 2; q += kBlock) {  // 2 x 16 B per pixel
     const int pix = q >> 1, hf = q & 1;
-    *reinterpret_cast<bf16x8*>(a + pix * kSppfCg + hf * 8) =
-        *reinterpret_cast<const bf16x8*>(base + (long long)pix * ld + hf * 8);
+    *reinterpret_cast<uint4*>(a + pix * kSppfCg + hf * 8) =
+        sppf_key4(*reinterpret_cast<const uint4*>(base + (long long)pix * ld + hf * 8));
   }
-  // max of bf16 values is exact in bf16: no float round trip needed beyond the compare
+  // Max on order-preserving int16 keys, two channels per v_pk_max_i16: key(x) = x ^ 0x7fff
+  // for negative bf16 x (sign set: the magnitude bits flipped, so a larger magnitude orders
+  // lower), x otherwise.  The map is its own inverse and exact; the previous float path spent
+  // 8 converts + 8 fmax per 16-B read.  x is stored as keys.  Out-of-image taps are clamped
+  // onto in-window pixels (a duplicate never changes a max): the tap loops have no branches.
   for (int k = 1; k <= 3; ++k) {
-    __syncthreads();  // a complete (x or y_{k-1})
+    __syncthreads();  // a complete (keys of x or y_{k-1})
     for (int q = threadIdx.x; q < HW * 2; q += kBlock) {  // t = row max, radius 2
       const int pix = q >> 1, hf = q & 1;
       const int y = pix / W, x = pix - y * W;
-      float m[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+      uint4 m = *reinterpret_cast<const uint4*>(a + pix * kSppfCg + hf * 8);
 #pragma unroll
       for (int dx = -2; dx <= 2; ++dx) {
-        const int xi = x + dx;
-        if ((unsigned)xi >= (unsigned)W) continue;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(a + (y * W + xi) * kSppfCg + hf * 8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], (float)v[j]);
+        if (dx == 0) continue;
+        const int xi = min(max(x + dx, 0), W - 1);
+        m = sppf_max4(m, *reinterpret_cast<const uint4*>(a + (y * W + xi) * kSppfCg + hf * 8));
       }
-      bf16x8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(m[j]);
-      *reinterpret_cast<bf16x8*>(t + pix * kSppfCg + hf * 8) = o;
+      *reinterpret_cast<uint4*>(t + pix * kSppfCg + hf * 8) = m;
     }
     __syncthreads();  // t complete; a no longer read
     for (int q = threadIdx.x; q < HW * 2; q += kBlock) {  // a = y_k = column max of t
       const int pix = q >> 1, hf = q & 1;
       const int y = pix / W, x = pix - y * W;
-      float m[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) m[j] = -INFINITY;
+      uint4 m = *reinterpret_cast<const uint4*>(t + pix * kSppfCg + hf * 8);
 #pragma unroll
       for (int dy = -2; dy <= 2; ++dy) {
-        const int yi = y + dy;
-        if ((unsigned)yi >= (unsigned)H) continue;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(t + (yi * W + x) * kSppfCg + hf * 8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], (float)v[j]);
+        if (dy == 0) continue;
+        const int yi = min(max(y + dy, 0), H - 1);
+        m = sppf_max4(m, *reinterpret_cast<const uint4*>(t + (yi * W + x) * kSppfCg + hf * 8));
       }
-      bf16x8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(m[j]);
-      if (k < 3) *reinterpret_cast<bf16x8*>(a + pix * kSppfCg + hf * 8) = o;
-      *reinterpret_cast<bf16x8*>(base + (long long)pix * ld + k * C + hf * 8) = o;
+      if (k < 3) *reinterpret_cast<uint4*>(a + pix * kSppfCg + hf * 8) = m;
+      *reinterpret_cast<uint4*>(base + (long long)pix * ld + k * C + hf * 8) = sppf_key4(m);
     }
   }
 }
