@@ -44,7 +44,7 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("KVEDGE_BENCH_BATCH", 0)),
                     help="per-GPU batch (0 = kvedge_amd.engine.BENCH_BATCH: ResNet-50 1280, "
-                         "YOLOv8n 384, from the batch sweeps in profiles/)")
+                         "YOLOv8n 512, from the batch sweeps in profiles/)")
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "yolov8n"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--streams", type=int, default=int(os.environ.get("KVEDGE_STREAMS", 0)),

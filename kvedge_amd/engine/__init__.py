@@ -23,10 +23,12 @@ from .. import ops
 # Per-GPU batch bench.py times by default (and tests/test_bench_config_gpu.py checks).
 # ResNet-50: 1280, from the same-box batch sweeps (profiles/r2_v8_batch_sweep.jsonl):
 # 79.6-80.3k img/s at 1280 against 78.1-78.2k at 640, the largest batch whose activations
-# still fit one launch per conv (2 GiB per operand; ~1330 images).  YOLOv8n: 384 (sweep knee,
-# profiles/r1_v13_batch_sweep.jsonl).  Edge-module serving uses its own, latency-bound batch
+# still fit one launch per conv (2 GiB per operand; ~1330 images); re-checked on the round-4
+# tree (profiles/r4_v7_resnet50_batch_recheck.md).  YOLOv8n: 512, from the round-4 same-box
+# re-check (profiles/r4_v7_yolov8n_batch_recheck.md: 46.5-46.8k against 45.9-46.0k at 384;
+# 384 was round 1's sweep knee).  Edge-module serving uses its own, latency-bound batch
 # (module twin `batch`, default 64).
-BENCH_BATCH = {"resnet50": 1280, "yolov8n": 384}
+BENCH_BATCH = {"resnet50": 1280, "yolov8n": 512}
 # Batch slices per step, each on its own HIP stream (parallel branches of one hipGraph).
 # Two slices run concurrently fill each other's kernel drain/fill bubbles (same-box A/B,
 # profiles/r2_v17_streams_ab.jsonl): ResNet-50 b1280 75.4k -> 79.9k img/s, YOLOv8n b384
