@@ -89,15 +89,17 @@ apt:
       keyid: BC528686B50D79E339D3721CEB3E94ADBE1229CF
 {{- end }}
 bootcmd:
-  - [sh, -c, "mkdir -p /mnt/app-secret /var/lib/kvedge && echo \"bootcmd $(date +%s.%N)\" >> /var/lib/kvedge/boot-timing"]
+  - [sh, -c, "mkdir -p /mnt/app-secret /var/lib/kvedge && echo \"bootcmd $(date +%s.%N) $(cat /proc/sys/kernel/random/boot_id)\" >> /var/lib/kvedge/boot-timing"]
   - [sh, -c, "mountpoint -q /mnt/app-secret || mount -o ro /dev/disk/by-id/virtio-{{ include "kvedge.secretSerial" . }} /mnt/app-secret || mount -o ro /dev/$(lsblk -dno NAME,SERIAL | awk '$2==\"{{ include "kvedge.secretSerial" . }}\"{print $1}') /mnt/app-secret"]
 write_files:
   - path: /usr/local/sbin/kvedge-stamp
     permissions: "0755"
     content: |
       #!/bin/sh
+      # "<name> <epoch> <boot id>": the boot id scopes a stamp to one boot (the file is on
+      # the persistent boot disk and keeps every boot's stamps for the collector)
       mkdir -p /var/lib/kvedge
-      echo "$1 $(date +%s.%N)" >> /var/lib/kvedge/boot-timing
+      echo "$1 $(date +%s.%N) $(cat /proc/sys/kernel/random/boot_id 2>/dev/null)" >> /var/lib/kvedge/boot-timing
   - path: /usr/local/sbin/kvedge-apply-config
     permissions: "0755"
     content: |
@@ -173,19 +175,25 @@ write_files:
     permissions: "0755"
     content: |
       #!/bin/sh
-      # VMI probe (guest-agent exec): `ready` = the module heartbeat is fresh (or, with no
-      # module, iotedge check passed); `live` = no STALE heartbeat (absent is fine: booting)
+      # VMI probe (guest-agent exec).  Evidence counts only if THIS boot wrote it: the
+      # heartbeat and boot-timing live on the persistent boot disk, so a previous boot's
+      # fresh heartbeat or iotedge_check_pass line must not make a restarted VMI Ready.
+      #   ready = this boot's module heartbeat is fresh (or, with no module, this boot's
+      #           iotedge check passed)
+      #   live  = no STALE heartbeat of this boot (none yet, or a previous boot's: booting)
       hb=/var/lib/kvedge/heartbeat; max={{ $v.health.heartbeatMaxAgeS }}
+      boot=$(cat /proc/sys/kernel/random/boot_id 2>/dev/null)
       age() { echo $(( $(date +%s) - $(stat -c %Y "$hb") )); }
+      this_boot() { [ -n "$boot" ] && [ -f "$hb" ] && grep -qF "\"boot_id\": \"$boot\"" "$hb"; }
       case "$1" in
         ready)
       {{- if $v.module.enabled }}
-          [ -f "$hb" ] && [ "$(age)" -le "$max" ] ;;
+          this_boot && [ "$(age)" -le "$max" ] ;;
       {{- else }}
-          grep -q '^iotedge_check_pass ' /var/lib/kvedge/boot-timing 2>/dev/null ;;
+          [ -n "$boot" ] && awk -v b="$boot" '$1=="iotedge_check_pass" && $3==b {f=1} END{exit !f}' /var/lib/kvedge/boot-timing 2>/dev/null ;;
       {{- end }}
         live)
-          [ ! -f "$hb" ] || [ "$(age)" -le "$max" ] ;;
+          ! this_boot || [ "$(age)" -le "$max" ] ;;
         *) exit 2 ;;
       esac
   - path: /etc/systemd/system/kvedge-config.service

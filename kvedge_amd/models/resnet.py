@@ -157,14 +157,17 @@ class DeployedBottleneck:
         return (c1.cout in (64, 128) and (self.dual is not None or self.down is None) and
                 (self.dual is None or c1.cout == 64) and k <= 128)
 
-    def tail_fits(self, x: torch.Tensor) -> bool:
+    def tail_fits(self, x: torch.Tensor, batch: int = 0) -> bool:
         """Batch-size gate of the fused boundary for input ``x``: the v9 seam gives each
         8-wave workgroup 128 rows and walks every y tile in it, so it only pays when the
         layer has rows for a workgroup on every CU (ops.SEAM_MIN_WGS); edge batches keep
-        the split-K conv3 and conv1 launches.  The stage-1 tail has no such limit."""
+        the split-K conv3 and conv1 launches.  The stage-1 tail has no such limit.
+        ``batch``: gate on this batch instead of x's (micro-batches use the FULL batch, so
+        both paths fuse the same boundaries and round y the same way -- ADVICE r4)."""
         if self.c3.spec.cout == 256:
             return True
         N, Ho, Wo, _ = self.out_shape(x.shape)
+        N = batch or N
         return (N * Ho * Wo + 127) // 128 >= ops.SEAM_MIN_WGS
 
     def call_tail(self, x, nxt: "DeployedBottleneck", t1=None, out=None, z=None):
@@ -270,9 +273,11 @@ class KvResNet50:
                 for j in range(nb):
                     b, nxt = self.blocks[j], self.blocks[j + 1]
                     last = j == nb - 1
-                    # the same batch gate as the whole-batch path below: a seam at micro-batch
-                    # size where the whole batch runs the pair unfused changes y's bf16 rounding
-                    fuse = self.fuse_tail and y.is_cuda and b.can_tail(nxt) and b.tail_fits(y)
+                    # the same batch gate as the whole-batch path below, evaluated on the
+                    # FULL batch B: a micro-batch-sized gate would fuse (or not) differently
+                    # from the whole-batch path and change y's bf16 rounding
+                    fuse = (self.fuse_tail and y.is_cuda and b.can_tail(nxt) and
+                            b.tail_fits(y, batch=B))
                     if last and full is None:
                         shp = b.out_shape(y.shape)
                         full = ops.empty((B,) + shp[1:], dtype=y.dtype, device=y.device)

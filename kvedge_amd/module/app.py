@@ -57,6 +57,19 @@ from .config import ModuleConfig
 from .transport import Deferred, Transport, now_iso
 
 BOUNDARY_S = 0.2  # target spacing of lockstep control boundaries (auto sync_every)
+# heartbeat cadence, independent of telemetry (well under the chart's default
+# health.heartbeatMaxAgeS = 120 s, whatever report_interval_s / max_messages are)
+HEARTBEAT_S = 10.0
+BOOT_ID_PATH = "/proc/sys/kernel/random/boot_id"
+
+
+def _read_boot_id(path: str) -> str:
+    """The kernel's per-boot UUID ('' where there is none: non-Linux, tests)."""
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return ""
 NOT_CONTROL_POINT = ("fleet configuration is controlled by rank 0's twin (VM 0); "
                      "this device is rank {rank}")
 
@@ -129,7 +142,7 @@ class ModuleApp:
     def __init__(self, transport: Transport, config: Optional[ModuleConfig] = None,
                  device: Optional[str] = None, state_path: Optional[str] = None,
                  clock=time.perf_counter, stamp_path: Optional[str] = None,
-                 heartbeat_path: Optional[str] = None):
+                 heartbeat_path: Optional[str] = None, boot_id_path: str = BOOT_ID_PATH):
         self.tr = transport
         self.cfg = (config or ModuleConfig()).validate()
         self.device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
@@ -140,6 +153,10 @@ class ModuleApp:
         # module liveness for the VMI probes (chart: kvedge-health reads its mtime): one
         # small JSON rewritten atomically at every telemetry report, local rank 0 only
         self.heartbeat_path = heartbeat_path
+        # the guest's boot id goes into the heartbeat and the stamps: the chart's
+        # `kvedge-health` accepts only evidence written during the current boot
+        self.boot_id = _read_boot_id(boot_id_path)
+        self._last_hb = None  # clock() of the last heartbeat write
         self.clock = clock
         self.engine = None
         self.model = None
@@ -305,7 +322,7 @@ class ModuleApp:
         try:
             os.makedirs(os.path.dirname(self.stamp_path) or ".", exist_ok=True)
             with open(self.stamp_path, "a") as f:
-                f.write(f"{name} {time.time():.6f}\n")
+                f.write(f"{name} {time.time():.6f} {self.boot_id}\n".rstrip() + "\n")
         except OSError:
             pass  # read-only / missing mount: timing is best-effort, never fatal
 
@@ -316,12 +333,23 @@ class ModuleApp:
             os.makedirs(os.path.dirname(self.heartbeat_path) or ".", exist_ok=True)
             tmp = self.heartbeat_path + ".tmp"
             with open(tmp, "w") as f:
-                json.dump({"ts": time.time(), "heartbeat": self.state["total_steps"],
+                json.dump({"ts": time.time(), "boot_id": self.boot_id,
+                           "heartbeat": self.state["total_steps"],
+                           "messages": self.state["messages"],
                            "images_per_s": msg.get("images_per_s"),
                            "model": self.cfg.model, "rank": self.rank}, f)
             os.replace(tmp, self.heartbeat_path)
         except OSError:
             pass  # read-only / missing mount: the probe then reports not-ready, never fatal
+        self._last_hb = self.clock()
+
+    def _heartbeat_due(self):
+        """Liveness on a fixed cadence (HEARTBEAT_S), independent of telemetry: a module
+        whose simulated sensor hit max_messages, or whose report interval exceeds the
+        probe's max age, is still alive and must keep its heartbeat fresh."""
+        if self.heartbeat_path and (self._last_hb is None or
+                                    self.clock() - self._last_hb >= HEARTBEAT_S):
+            self._heartbeat(self.last_telemetry or {})
 
     def _build_local(self):
         """Build model + engine for self.cfg on this rank (no collectives)."""
@@ -408,6 +436,7 @@ class ModuleApp:
             self._sim_step()
         elif self.engine is not None:
             self._infer_step()
+        self._heartbeat_due()
         self._tick += 1
         self._since_boundary += 1
         if self._since_boundary >= self.sync_every:
@@ -460,7 +489,6 @@ class ModuleApp:
                 self.state["messages"] += 1
                 self._last_report = now
                 self._save_state()
-                self._heartbeat({})
                 if not self._first_inference_stamped:
                     self._first_inference_stamped = True
                     self._stamp("module_first_message")

@@ -80,19 +80,33 @@ def visible_gpu_count(topology: Optional[str] = None) -> int:
     whose ``gfx_target_version`` is non-zero (CPU nodes report 0).  The visibility masks
     are applied in the runtime's order: ROCR_VISIBLE_DEVICES selects among the agents,
     then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES index into what is left.
-    ``KVEDGE_KFD_TOPOLOGY`` overrides the sysfs root (tests)."""
+    The sysfs topology is not per-container: a process that a cgroup / device plugin
+    limits to some of the render nodes still sees every GPU there.  Like the ROCm runtime,
+    which enumerates only the agents whose ``/dev/dri/renderD<drm_render_minor>`` it can
+    open, a GPU node counts only if that node is readable and writable.
+    ``KVEDGE_KFD_TOPOLOGY`` / ``KVEDGE_DRI_ROOT`` override the sysfs and /dev/dri roots
+    (tests)."""
     import glob
 
     root = topology or os.environ.get("KVEDGE_KFD_TOPOLOGY", _KFD_TOPOLOGY)
+    dri = os.environ.get("KVEDGE_DRI_ROOT", "/dev/dri")
+    check_dri = os.path.isdir(dri)  # no /dev/dri view at all: nothing to check against
     n = 0
-    for prop in glob.glob(os.path.join(root, "*", "properties")):
+    for prop in sorted(glob.glob(os.path.join(root, "*", "properties"))):
         try:
+            kv = {}
             with open(prop) as f:
                 for ln in f:
                     k, _, v = ln.partition(" ")
-                    if k == "gfx_target_version":
-                        n += int(v.strip() or 0) != 0
-                        break
+                    kv[k] = v.strip()
+            if int(kv.get("gfx_target_version", "0") or 0) == 0:
+                continue
+            minor = kv.get("drm_render_minor")
+            if check_dri and minor is not None and int(minor) > 0:
+                node = os.path.join(dri, f"renderD{int(minor)}")
+                if not os.access(node, os.R_OK | os.W_OK):
+                    continue  # masked from this container / cgroup
+            n += 1
         except (OSError, ValueError):
             continue
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):

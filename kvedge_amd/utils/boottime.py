@@ -79,11 +79,12 @@ def vmi_running_at(vmi_json: dict) -> Optional[float]:
 
 
 def parse_stamps(text: str) -> Dict[str, float]:
-    """Guest stamp file -> {name: first epoch} (later duplicates = later boots, kept as name#n)."""
+    """Guest stamp file -> {name: first epoch} (later duplicates = later boots, kept as name#n).
+    Lines are ``<name> <epoch>`` or, since round 5, ``<name> <epoch> <boot id>``."""
     out: Dict[str, float] = {}
     for ln in text.splitlines():
         parts = ln.split()
-        if len(parts) != 2:
+        if len(parts) not in (2, 3):
             continue
         name, t = parts[0], float(parts[1])
         key, n = name, 1

@@ -239,7 +239,8 @@ def _fake_root_script(script: str, root) -> str:
             .replace("/etc/aziot", f"{root}/etc/aziot")
             .replace("/var/lib/kvedge", f"{root}/var/lib/kvedge")
             .replace("/usr/local/sbin/kvedge-stamp", f"{root}/stamp")
-            .replace("/dev/kfd", f"{root}/dev/kfd").replace("/dev/dri", f"{root}/dev/dri"))
+            .replace("/dev/kfd", f"{root}/dev/kfd").replace("/dev/dri", f"{root}/dev/dri")
+            .replace("/proc/sys/kernel/random/boot_id", f"{root}/boot_id"))
 
 
 def test_cloudinit_scripts_in_fake_root(tmp_path):
@@ -483,32 +484,60 @@ def test_vmi_health_probes_and_heartbeat_script(tmp_path):
     dep = json.loads(cm["data"]["deployment.json"])
     env = dep["modulesContent"]["$edgeAgent"]["properties.desired"]["modules"]["kvedge"]["env"]
     assert env["KVEDGE_HEARTBEAT"]["value"] == "/var/lib/kvedge/heartbeat"
-    # the script, in a fake root
+    # the script, in a fake root (its own boot id file)
     files = {f["path"]: f["content"] for f in ci["write_files"]}
     (tmp_path / "var/lib/kvedge").mkdir(parents=True)
+    boot_id = tmp_path / "boot_id"
+    boot_id.write_text("boot-A\n")
     sh = tmp_path / "health.sh"
     sh.write_text(_fake_root_script(files["/usr/local/sbin/kvedge-health"], tmp_path))
     probe = lambda what: subprocess.run(["sh", str(sh), what]).returncode  # noqa: E731
     assert probe("ready") != 0 and probe("live") == 0  # booting: no heartbeat yet
-    # the module writes the heartbeat at its first report
+    # the module writes the heartbeat (with the boot id) from its first step on
     tr = FakeTransport({"model": "simulated-temperature", "send_interval_s": 1.0})
     hb = tmp_path / "var/lib/kvedge/heartbeat"
-    app = ModuleApp(tr, device="cpu", heartbeat_path=str(hb)).start()
+    app = ModuleApp(tr, device="cpu", heartbeat_path=str(hb), boot_id_path=str(boot_id)).start()
     app.run(max_steps=2)
     app.stop()
-    assert json.loads(hb.read_text())["model"] == "simulated-temperature"
+    beat = json.loads(hb.read_text())
+    assert beat["model"] == "simulated-temperature" and beat["boot_id"] == "boot-A"
     assert probe("ready") == 0 and probe("live") == 0
     old = time.time() - 3600
     os.utime(hb, (old, old))  # module hung: heartbeat stale
     assert probe("ready") != 0 and probe("live") != 0
-    # module disabled: readiness = iotedge check passed
+    # the VMI restarted.  The heartbeat the previous boot wrote
+    # 5 s ago is fresh by age but from another boot: not ready (and live: booting)
+    recent = time.time() - 5
+    os.utime(hb, (recent, recent))
+    boot_id.write_text("boot-B\n")
+    assert probe("ready") != 0 and probe("live") == 0
+    # ... until this boot's module writes its own
+    app2 = ModuleApp(FakeTransport({"model": "simulated-temperature"}), device="cpu",
+                     heartbeat_path=str(hb), boot_id_path=str(boot_id)).start()
+    app2.run(max_steps=1)
+    app2.stop()
+    assert probe("ready") == 0 and probe("live") == 0
+    # module disabled: readiness = THIS boot's iotedge check passed
     _, objs2 = render(sets=["module.enabled=false"])
     _, ci2 = _cloudinit(objs2)
-    f2 = {f["path"]: f["content"] for f in ci2["write_files"]}["/usr/local/sbin/kvedge-health"]
-    sh.write_text(_fake_root_script(f2, tmp_path))
+    f2 = {f["path"]: f["content"] for f in ci2["write_files"]}
+    sh.write_text(_fake_root_script(f2["/usr/local/sbin/kvedge-health"], tmp_path))
     assert probe("ready") != 0
-    (tmp_path / "var/lib/kvedge/boot-timing").write_text("iotedge_check_pass 1.0\n")
+    stamp = tmp_path / "stamp"
+    stamp.write_text(_fake_root_script(f2["/usr/local/sbin/kvedge-stamp"], tmp_path))
+    bt = tmp_path / "var/lib/kvedge/boot-timing"
+    # (ii) an iotedge_check_pass line from before the last bootcmd (the previous boot)
+    bt.write_text("bootcmd 1.0 boot-B\niotedge_check_pass 2.0 boot-B\n")
+    boot_id.write_text("boot-C\n")
+    bt.write_text(bt.read_text() + "bootcmd 3.0 boot-C\n")
+    assert probe("ready") != 0
+    assert subprocess.run(["sh", str(stamp), "iotedge_check_pass"]).returncode == 0
+    assert bt.read_text().splitlines()[-1].split()[2] == "boot-C"
     assert probe("ready") == 0
+    # the stamp collector still reads every boot's lines
+    from kvedge_amd.utils.boottime import parse_stamps
+    st = parse_stamps(bt.read_text())
+    assert "iotedge_check_pass#2" in st and "bootcmd#2" in st
     _, objs3 = render(sets=["health.enabled=false"])
     spec3 = by_kind(objs3, "VirtualMachine")[0]["spec"]["template"]["spec"]
     assert "readinessProbe" not in spec3 and "livenessProbe" not in spec3

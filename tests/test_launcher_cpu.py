@@ -79,6 +79,27 @@ def test_visible_gpu_count_from_sysfs(tmp_path, monkeypatch):
     assert parallel.visible_gpu_count(str(tmp_path / "missing")) == 0
 
 
+def test_visible_gpu_count_skips_masked_render_nodes(tmp_path, monkeypatch):
+    """sysfs lists every GPU of the host; a container limited to some
+    render nodes must count only the GPUs whose /dev/dri/renderD<minor> it can open."""
+    topo = _fake_topology(tmp_path / "nodes", [0, 90500, 90500, 90500])
+    for i, minor in ((1, 128), (2, 129), (3, 130)):
+        with open(tmp_path / "nodes" / str(i) / "properties", "a") as f:
+            f.write(f"drm_render_minor {minor}\n")
+    dri = tmp_path / "dri"
+    dri.mkdir()
+    for minor in (128, 130):
+        (dri / f"renderD{minor}").write_text("")
+    for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("KVEDGE_DRI_ROOT", str(dri))
+    assert parallel.visible_gpu_count(topo) == 2
+    (dri / "renderD129").write_text("")
+    assert parallel.visible_gpu_count(topo) == 3
+    monkeypatch.setenv("KVEDGE_DRI_ROOT", str(tmp_path / "no-dri"))  # no view: trust sysfs
+    assert parallel.visible_gpu_count(topo) == 3
+
+
 def test_bench_launcher_never_touches_hip(tmp_path):
     """GPU path of the launcher: devices counted from sysfs; too few -> clean refusal,
     and no torch.cuda call on the way."""

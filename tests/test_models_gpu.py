@@ -187,6 +187,25 @@ def test_resnet50_microbatch_fused_tail(resnet, mb, nb):
     assert torch.allclose(lg_full, lg_mb, atol=1e-2, rtol=1e-2), (lg_full - lg_mb).abs().max()
 
 
+def test_resnet50_microbatch_seam_gate_uses_full_batch(resnet, monkeypatch):
+    """the seam gate of the micro-batched blocks is evaluated on the FULL
+    batch.  With SEAM_MIN_WGS between the micro-batch's and the full batch's workgroup
+    counts (8 images at 28x28: 49 workgroups of 128 rows; micro-batch 2: 13), both paths
+    must fuse the same stage-2 boundary and give the same logits."""
+    _, kv, _ = resnet
+    monkeypatch.setattr(ops, "SEAM_MIN_WGS", 20)
+    fr = _frames(8, 6).cuda()
+    with torch.no_grad():
+        lg_full = kv.logits(fr, frames_in=True).float()
+        kv.microbatch, kv.microbatch_blocks = 2, 5
+        try:
+            lg_mb = kv.logits(fr, frames_in=True).float()
+        finally:
+            kv.microbatch, kv.microbatch_blocks = 0, 3
+    torch.cuda.synchronize()
+    assert torch.allclose(lg_full, lg_mb, atol=1e-2, rtol=1e-2), (lg_full - lg_mb).abs().max()
+
+
 @pytest.mark.parametrize("hw,n", [((224, 224), 3), ((64, 96), 5), ((38, 20), 5), ((224, 224), 40),
                                   ((36, 20), 300), ((22, 28), 7)])
 def test_stem12_pool_frames_kernel(resnet, hw, n):

@@ -42,6 +42,46 @@ def test_simulated_temperature_module(tmp_path):
     app.stop()
 
 
+def test_heartbeat_outlives_the_message_cap_and_restarts(tmp_path):
+    """the simulated sensor stops SENDING at max_messages, but the module
+    is alive and its heartbeat must stay fresh -- also after a restart that resumes with
+    the cap already reached (else `kvedge-health live` fails and KubeVirt restarts the VM
+    forever).  The heartbeat runs on its own cadence (app.HEARTBEAT_S), not on sends."""
+    from kvedge_amd.module import app as app_mod
+
+    state, hb = str(tmp_path / "s.json"), tmp_path / "heartbeat"
+    clk = Clock()
+    cfg = {"model": "simulated-temperature", "send_interval_s": 1.0, "max_messages": 2,
+           "report_interval_s": 600.0}
+    tr = FakeTransport(cfg)
+    a = ModuleApp(tr, device="cpu", state_path=state, clock=clk, heartbeat_path=str(hb)).start()
+    a.run(max_steps=400)  # 100 s on the fake clock, far past the cap
+    a.stop()
+    assert len(tr.outputs("temperatureOutput")) == 2
+    beats = []
+    orig = ModuleApp._heartbeat
+
+    def spy(self, msg):
+        beats.append(self.clock.t)
+        return orig(self, msg)
+
+    ModuleApp._heartbeat = spy
+    try:  # restart: the state file says the cap is reached; nothing is sent, beats go on
+        tr2 = FakeTransport(cfg)
+        clk2 = Clock()
+        a2 = ModuleApp(tr2, device="cpu", state_path=state, clock=clk2,
+                       heartbeat_path=str(hb)).start()
+        a2.run(max_steps=400)
+        a2.stop()
+    finally:
+        ModuleApp._heartbeat = orig
+    assert tr2.outputs("temperatureOutput") == []
+    assert len(beats) >= 9  # 100 s / HEARTBEAT_S
+    gaps = [b - a_ for a_, b in zip(beats, beats[1:])]
+    assert max(gaps) <= app_mod.HEARTBEAT_S + 0.5
+    assert json.loads(hb.read_text())["messages"] == 2
+
+
 def test_resnet_module_twin_methods_resume(tmp_path):
     state = str(tmp_path / "state.json")
     tr = FakeTransport({"model": "resnet50", "batch": 1, "report_interval_s": 1.0,

@@ -282,3 +282,35 @@ def test_kubectl_cluster_reports_unschedulable_and_node_loss():
     assert rec[names[0]].ok and rec[names[0]].to_node == "node-b"
     assert not rec[names[1]].ok and "timed out" in rec[names[1]].reason
     assert any("--for=condition=Ready" in c and names[0] in c for c in seen)
+
+
+def test_module_ready_is_scoped_to_the_new_boot():
+    """VERDICT r4 next #3 / ADVICE r4 (medium): the heartbeat lives on the persistent boot
+    disk.  A heartbeat the previous boot wrote 5 s before the VMI died is fresh by age, but
+    it must not make the restarted VMI Ready: readiness comes only from a heartbeat of the
+    CURRENT boot, i.e. no earlier than the new boot + the module's start-up time."""
+    c, ctl = _cluster(access=RWX)
+    ctl.reconcile()
+    old = c.vmis["vm0"]
+    c.module_heartbeat("vm0")          # the old boot's module, alive
+    c.advance(5.0)
+    assert c.probe_ready("vm0")
+    src = old.node
+    rec = {r.vm: r for r in ctl.drain(src)}["vm0"]
+    new = c.vmis["vm0"]
+    assert new.boot_id != old.boot_id
+    ev = {w: t for t, v, w, _ in [(e.t, e.vm, e.what, e.detail) for e in c.events]
+          if v == "vm0"}
+    # the old heartbeat was < 120 s old when the new VMI came up, yet Ready waited for
+    # the new boot's own module
+    assert rec.ok and rec.module_ready
+    assert ev["module_ready"] >= new.booted_at + c.timings.module_ready
+    assert c.pvcs["vm0-dv"].heartbeat[0] == new.boot_id
+    # a module that never starts on the new boot: the previous boot's heartbeat alone
+    # never passes the probe
+    c2, ctl2 = _cluster(access=RWX)
+    ctl2.reconcile()
+    c2.module_heartbeat("vm0")
+    c2.break_module("vm0")
+    rec2 = {r.vm: r for r in ctl2.drain(c2.vmis["vm0"].node)}["vm0"]
+    assert not rec2.ok and not rec2.module_ready
