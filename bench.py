@@ -73,6 +73,10 @@ def main(argv=None):
     ap.add_argument("--edge", default=os.environ.get("KVEDGE_EDGE", "1,8,64"),
                     help="ResNet-50: after the headline (untimed for it), p50/p99 latency at "
                          "these edge batch sizes -> extra.edge ('' = skip)")
+    ap.add_argument("--yolo", type=int, default=int(os.environ.get("KVEDGE_BENCH_YOLO", 1)),
+                    help="ResNet-50 run: after the headline and the edge block (untimed for "
+                         "them), also time YOLOv8n + decode + NMS at its bench config "
+                         "(engine.BENCH_BATCH / BENCH_STREAMS) -> extra.yolov8n (0 = skip)")
     ap.add_argument("--perturb-rank", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--hang-rank", type=int, default=-1, help=argparse.SUPPRESS)
     raw = list(sys.argv[1:] if argv is None else argv)
@@ -191,6 +195,14 @@ def main(argv=None):
         edge = edge_latency(model, hw, [int(b) for b in a.edge.split(",") if b.strip()],
                             device=di.device, seed=a.seed + di.rank)
 
+    yolo = None
+    if on_gpu and a.model == "resnet50" and a.yolo:
+        # BASELINE.json config 4 under the same clock discipline as the headline: fresh
+        # engine at its own bench config, W untimed warmup steps, K timed steps bracketed
+        # by barrier + synchronize, slowest rank's time (the ResNet-50 engine stays
+        # allocated: a few GB of 288)
+        yolo = _time_yolo(a, di, sync)
+
     world = parallel.info().world_size
     imgs = world * a.batch * a.steps
     value = imgs / max_elapsed
@@ -234,6 +246,8 @@ def main(argv=None):
     }
     if edge is not None:
         res["extra"]["edge"] = edge
+    if yolo is not None:
+        res["extra"]["yolov8n"] = yolo
     if lat_hist is not None:
         lat_hist.allreduce()  # fleet-wide step-latency distribution (one SUM all-reduce)
         res["extra"]["step_latency_ms"] = {k: round(v, 4) for k, v in lat_hist.summary().items()}
@@ -258,6 +272,46 @@ def main(argv=None):
               f"(digests {rc.digests})", file=sys.stderr)
         return 3
     return 0
+
+
+def _time_yolo(a, di, sync):
+    """YOLOv8n (incl. decode + NMS) images/sec at engine.BENCH_BATCH["yolov8n"] per GPU with
+    engine.BENCH_STREAMS["yolov8n"] slices: same W/K and timing rules as the headline."""
+    import torch
+    from kvedge_amd import parallel
+    from kvedge_amd.engine import BENCH_BATCH, BENCH_STREAMS, InferenceEngine
+    from kvedge_amd.models.yolov8 import KvYoloV8n
+
+    torch.cuda.empty_cache()
+    batch, streams = BENCH_BATCH["yolov8n"], BENCH_STREAMS["yolov8n"]
+    t_build = time.perf_counter()
+    model = KvYoloV8n.build(seed=a.seed, device=di.device, calibrate=True)
+    parallel.broadcast_tensors(parallel.model_tensors(model), src=0)
+    eng = InferenceEngine(model, batch, KvYoloV8n.image_size, device=di.device,
+                          seed=a.seed + di.rank, use_graph=True, streams=streams)
+    eng.prepare(warmup=2, autotune=True)
+    build_s = time.perf_counter() - t_build
+    for _ in range(a.warmup):
+        eng.run()
+    sync()
+    parallel.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        eng.run()
+    sync()
+    elapsed = time.perf_counter() - t0
+    parallel.barrier()
+    sync()
+    (mx,) = parallel.allreduce_scalars([elapsed], op="max")
+    world = parallel.info().world_size
+    out = {"metric": METRICS["yolov8n"], "value": round(world * batch * a.steps / mx, 2),
+           "ms_per_step": round(mx / a.steps * 1e3, 4), "per_gpu_batch": batch,
+           "streams": eng.n_streams, "steps": a.steps, "warmup": a.warmup,
+           "image_size": KvYoloV8n.image_size, "build_s": round(build_s, 2)}
+    del eng, model
+    torch.cuda.empty_cache()
+    return out
 
 
 if __name__ == "__main__":

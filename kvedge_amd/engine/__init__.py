@@ -120,10 +120,15 @@ class InferenceEngine:
         self.outputs = _cat_outputs(parts)
         return self.outputs
 
-    def prepare(self, warmup: int = 2, autotune: bool = True, verbose: bool = False):
+    def prepare(self, warmup: int = 2, autotune: bool = True, verbose: bool = False,
+                tune_cache: Optional[str] = None):
         """Autotune conv tiles for this batch, warm up (code objects load, allocator
-        pools fill), then capture the step into a hipGraph."""
+        pools fill), then capture the step into a hipGraph.  ``tune_cache``: JSON file of
+        earlier picks (autotune.autotune), so a restarted module skips the timing sweep.
+        ``self.prep_s`` keeps the phase times (tune / warmup / capture)."""
         self.tuning = {}
+        self.prep_s = {}
+        t0 = time.perf_counter()
         if autotune and self.device.type == "cuda":
             from .autotune import autotune as _tune
 
@@ -131,10 +136,16 @@ class InferenceEngine:
             # tiles are pinned per layer for the shape the model actually runs: one slice
             conc = self.n_streams if os.environ.get("KVEDGE_TUNE_CONCURRENT", "1") != "0" else 1
             self.tuning = _tune(self.model, self.frames[:self.batch // self.n_streams],
-                                verbose=verbose, concurrency=conc)
+                                verbose=verbose, concurrency=conc, cache_path=tune_cache)
+            torch.cuda.synchronize(self.device)
+        t1 = time.perf_counter()
+        self.prep_s["tune"] = t1 - t0
         if not self.use_graph:
             for _ in range(warmup):
                 self._step()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            self.prep_s["warmup"] = time.perf_counter() - t1
             return self
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -143,6 +154,8 @@ class InferenceEngine:
                 self._step()
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
+        t2 = time.perf_counter()
+        self.prep_s["warmup"] = t2 - t1
         self.graph = torch.cuda.CUDAGraph()
         # capture on the warm-up stream: per-stream state made during warm-up (the split-K
         # workspace, ops.splitk_workspace) is then reused, not re-allocated -- and zero-filled
@@ -150,6 +163,7 @@ class InferenceEngine:
         with torch.cuda.graph(self.graph, stream=s):
             self._step()
         torch.cuda.synchronize(self.device)
+        self.prep_s["capture"] = time.perf_counter() - t2
         return self
 
     def run(self):

@@ -135,14 +135,31 @@ def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
         return {}
     if refine_iters is None:
         refine_iters = int(os.environ.get("KVEDGE_AUTOTUNE_REFINE_ITERS", "20"))
+    ntiles = int(torch.ops.kvedge.conv_num_tiles())
+    sig = _cache_signature(ntiles, concurrency)
     cache = {}
     if cache_path and os.path.exists(cache_path):
-        with open(cache_path) as f:
-            cache = {k: tuple(v) for k, v in json.load(f).items()}
+        try:
+            with open(cache_path) as f:
+                doc = json.load(f)
+            # picks are valid only for the same kernel library, tile table, device and
+            # concurrency; anything else (an older build, the old flat format) is ignored
+            if isinstance(doc, dict) and doc.get("signature") == sig:
+                cache = {k: tuple(v) for k, v in doc.get("picks", {}).items()}
+        except (OSError, ValueError):
+            cache = {}
     with record_convs() as rec:
         model(example_input)
     torch.cuda.synchronize()
-    ntiles = int(torch.ops.kvedge.conv_num_tiles())
+    # all-or-nothing: the cache is used only if it covers every layer of this model on
+    # EVERY rank -- data-parallel ranks must time the same keys (one all-reduce below)
+    if cache and not all(repr(key) in cache for _, key, _ in rec):
+        cache = {}
+    from .. import parallel
+
+    if parallel.is_dist() and parallel.allreduce_scalars(
+            [1.0 if cache else 0.0], op="min")[0] < 1.0:
+        cache = {}
     # A/B knob: tune over the first KVEDGE_TILE_LIMIT tiles only (e.g. without a new family)
     lim = int(os.environ.get("KVEDGE_TILE_LIMIT", "0"))
     if 0 < lim < ntiles:
@@ -202,9 +219,28 @@ def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
         layer.tile = (results.get(ks) or cache[ks])[0]
         if ks not in results:
             results[ks] = cache[ks]
-    if cache_path:
-        os.makedirs(os.path.dirname(cache_path) or ".", exist_ok=True)
-        cache.update(results)
-        with open(cache_path, "w") as f:
-            json.dump(cache, f, indent=0)
+    if cache_path and todo and parallel.info().local_rank == 0:  # one writer per VM disk
+        try:
+            os.makedirs(os.path.dirname(cache_path) or ".", exist_ok=True)
+            cache.update(results)
+            tmp = cache_path + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump({"signature": sig, "picks": cache}, f, indent=0)
+            os.replace(tmp, cache_path)
+        except OSError:
+            pass  # read-only disk: tuning still applied, just not remembered
     return results
+
+
+def _cache_signature(ntiles: int, concurrency: int) -> str:
+    """Identity of what a cached pick depends on: the kernel library build (size and
+    mtime of the loaded .so), its tile table, the device, the timing concurrency."""
+    from .. import ops
+
+    try:
+        st = os.stat(ops._LIB_PATH)
+        lib = f"{st.st_size}:{int(st.st_mtime)}"
+    except OSError:
+        lib = "?"
+    dev = torch.cuda.get_device_name() if torch.cuda.is_available() else "cpu"
+    return f"lib={lib};tiles={ntiles};conc={concurrency};dev={dev}"

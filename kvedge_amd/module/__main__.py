@@ -10,11 +10,26 @@ import argparse
 import os
 import signal
 import sys
+import time
 
 from .. import parallel
 from .app import ModuleApp
 from .config import ModuleConfig
 from .transport import make_transport
+
+_T_IMPORTED = time.time()  # torch, the op library bindings and the module are imported
+
+
+def _process_start_epoch():
+    """Epoch at which the kernel started this process (/proc: boot time + start ticks)."""
+    try:
+        with open("/proc/self/stat") as f:
+            start_ticks = int(f.read().rsplit(")", 1)[1].split()[19])
+        with open("/proc/stat") as f:
+            btime = next(int(ln.split()[1]) for ln in f if ln.startswith("btime"))
+        return btime + start_ticks / os.sysconf("SC_CLK_TCK")
+    except (OSError, ValueError, StopIteration, IndexError):
+        return None
 
 
 def _topology_from_env() -> int:
@@ -73,6 +88,9 @@ def main(argv=None):
                     help="heartbeat file rewritten at every report (VMI health probes)")
     ap.add_argument("--stamps", default=os.environ.get("KVEDGE_STAMPS", "/var/lib/kvedge/boot-timing"),
                     help="guest boot-timing stamp file (module_first_inference is appended)")
+    ap.add_argument("--tune-cache", default=os.environ.get("KVEDGE_TUNE_CACHE",
+                                                           "/var/lib/kvedge/tune-cache.json"),
+                    help="autotuner picks on the persistent disk ('' = always re-tune)")
     a = ap.parse_args(argv)
     di = parallel.init_from_env(prefer_gpu=True)
     cfg = ModuleConfig(model=a.model, batch=a.batch, dtype=a.dtype, seed=a.seed,
@@ -83,7 +101,11 @@ def main(argv=None):
     # one IoT Edge identity per VM: only local rank 0 talks to edgeHub
     kind = a.transport if di.local_rank == 0 or a.transport != "azure" else "null"
     app = ModuleApp(make_transport(kind), cfg, state_path=a.state,
-                    stamp_path=a.stamps or None, heartbeat_path=a.heartbeat or None)
+                    stamp_path=a.stamps or None, heartbeat_path=a.heartbeat or None,
+                    tune_cache=a.tune_cache or None)
+    # cold-start legs: this process's start (kernel start time) and the end of imports
+    app._stamp("module_process_start", _process_start_epoch())
+    app._stamp("module_imported", _T_IMPORTED)
     # SIGTERM (edgeAgent stop, VM shutdown) only votes to stop: the replicas leave the
     # loop together at the next control boundary, so the final report's collectives match
     signal.signal(signal.SIGTERM, lambda *_: app.request_stop())

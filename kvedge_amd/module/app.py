@@ -142,7 +142,8 @@ class ModuleApp:
     def __init__(self, transport: Transport, config: Optional[ModuleConfig] = None,
                  device: Optional[str] = None, state_path: Optional[str] = None,
                  clock=time.perf_counter, stamp_path: Optional[str] = None,
-                 heartbeat_path: Optional[str] = None, boot_id_path: str = BOOT_ID_PATH):
+                 heartbeat_path: Optional[str] = None, boot_id_path: str = BOOT_ID_PATH,
+                 tune_cache: Optional[str] = None):
         self.tr = transport
         self.cfg = (config or ModuleConfig()).validate()
         self.device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
@@ -157,6 +158,10 @@ class ModuleApp:
         # `kvedge-health` accepts only evidence written during the current boot
         self.boot_id = _read_boot_id(boot_id_path)
         self._last_hb = None  # clock() of the last heartbeat write
+        # autotuner picks kept on the persistent disk: a restarted module (same library,
+        # device, batch) skips the tile sweep (engine.prepare(tune_cache=...))
+        self.tune_cache = tune_cache
+        self.build_phases: Dict[str, float] = {}  # wall-clock epochs of the first build
         self.clock = clock
         self.engine = None
         self.model = None
@@ -316,13 +321,14 @@ class ModuleApp:
             json.dump(dict(self.state, config=self.cfg.to_dict(), ts=now_iso()), f)
         os.replace(tmp, self.state_path)  # atomic on the persistent disk
 
-    def _stamp(self, name: str):
+    def _stamp(self, name: str, t: Optional[float] = None):
         if not self.stamp_path:
             return
         try:
             os.makedirs(os.path.dirname(self.stamp_path) or ".", exist_ok=True)
+            t = time.time() if t is None else t
             with open(self.stamp_path, "a") as f:
-                f.write(f"{name} {time.time():.6f} {self.boot_id}\n".rstrip() + "\n")
+                f.write(f"{name} {t:.6f} {self.boot_id}\n".rstrip() + "\n")
         except OSError:
             pass  # read-only / missing mount: timing is best-effort, never fatal
 
@@ -377,11 +383,27 @@ class ModuleApp:
             self.model = KvYoloV8n(init_yolov8n(cfg.seed, calibrate=dev.type == "cuda"), dev,
                                    conf=cfg.conf, iou=cfg.iou, max_det=cfg.max_det)
         camera = cfg.source == "camera"
+        t_model = time.time()
         self.engine = InferenceEngine(self.model, cfg.batch, cfg.resolved_image_size(), device=dev,
                                       seed=cfg.seed + self.rank, use_graph=cfg.use_graph,
                                       synthetic=not camera,
                                       streams=edge_streams(cfg.batch) if dev.type == "cuda" else 1)
-        self.engine.prepare(warmup=1, autotune=dev.type == "cuda")
+        self.engine.prepare(warmup=1, autotune=dev.type == "cuda",
+                            tune_cache=self.tune_cache if dev.type == "cuda" else None)
+        if not self.build_phases:
+            # cold-start legs (tools/module_cold_start.py): model built -> tiles tuned
+            # (or read from the cache) -> warmed -> graph captured
+            p = self.engine.prep_s
+            t = t_model
+            self.build_phases["module_model_built"] = t
+            for leg, name in (("tune", "module_tuned"), ("warmup", "module_warm"),
+                              ("capture", "module_graph_captured")):
+                t += p.get(leg, 0.0)
+                self.build_phases[name] = t
+            for name, t in self.build_phases.items():
+                self._stamp(name, t)
+            log_event(self.log, "engine_built", tuned_layers=len(self.engine.tuning or {}),
+                      **{f"{k}_s": round(v, 3) for k, v in p.items()})
         if camera:
             from ..runtime import FrameRing
 
