@@ -238,6 +238,8 @@ def main(argv=None):
         "extra": {
             "tflops_per_gpu": round(value / world * flops / 1e12, 2) if flops else None,
             "build_s": round(build_s, 2),
+            "prepare_s": {k: round(v, 2) for k, v in (getattr(eng, "prep_s", None) or {}).items()},
+            "graph_refine": getattr(eng, "refine", None),
             "replica_check": {"ok": rc.ok, "max_rel_dev": rc.max_rel_dev,
                               "digests": rc.digests},
             "backend": di.backend,
@@ -308,7 +310,8 @@ def _time_yolo(a, di, sync):
     out = {"metric": METRICS["yolov8n"], "value": round(world * batch * a.steps / mx, 2),
            "ms_per_step": round(mx / a.steps * 1e3, 4), "per_gpu_batch": batch,
            "streams": eng.n_streams, "steps": a.steps, "warmup": a.warmup,
-           "image_size": KvYoloV8n.image_size, "build_s": round(build_s, 2)}
+           "image_size": KvYoloV8n.image_size, "build_s": round(build_s, 2),
+           "graph_refine": eng.refine}
     del eng, model
     torch.cuda.empty_cache()
     return out

@@ -147,7 +147,7 @@ class InferenceEngine:
                 torch.cuda.synchronize(self.device)
             self.prep_s["warmup"] = time.perf_counter() - t1
             return self
-        s = torch.cuda.Stream(device=self.device)
+        self._cap_stream = s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(max(1, warmup)):
@@ -156,15 +156,42 @@ class InferenceEngine:
         torch.cuda.synchronize(self.device)
         t2 = time.perf_counter()
         self.prep_s["warmup"] = t2 - t1
-        self.graph = torch.cuda.CUDAGraph()
+        self.graph, self.outputs = self.capture(warm=False)
+        self.prep_s["capture"] = time.perf_counter() - t2
+        self.refine = None
+        if (autotune and self.tuning and
+                os.environ.get("KVEDGE_GRAPH_REFINE", "1") != "0"):
+            # in-graph pick of the tiles (autotune.graph_refine): per-layer timing alone
+            # does not see the neighbouring layers and the other slice's kernels
+            from .autotune import graph_refine
+
+            t3 = time.perf_counter()
+            self.refine = graph_refine(
+                self, budget_s=float(os.environ.get("KVEDGE_GRAPH_REFINE_S", "30")),
+                verbose=verbose)
+            self.prep_s["graph_refine"] = time.perf_counter() - t3
+        return self
+
+    def capture(self, warm: bool = True):
+        """Capture one step (with the layers' current tiles) into a new hipGraph; returns
+        (graph, its output tensors).  ``self.graph`` is not touched.  ``warm``: one eager step first on the capture
+        stream (validates the tiles, creates per-stream state such as the split-K
+        workspace outside the capture)."""
+        s = self._cap_stream
+        if warm:
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                self._step()
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
         # capture on the warm-up stream: per-stream state made during warm-up (the split-K
         # workspace, ops.splitk_workspace) is then reused, not re-allocated -- and zero-filled
         # by a kernel recorded into the graph, i.e. on every replay -- for a new stream
-        with torch.cuda.graph(self.graph, stream=s):
+        with torch.cuda.graph(g, stream=s):
             self._step()
         torch.cuda.synchronize(self.device)
-        self.prep_s["capture"] = time.perf_counter() - t2
-        return self
+        return g, self.outputs  # the outputs live in this graph's private pool
 
     def run(self):
         """Launch one step (async on GPU)."""

@@ -214,9 +214,18 @@ def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
         results[ks] = (best, round(ts[best], 2) if best >= 0 else None)
         if verbose:
             print(f"autotune {key} -> tile {best} {results[ks][1]} us", flush=True)
+    # runner-up tiles per key (by the same timing), for the in-graph refine pass
+    # (graph_refine below): every tile within ``ALT_TOL`` of the best, best first
+    alts = {}
+    for (ks, _), ts in zip(todo.items(), fleet):
+        fin = sorted((ts[t], t) for t in range(ntiles) if ts[t] != float("inf"))
+        if fin:
+            alts[ks] = [t for us, t in fin if us <= fin[0][0] * (1.0 + ALT_TOL)][:1 + ALT_MAX]
     for layer, key, fn in rec:
         ks = repr(key)
         layer.tile = (results.get(ks) or cache[ks])[0]
+        layer.tile_alts = alts.get(ks, [layer.tile])
+        layer.tile_us = (results.get(ks) or cache[ks])[1] or 0.0
         if ks not in results:
             results[ks] = cache[ks]
     if cache_path and todo and parallel.info().local_rank == 0:  # one writer per VM disk
@@ -230,6 +239,124 @@ def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
         except OSError:
             pass  # read-only disk: tuning still applied, just not remembered
     return results
+
+
+ALT_TOL = 0.25  # runner-ups within 25 % of a layer's best (isolated timing) are graph-tested
+ALT_MAX = 2     # ... at most two per layer
+
+
+def graph_refine(engine, budget_s: float = 30.0, min_gain: float = 0.003,
+                 verbose: bool = False) -> Dict:
+    """In-graph tile refinement: the per-layer timing above measures a
+    layer alone (or as concurrent copies of itself), but in the bench graph each kernel
+    runs next to the previous and next layer of its own slice and whatever the other
+    slice runs at that moment.  A tile that wins alone can lose there, and the reverse.
+
+    For every layer with runner-up tiles (``layer.tile_alts``), largest layers first, the
+    step graph is re-captured with the runner-up and timed against the current graph,
+    replays interleaved A B B A ... on the same stream (drift hits both alike).  A change
+    is kept only if the WHOLE STEP gets faster by more than ``min_gain`` in two separate
+    measurements.  Layers with the same shape key keep separate picks.  Stops at
+    ``budget_s``.  Returns {"trials", "kept", "step_ms_before", "step_ms_after"}."""
+    import time as _time
+
+    layers = []
+    with record_convs() as rec:
+        engine.model(engine.frames[:engine.batch // engine.n_streams])
+    torch.cuda.synchronize()
+    seen = set()
+    for layer, key, fn in rec:
+        if id(layer) in seen or len(getattr(layer, "tile_alts", ())) < 2:
+            continue
+        seen.add(id(layer))
+        layers.append(layer)
+    layers.sort(key=lambda l: -(getattr(l, "tile_us", 0.0) or 0.0))  # largest first
+    if not layers or engine.graph is None:
+        return {"trials": 0, "kept": 0}
+    t_end = _time.perf_counter() + budget_s
+    cur, cur_out = engine.graph, engine.outputs
+    base = _replay_ms(cur, 3)
+    rounds = max(4, min(40, int(200.0 / max(base, 1e-3))))
+    before = _ab(cur, cur, rounds)[0]
+    trials = kept = 0
+    from .. import parallel
+
+    dist = parallel.is_dist()
+
+    def fleet(gain, over):
+        """Data-parallel ranks decide together (mean gain, any rank over budget): every
+        replica must pin the same tiles (C4 compares their outputs)."""
+        if not dist:
+            return gain, over
+        g, o = parallel.allreduce_scalars([gain, 1.0 if over else 0.0], op="sum")
+        return g / parallel.info().world_size, o > 0
+
+    for layer in layers:
+        for t in layer.tile_alts:
+            if t == layer.tile:
+                continue
+            if fleet(0.0, _time.perf_counter() > t_end)[1]:
+                break
+            old = layer.tile
+            layer.tile = t
+            g = None
+            try:
+                g, g_out = engine.capture()
+                ok = 1.0
+            except RuntimeError:  # tile not valid in this context
+                ok = 0.0
+            if fleet(ok, False)[0] < 1.0:  # invalid on some rank: skip everywhere
+                layer.tile = old
+                g = g_out = None
+                continue
+            trials += 1
+            a, b = _ab(cur, g, rounds)
+            gain = fleet((a - b) / a, False)[0]
+            if gain > min_gain:
+                a2, b2 = _ab(cur, g, 2 * rounds)
+                gain = min(gain, fleet((a2 - b2) / a2, False)[0])
+            if gain > min_gain:
+                kept += 1
+                del cur, cur_out
+                cur, cur_out = g, g_out
+                if verbose:
+                    print(f"graph_refine: tile {old} -> {t}: step {a:.3f} -> {b:.3f} ms",
+                          flush=True)
+            else:
+                layer.tile = old
+                del g, g_out
+    engine.graph, engine.outputs = cur, cur_out  # a rejected capture last set outputs
+    after = _ab(cur, cur, rounds)[0]
+    return {"trials": trials, "kept": kept, "step_ms_before": round(before, 4),
+            "step_ms_after": round(after, 4)}
+
+
+def _replay_ms(g, n: int) -> float:
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    g.replay()
+    st.record()
+    for _ in range(n):
+        g.replay()
+    en.record()
+    torch.cuda.synchronize()
+    return st.elapsed_time(en) / n
+
+
+def _ab(ga, gb, rounds: int):
+    """Median ms per replay of graphs A and B, interleaved (A B, B A, A B ...)."""
+    ta, tb = [], []
+    _hold_gpu(2 * rounds)
+    for r in range(rounds):
+        order = ((ga, ta), (gb, tb)) if r % 2 == 0 else ((gb, tb), (ga, ta))
+        for g, acc in order:
+            st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            st.record()
+            g.replay()
+            en.record()
+            acc.append((st, en))
+    torch.cuda.synchronize()
+    med = lambda xs: sorted(s.elapsed_time(e) for s, e in xs)[len(xs) // 2]  # noqa: E731
+    return med(ta), med(tb)
 
 
 def _cache_signature(ntiles: int, concurrency: int) -> str:

@@ -178,8 +178,9 @@ def test_module_cli_topologies(tmp_path):
     assert [p.returncode for p in procs] == [0, 0], outs[1][1][-3000:]
     tel0, tel1 = _telemetry(outs[0][0]), _telemetry(outs[1][0])
     assert tel0 and tel0[-1]["world_size"] == 2 and not tel1
-    assert open(os.path.join(str(tmp_path), "stamps-b1")).read().startswith(
-        "module_first_inference ")
+    names = [ln.split()[0] for ln in
+             open(os.path.join(str(tmp_path), "stamps-b1")).read().splitlines()]
+    assert names[0] == "module_process_start" and names[-1] == "module_first_inference"
 
 
 def _sync_worker(rank, world, port, q):
