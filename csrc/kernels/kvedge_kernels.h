@@ -145,6 +145,27 @@ int kv_preprocess_s2d(const uint8_t* x, void* y, int N, int H, int W, const floa
 int kv_batchnorm_nhwc(const void* x, void* y, const float* scale, const float* shift,
                       int64_t rows, int C, int relu, hipStream_t s);
 
+// ---------------------------------------------------------------------------
+// v11 fused identity bottleneck (bneck_fused.hip): y = ReLU(W3 . ReLU(conv3x3(ReLU(W1 . x +
+// b1)) + b2) + b3 + x), NHWC bf16, x / y [N, H, W, 4C] contiguous, packed weights
+// w1 [C][4C], w2 [C][9C] (tap-major, cin minor), w3 [4C][C]; fp32 biases.
+// ---------------------------------------------------------------------------
+typedef struct KvBneckParams {
+  const void* x;
+  void* y;
+  const void* w1;
+  const float* b1;
+  const void* w2;
+  const float* b2;
+  const void* w3;
+  const float* b3;
+  int N, H, W, C;
+  int x_bytes;  // N * H * W * 4C * 2 (also y's)
+  int dbg;      // debug (tests/tools only): 1 / 2 = write z1 / z2 into y[..., :C] and stop
+} KvBneckParams;
+int kv_bneck_fused_supported(int C, int H, int W);
+int kv_bneck_fused(const KvBneckParams* p, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

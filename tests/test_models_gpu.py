@@ -270,3 +270,17 @@ def test_yolov8n_fused_stem_b1_parity(yolo):
         cg, cu = float(cs(g, c, dim=0)), float(cs(u, c, dim=0))
         assert cg > 0.998 and cg >= cu - 5e-4, (cg, cu)
         assert float(cs(g, u, dim=0)) > 0.999
+
+
+def test_resnet50_fused_bottleneck_path_matches_default(resnet, monkeypatch):
+    """The opt-in v11 path (KVEDGE_BNECK=1: stages 2-3 identity blocks as one launch each)
+    gives the default path's logits up to bf16 reordering noise."""
+    _, kv, _ = resnet
+    fr = _frames(6, 9).cuda()
+    with torch.no_grad():
+        base = kv.logits(fr, frames_in=True).float()
+        monkeypatch.setattr(ops, "BNECK_ENABLED", True)
+        fused = kv.logits(fr, frames_in=True).float()
+    torch.cuda.synchronize()
+    cos = torch.nn.functional.cosine_similarity(base.flatten(), fused.flatten(), dim=0)
+    assert cos > 0.999, float(cos)

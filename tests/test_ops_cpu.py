@@ -127,3 +127,20 @@ def test_s2d_stem_equals_strided_conv():
         ref = F.conv2d(x4, conv.weight.detach().to(torch.bfloat16).float(), None, 2, p)
         assert y.shape == ref.permute(0, 2, 3, 1).shape
         assert (y - ref.permute(0, 2, 3, 1)).abs().max() < 0.05 * ref.abs().max() + 0.05
+
+
+def test_mfma_frag_major_layout():
+    """ops.mfma_frag_major: fragment (cs, ks) lane l holds row 32 cs + l % 32, K elements
+    16 ks + 8 (l // 32) .. + 8 -- the A operand of v_mfma_f32_32x32x16_bf16 (bneck_fused.hip)."""
+    import torch
+    from kvedge_amd import ops
+
+    N, K = 96, 48
+    w = torch.arange(N * K, dtype=torch.float32).reshape(N, K)
+    f = ops.mfma_frag_major(w).reshape(N // 32, K // 16, 64, 8)
+    for cs in range(N // 32):
+        for ks in range(K // 16):
+            for lane in (0, 5, 31, 32, 47, 63):
+                r, h = lane % 32, lane // 32
+                want = w[32 * cs + r, 16 * ks + 8 * h:16 * ks + 8 * h + 8]
+                assert torch.equal(f[cs, ks, lane], want)
