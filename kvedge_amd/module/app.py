@@ -397,7 +397,8 @@ class ModuleApp:
             t = t_model
             self.build_phases["module_model_built"] = t
             for leg, name in (("tune", "module_tuned"), ("warmup", "module_warm"),
-                              ("capture", "module_graph_captured")):
+                              ("capture", "module_graph_captured"),
+                              ("graph_refine", "module_graph_refined")):
                 t += p.get(leg, 0.0)
                 self.build_phases[name] = t
             for name, t in self.build_phases.items():

@@ -210,7 +210,7 @@ def test_failed_rebuild_rolls_back_and_stamps(tmp_path):
     names = [ln.split()[0] for ln in stamps.read_text().splitlines()]
     # the first build's cold-start legs, then the first inference
     assert names == ["module_model_built", "module_tuned", "module_warm",
-                     "module_graph_captured", "module_first_inference"]
+                     "module_graph_captured", "module_graph_refined", "module_first_inference"]
     eng = app.engine
     tr.push_twin_patch({"batch": 4096})
     app.run(max_steps=1)

@@ -16,6 +16,8 @@ Each run writes the module's boot-timing stamps (the same file format as the gue
   tune     -> conv tiles pinned (timed sweep, or read from the cache)
   warmup   -> warm-up steps
   capture  -> hipGraph captured
+  graph_refine -> runner-up tiles A/B-timed in the captured step (engine.autotune.graph_refine;
+           nothing to try when the tiles came from the cache)
   first    -> first inference finished
 
   python tools/module_cold_start.py --model resnet50 --batch 64 --out gpurun_out/cold.json
@@ -34,7 +36,8 @@ LEGS = [("import", "module_process_start", "module_imported"),
         ("tune", "module_model_built", "module_tuned"),
         ("warmup", "module_tuned", "module_warm"),
         ("capture", "module_warm", "module_graph_captured"),
-        ("first", "module_graph_captured", "module_first_inference")]
+        ("graph_refine", "module_graph_captured", "module_graph_refined"),
+        ("first", "module_graph_refined", "module_first_inference")]
 
 
 def one_run(model, batch, steps, work, cache, tag):
