@@ -244,6 +244,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   };
   unsigned long long* K = keys;
   int nsel = cnt;
+  bool sorted = false;  // the top set already came out of its sort (bucket or fallback)
   if (cnt > kSel) {
     int* hist = reinterpret_cast<int*>(sel);
     for (int i = tid; i < kBins; i += blockDim.x) hist[i] = 0;
@@ -275,9 +276,83 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
       }
     }
     __syncthreads();
-    if (s_nsel <= kSelMax) {
+    // Bucket sort of the top set (the 2048-key bitonic network was 43 of
+    // the ~100 us a crowded image spends in NMS, profiles/r4_v5_nms_probe.txt).  The
+    // histogram already orders the keys by bin; each top-set bin gets a descending slot range
+    // (suffix sums of its counts), keys are scattered into their bin's range with one LDS
+    // atomic each, and only keys that share a bin are ranked against each other.  The bin
+    // cursors live in the free tail of keys[] (cnt <= kMaxCand - kBins / 2 -- the top set
+    // of a 640x640 image has at most 8400 candidates); a bin with more than kBinRankMax keys
+    // (a degenerate score pile-up) falls back to the bitonic network.
+    constexpr int kBinRankMax = 64;
+    int* cur = reinterpret_cast<int*>(keys + (kMaxCand - kBins / 2));
+    const bool bucket = s_nsel <= kSelMax && cnt <= kMaxCand - kBins / 2 && !(diag & 8);
+    if (bucket) {
+      const int T = s_T;
+      if (tid < 64) {  // wave 0: lane L owns bins [32 L, 32 L + 32); descending exclusive sums
+        int sum = 0, mx = 0;
+        for (int b = 0; b < 32; ++b) {
+          const int bb = tid * 32 + b;
+          const int c = bb >= T ? hist[bb] : 0;
+          sum += c;
+          mx = max(mx, c);
+        }
+        int suf = sum;  // inclusive suffix over lanes >= L
+        for (int off = 1; off < 64; off <<= 1) {
+          const int v = __shfl_down(suf, off);
+          if (tid + off < 64) suf += v;
+        }
+        int run = suf - sum;  // slots taken by the bins above this lane's
+        for (int b = 31; b >= 0; --b) {
+          const int bb = tid * 32 + b;
+          cur[bb] = run;  // start of bin bb (the scatter advances it to the bin's end)
+          run += bb >= T ? hist[bb] : 0;
+        }
+        for (int off = 32; off > 0; off >>= 1) mx = max(mx, __shfl_xor(mx, off));
+        if (tid == 0) s_n2 = mx;
+      }
+      __syncthreads();
+      const int binmax = s_n2;
+      __syncthreads();  // every thread has read s_n2 before the fallback below reuses it
+      if (binmax <= kBinRankMax) {
+        for (int i = tid; i < cnt; i += blockDim.x) {
+          const unsigned long long key = keys[i];
+          const int b = bin_of(key);
+          if (b >= T) sel[atomicAdd(&cur[b], 1)] = key;
+        }
+        __syncthreads();
+        // rank inside the bin: cur[b] is now the bin's end, its start the end of bin b + 1
+        const int ns = s_nsel;
+        unsigned long long mine[kSelMax / (64 * kNmsWaves)];
+        int dst[kSelMax / (64 * kNmsWaves)];
+#pragma unroll
+        for (int k = 0; k < kSelMax / (64 * kNmsWaves); ++k) {
+          const int i = tid + k * 64 * kNmsWaves;
+          dst[k] = -1;
+          if (i < ns) {
+            const unsigned long long key = sel[i];
+            const int b = bin_of(key);
+            const int lo0 = b + 1 < kBins ? cur[b + 1] : 0, hi0 = cur[b];
+            int r = 0;
+            for (int j = lo0; j < hi0; ++j) r += sel[j] > key;
+            mine[k] = key;
+            dst[k] = lo0 + r;
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kSelMax / (64 * kNmsWaves); ++k)
+          if (dst[k] >= 0) sel[dst[k]] = mine[k];
+        __syncthreads();
+        K = sel;
+        nsel = ns;
+      }
+    }
+    if (s_nsel <= kSelMax && K == keys) {
       const int T = s_T;
       const int ln = tid & 63;
+      if (tid == 0) s_n2 = 0;
+      __syncthreads();
       for (int i0 = 0; i0 < cnt; i0 += blockDim.x) {  // wave-aggregated, as the compaction
         const int i = i0 + tid;
         const unsigned long long key = i < cnt ? keys[i] : 0ull;
@@ -291,6 +366,8 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
       __syncthreads();
       K = sel;
       nsel = s_n2;
+      if (!(diag & 2)) bitonic(K, nsel);
+      sorted = true;
     }
   }
   if (diag & 4) t_ph[1] = __builtin_amdgcn_s_memrealtime();
@@ -299,7 +376,8 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   // one pass and one barrier instead of the bitonic network's log^2 barrier-separated stages
   // (28 at 128 keys, 42 us per image measured: profiles/r4_v5_nms_probe.txt).  Keys are unique
   // (the index is in the low word), so the ranks are a permutation.
-  if (!(diag & 2)) {
+  if (K == sel && cnt > kSel) sorted = true;  // the bucket sort above
+  if (!(diag & 2) && !sorted) {
     if (K == keys && nsel <= kRankSortMax) {  // (a top set in sel stays bitonic: the
       unsigned long long* dst = sel;           // full-sort fallback below needs keys intact)
       for (int i0 = 0; i0 < nsel; i0 += blockDim.x) {
@@ -475,7 +553,8 @@ extern "C" int kv_nms(const float* boxes, const float* scores, const int* cls, i
   if (N <= 0) return 0;
   // KVEDGE_NMS_DIAG (timing experiments only; outputs wrong): bit 0 skips the greedy
   // suppression, bit 1 the top-set sort; bit 2 writes per-phase durations into each image's
-  // first output row
+  // first output row; bit 3 (outputs right) sorts the top set with the bitonic network
+  // instead of the bucket sort (A/B)
   const char* dg = getenv("KVEDGE_NMS_DIAG");
   hipLaunchKernelGGL(nms_kernel, dim3(N), dim3(64 * kNmsWaves), 0, s, boxes, scores, cls, A, conf_thres,
                      iou_thres, max_det, out, count, dg ? atoi(dg) : 0);

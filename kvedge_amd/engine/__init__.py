@@ -95,8 +95,12 @@ class InferenceEngine:
         if streams < 1 or batch % streams:
             raise ValueError(f"batch {batch} does not split into {streams} equal slices")
         self.n_streams = streams if self.device.type == "cuda" else 1
-        self._side = [torch.cuda.Stream(device=self.device)
-                      for _ in range(self.n_streams)] if self.n_streams > 1 else []
+        # KVEDGE_STREAM_PRIO=1: the first slice's stream at high priority, the others normal
+        # (the dispatcher then feeds slice 0's workgroups first and the others fill the CUs
+        # its kernels leave idle) -- an A/B knob, off by default
+        prio = os.environ.get("KVEDGE_STREAM_PRIO", "0") == "1"
+        self._side = [torch.cuda.Stream(device=self.device, priority=-1 if (prio and i == 0) else 0)
+                      for i in range(self.n_streams)] if self.n_streams > 1 else []
 
     # one full edge-module step: synthesize frames, run the model
     def _step(self):

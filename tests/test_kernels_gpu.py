@@ -426,12 +426,14 @@ def test_nms_dense_overlaps():
     assert (o.cpu() - o_ref).abs().max() < 1e-4
 
 
-@pytest.mark.parametrize("case", ["spread", "clustered", "ties"])
+@pytest.mark.parametrize("case", ["spread", "clustered", "ties", "piles"])
 def test_nms_top_set(case):
     """YOLO-sized candidate lists (8400 anchors, most above conf) through the NMS top-set
-    path: 'spread' reaches max_det inside the sorted top set; 'clustered' (one class, boxes
-    piled on few centres) exhausts the top set first and falls back to the full sort;
-    'ties' (scores on 8 levels) puts > 2048 keys in one histogram bin (full-sort path)."""
+    path: 'spread' reaches max_det inside the bucket-sorted top set; 'clustered' (one class,
+    boxes piled on few centres) exhausts the top set first and falls back to the full sort;
+    'ties' (scores on 8 levels) puts > 2048 keys in one histogram bin (full-sort path);
+    'piles' (scores on 96 levels) keeps the top set under 2048 keys but puts > 64 in a bin
+    (the bucket sort's bitonic fallback)."""
     g = torch.Generator().manual_seed(5)
     A, N = 8400, 3
     if case == "clustered":
@@ -446,6 +448,8 @@ def test_nms_top_set(case):
     scores = torch.rand(N, A, generator=g) * 0.7 + 0.3
     if case == "ties":
         scores = (scores * 8).floor() / 8 + 0.05
+    if case == "piles":
+        scores = (scores * 96).floor() / 96 + 0.002
     o_ref, n_ref = ops.nms(boxes, scores, cls, conf=0.25, iou=0.7, max_det=300)
     o, n = ops.nms(boxes.cuda(), scores.cuda(), cls.cuda(), conf=0.25, iou=0.7, max_det=300)
     assert torch.equal(n.cpu(), n_ref), (n, n_ref)
