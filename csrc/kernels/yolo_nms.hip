@@ -286,7 +286,10 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
     // (a degenerate score pile-up) falls back to the bitonic network.
     constexpr int kBinRankMax = 64;
     int* cur = reinterpret_cast<int*>(keys + (kMaxCand - kBins / 2));
-    const bool bucket = s_nsel <= kSelMax && cnt <= kMaxCand - kBins / 2 && !(diag & 8);
+    // measured level-to-slower than the bitonic network on the bench's decode output (101.3
+    // vs 96.7 us per b256 slice, profiles/r5_v5_nms_probe_bucket.txt: the kernel is set by
+    // its slowest image, whose compaction and suppression dominate), so opt-in (diag bit 3)
+    const bool bucket = s_nsel <= kSelMax && cnt <= kMaxCand - kBins / 2 && (diag & 8);
     if (bucket) {
       const int T = s_T;
       if (tid < 64) {  // wave 0: lane L owns bins [32 L, 32 L + 32); descending exclusive sums
@@ -553,8 +556,8 @@ extern "C" int kv_nms(const float* boxes, const float* scores, const int* cls, i
   if (N <= 0) return 0;
   // KVEDGE_NMS_DIAG (timing experiments only; outputs wrong): bit 0 skips the greedy
   // suppression, bit 1 the top-set sort; bit 2 writes per-phase durations into each image's
-  // first output row; bit 3 (outputs right) sorts the top set with the bitonic network
-  // instead of the bucket sort (A/B)
+  // first output row; bit 3 (outputs right) sorts the top set with the histogram bucket sort
+  // instead of the bitonic network (A/B)
   const char* dg = getenv("KVEDGE_NMS_DIAG");
   hipLaunchKernelGGL(nms_kernel, dim3(N), dim3(64 * kNmsWaves), 0, s, boxes, scores, cls, A, conf_thres,
                      iou_thres, max_det, out, count, dg ? atoi(dg) : 0);

@@ -426,14 +426,18 @@ def test_nms_dense_overlaps():
     assert (o.cpu() - o_ref).abs().max() < 1e-4
 
 
+@pytest.mark.parametrize("bucket", [False, True])
 @pytest.mark.parametrize("case", ["spread", "clustered", "ties", "piles"])
-def test_nms_top_set(case):
+def test_nms_top_set(case, bucket, monkeypatch):
     """YOLO-sized candidate lists (8400 anchors, most above conf) through the NMS top-set
     path: 'spread' reaches max_det inside the bucket-sorted top set; 'clustered' (one class,
     boxes piled on few centres) exhausts the top set first and falls back to the full sort;
     'ties' (scores on 8 levels) puts > 2048 keys in one histogram bin (full-sort path);
     'piles' (scores on 96 levels) keeps the top set under 2048 keys but puts > 64 in a bin
-    (the bucket sort's bitonic fallback)."""
+    (the bucket sort's bitonic fallback).  bucket: the opt-in histogram bucket sort of the
+    top set (KVEDGE_NMS_DIAG bit 3) instead of the default bitonic network."""
+    if bucket:
+        monkeypatch.setenv("KVEDGE_NMS_DIAG", "8")
     g = torch.Generator().manual_seed(5)
     A, N = 8400, 3
     if case == "clustered":

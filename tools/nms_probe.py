@@ -42,7 +42,7 @@ def main():
           "suppression %.1f" % tuple(float(ph[:, i].max()) for i in range(3)))
     nc = (scores > m.conf).sum(1)
     print(f"candidates per image: max {int(nc.max())}, images over 1024: {int((nc > 1024).sum())}")
-    for d in ("0", "8", "1", "2", "3"):  # 8: the bitonic top-set sort instead of the bucket sort
+    for d in ("0", "8", "1", "2", "3"):  # 8: the bucket top-set sort instead of the bitonic
         os.environ["KVEDGE_NMS_DIAG"] = d
         ts = []
         for _ in range(a.iters):
