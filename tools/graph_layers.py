@@ -8,8 +8,8 @@ kernel of the replays to (slice, layer):
 
 - the layer list comes from one instrumented eager forward of the slice shape
   (``tools/op_roofline.costs_only``): one row per op call, in call order, with its
-  compulsory HBM bytes, FLOPs and pinned tile; every op of the bench config is ONE kernel,
-  which the summary checks (kernels per slice == op rows);
+  compulsory HBM bytes, FLOPs and pinned tile; an op is one kernel, or two for a split-K
+  tile (GEMM + finalize, summed into the op's row), which the summary checks;
 - kernels are matched to slices by the stream-order constraint: a slice's next kernel is
   the next op of its list and cannot start before that slice's previous kernel ended.
 
@@ -55,9 +55,11 @@ def run(a):
     with torch.no_grad():
         rows = costs_only(model, eng.frames[:per], ops)
     torch.cuda.synchronize()
+    # kernels per op: a split-K tile is its GEMM and its finalize launch
+    nk = [2 if (t is not None and ops.is_splitk(t)) else 1 for _, _, _, t in rows]
     with open(a.labels, "w") as f:
         json.dump({"model": a.model, "batch": batch, "streams": streams,
-                   "rows": [[n, b, fl, t] for n, b, fl, t in rows]}, f)
+                   "rows": [[n, b, fl, t] for n, b, fl, t in rows], "kernels": nk}, f)
     for _ in range(3):
         eng.run()
     torch.cuda.synchronize()
@@ -76,18 +78,20 @@ def _short(name):
     return name.split("(")[0]
 
 
-def assign(kernels, n_ops, n_slices):
-    """kernels: [(start, end, name)] of one step sorted by start -> [(slice, op)] or None.
-    Greedy with the stream-order constraint; ties go to the slice that is further behind."""
+def assign(kernels, op_of, n_slices):
+    """kernels: [(start, end, name)] of one step sorted by start; op_of: the op index of each
+    kernel position of a slice's sequence -> [(slice, op)] or None.  Greedy with the
+    stream-order constraint; ties go to the slice that is further behind."""
+    n_pos = len(op_of)
     ptr = [0] * n_slices
     last_end = [-1] * n_slices
-    sig = [None] * n_ops  # kernel name per op, learned from the first slice to reach it
+    sig = [None] * n_pos  # kernel name per position, learned from the first slice there
     out = []
     for st, en, nm in kernels:
         cands = []
         for s in range(n_slices):
             p = ptr[s]
-            if p >= n_ops:
+            if p >= n_pos:
                 continue
             if sig[p] is not None and sig[p] != nm:
                 continue
@@ -97,16 +101,18 @@ def assign(kernels, n_ops, n_slices):
             return None
         _, p, s = min(cands)
         sig[p] = sig[p] or nm
-        out.append((s, p))
+        out.append((s, op_of[p]))
         ptr[s] += 1
         last_end[s] = en
-    return out if all(p == n_ops for p in ptr) else None
+    return out if all(p == n_pos for p in ptr) else None
 
 
 def summarize(path, labels, reps, hbm, peak, out=sys.stdout):
     lab = json.load(open(labels))
     rows, n_sl = lab["rows"], lab["streams"]
     n_ops = len(rows)
+    nk = lab.get("kernels") or [1] * n_ops
+    op_of = [p for p in range(n_ops) for _ in range(nk[p])]
     recs = list(csv.DictReader(open(path)))
     recs.sort(key=lambda r: int(r["Start_Timestamp"]))
     idx = max(i for i, r in enumerate(recs) if "synth_kernel" in r["Kernel_Name"]
@@ -129,19 +135,30 @@ def summarize(path, labels, reps, hbm, peak, out=sys.stdout):
         walls.append((t1 - t0) / 1e3)
         ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), _short(r["Kernel_Name"]))
               for r in step]
-        model_ks = [x for x in ks if not (x[2].startswith("at::") or "synth_dev" in x[2]
-                                          or "bump_kernel" in x[2])]
+        model_ks = [x for x in ks if not (x[2].startswith(("at::", "__amd_rocclr")) or
+                                          "synth_dev" in x[2] or "bump_kernel" in x[2])]
         other = [x for x in ks if x not in model_ks]
-        if len(model_ks) != n_ops * n_sl:
-            raise SystemExit(f"step {k}: {len(model_ks)} model kernels, expected "
-                             f"{n_ops} ops x {n_sl} slices (an op launched != 1 kernel)")
-        asg = assign(model_ks, n_ops, n_sl)
+        if len(model_ks) != len(op_of) * n_sl:
+            if k == 0 and len(model_ks) % n_sl == 0:
+                # an op launched an unexpected number of kernels: fall back to one row per
+                # kernel position of the slice sequence (labels are then kernel names)
+                import collections as _c
+                print(f"# note: {len(model_ks)} kernels per step for {len(op_of)} op kernels x "
+                      f"{n_sl} slices; rows are kernel positions, not ops: "
+                      f"{dict(_c.Counter(x[2][:40] for x in model_ks))}", file=sys.stderr)
+                n_ops = len(model_ks) // n_sl
+                op_of = list(range(n_ops))
+                rows = [[f"kernel #{i}", 0, 0.0, None] for i in range(n_ops)]
+            else:
+                raise SystemExit(f"step {k}: {len(model_ks)} model kernels, expected "
+                                 f"{len(op_of)} (of {n_ops} ops) x {n_sl} slices")
+        asg = assign(model_ks, op_of, n_sl)
         if asg is None:
             raise SystemExit(f"step {k}: kernels do not match the op order of any slice")
         lab_of = {}
         for (st, en, nm), (s, p) in zip(model_ks, asg):
             dur[p].append((en - st) / 1e3)
-            names[p] = nm
+            names[p] = names.get(p) or nm  # an op's first kernel names it
             lab_of[(st, en, nm)] = p
         # wall share: sweep the union of intervals, split each segment over active kernels
         ev = []
@@ -185,7 +202,7 @@ def summarize(path, labels, reps, hbm, peak, out=sys.stdout):
     tot_share = 0.0
     for p in range(n_ops):
         nm, byts, flops, tile = rows[p]
-        d = sum(dur[p]) / len(dur[p])
+        d = sum(dur[p]) / (nst * n_sl)  # an op's kernels summed, per slice and step
         fl = max(byts / (hbm * 1e12), flops / (peak * 1e15)) * 1e6
         sh = share[p] / nst
         tot_share += sh

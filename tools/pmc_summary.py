@@ -58,8 +58,13 @@ def main(root="gpurun_out/pmc", top=40, pattern="p*/p*_counter_collection.csv"):
              "lds/w": cs.get("SQ_INSTS_LDS", 0) / waves,
              "wait%": 100 * cs.get("SQ_WAIT_ANY", 0) / max(cs.get("SQ_WAVE_CYCLES", 1), 1),
              "winst%": 100 * cs.get("SQ_WAIT_INST_ANY", 0) / max(cs.get("SQ_WAVE_CYCLES", 1), 1),
-             "mfma_busy%": 100 * cs.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) /
-                           max(cs.get("GRBM_GUI_ACTIVE", 1) / 8 * 256 * 4, 1),
+             # busy cycles over SIMD-cycles (GUI_ACTIVE is summed over the 8 XCDs; 256 CUs x
+             # 4 SIMDs); "n/a" when the pass did not collect both counters (round-4 tables
+             # printed 0.0 there, which read as "MFMA idle")
+             "mfma_busy%": (100 * cs["SQ_VALU_MFMA_BUSY_CYCLES"] /
+                            max(cs["GRBM_GUI_ACTIVE"] / 8 * 256 * 4, 1))
+                           if "SQ_VALU_MFMA_BUSY_CYCLES" in cs and "GRBM_GUI_ACTIVE" in cs
+                           else "n/a",
              "l2hit%": 100 * cs.get("TCC_HIT_sum", 0) /
                        max(cs.get("TCC_HIT_sum", 0) + cs.get("TCC_MISS_sum", 0), 1),
              "bankc": cs.get("SQ_LDS_BANK_CONFLICT", 0),
