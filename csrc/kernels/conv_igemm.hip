@@ -346,6 +346,9 @@ int sk_launch(const KvConvParams* p, int tile, hipStream_t stream);
 // v10 direct-epilogue forms of the v4 family (conv_direct.hip): indices after v8
 int direct_de_num_tiles();
 int direct_de_launch(const KvConvParams* p, int tile, hipStream_t stream);
+// v12 skinny implicit GEMM for edge batches (conv_skinny.hip): indices after v10
+int skinny_num_tiles();
+int skinny_launch(const KvConvParams* p, int tile, hipStream_t stream);
 // v9 bottleneck seam, conv3 + residual -> next conv1 (conv_seam.hip): tail calls only, tile
 // indices after the whole table above (kv_conv_num_tiles() + i)
 int seam_num_tiles();
@@ -359,7 +362,8 @@ extern "C" int kv_nloop_sched_check(void) { return kvedge::nloop_sched_check(); 
 
 extern "C" int kv_conv_num_tiles(void) {
   return kNumTiles + glds_num_tiles() + stream_num_tiles() + direct_num_tiles() +
-         nloop_num_tiles() + xp_num_tiles() + sk_num_tiles() + direct_de_num_tiles();
+         nloop_num_tiles() + xp_num_tiles() + sk_num_tiles() + direct_de_num_tiles() +
+         skinny_num_tiles();
 }
 
 extern "C" int kv_conv_pick_tile(const KvConvParams* p) {
@@ -511,7 +515,9 @@ static int kv_conv2d_one(const KvConvParams* p, int tile, hipStream_t stream) {
   const int v7 = v6 + nloop_num_tiles();
   const int v8 = v7 + xp_num_tiles();
   const int v10 = v8 + sk_num_tiles();
-  if (tile >= v10 + direct_de_num_tiles()) return -6;
+  const int v12 = v10 + direct_de_num_tiles();
+  if (tile >= v12 + skinny_num_tiles()) return -6;
+  if (tile >= v12) return skinny_launch(p, tile - v12, stream);
   if (tile >= v10) return direct_de_launch(p, tile - v10, stream);
   if (tile >= v8) return sk_launch(p, tile - v8, stream);
   if (tile >= v7) return xp_launch(p, tile - v7, stream);

@@ -27,6 +27,10 @@ from .layers import (DeployedConv, DeployedDualConv, calibrate_bn, count_flops, 
                      frames_to_nchw)
 
 ACT_NONE, ACT_RELU = ops.ACT_NONE, ops.ACT_RELU
+# Stage-1 fused tails (v3 streaming tail tile) only from this many output rows (N*Ho*Wo) up;
+# below it conv3 and the next conv1 run as separate launches, which the edge-batch v12 tiles
+# cover (A/B knob; 0 = always fuse)
+TAIL1_MIN_ROWS = int(os.environ.get("KVEDGE_TAIL1_MIN_ROWS", "0"))
 
 
 # ---------------------------------------------------------------------------
@@ -181,10 +185,10 @@ class DeployedBottleneck:
         the split-K conv3 and conv1 launches.  The stage-1 tail has no such limit.
         ``batch``: gate on this batch instead of x's (micro-batches use the FULL batch, so
         both paths fuse the same boundaries and round y the same way -- ADVICE r4)."""
-        if self.c3.spec.cout == 256:
-            return True
         N, Ho, Wo, _ = self.out_shape(x.shape)
         N = batch or N
+        if self.c3.spec.cout == 256:
+            return N * Ho * Wo >= TAIL1_MIN_ROWS
         return (N * Ho * Wo + 127) // 128 >= ops.SEAM_MIN_WGS
 
     def call_tail(self, x, nxt: "DeployedBottleneck", t1=None, out=None, z=None):

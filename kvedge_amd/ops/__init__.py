@@ -63,7 +63,8 @@ def load(build_if_missing: bool = False) -> bool:
         return False
     _check_single_hip_runtime()
     global SPLITK0
-    SPLITK0 = int(torch.ops.kvedge.conv_num_tiles()) - N_DE_TILES - N_SPLITK_TILES
+    SPLITK0 = (int(torch.ops.kvedge.conv_num_tiles()) - N_SKINNY_TILES - N_DE_TILES -
+               N_SPLITK_TILES)
     _loaded = True
     return True
 
@@ -207,7 +208,8 @@ _WS: dict = {}
 SPLITK_MAX_ELEMS = 32 << 20  # 128 MB of fp32 per stream at most
 SPLITK_MAX_SPLIT = 32        # largest split of conv_sk.hip kSkTiles
 N_SPLITK_TILES = 19          # conv_sk.hip kSkTiles
-N_DE_TILES = 3               # v10 direct-epilogue tiles (conv_direct.hip): after split-K, last
+N_DE_TILES = 3               # v10 direct-epilogue tiles (conv_direct.hip): after split-K
+N_SKINNY_TILES = 9           # v12 edge-batch tiles (conv_skinny.hip kSknTiles): last
 SPLITK0 = 1 << 30            # first split-K tile index, set by load()
 
 

@@ -103,7 +103,7 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale
 
 
-N_TILES = 108  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue / N-160 (68-85) + v8 split-K (86-104) + v10 (105-107)
+N_TILES = 117  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue / N-160 (68-85) + v8 split-K (86-104) + v10 (105-107) + v12 (108-116)
 # + v6 A-resident N-loop 1x1 GEMM (58-67, conv_nloop.hip kNlTiles: one Kpad per tile;
 # 63-65 are the fused-downsample (dual) forms, 66-67 step 128 K at a time)
 NLOOP0 = 58
@@ -111,6 +111,8 @@ XP0 = 68  # v7: the v2 kernel's cross-stage pipelined loop (BK 32 rings, 8 waves
 SK0 = 86  # v8: split-K (conv_sk.hip kSkTiles): K slices per tile (clamped to the K steps)
 DE0 = 105  # v10: the direct family's direct-epilogue forms (conv_direct.hip): 8 waves at 1 / 2
 # workgroups per CU, the single-patch-buffer 4-wave form at 2 per CU
+SKN0 = 108  # v12: skinny edge-batch implicit GEMM (conv_skinny.hip kSknTiles): general /
+# 1x1 / dual convs whose every K source has Cin % 64 == 0, M < 65536
 # (cin, cout, k, stride, act) instantiated as v10 tile 0 / 1 / 2 (no residual, no fallback)
 DE_SHAPES = {
     0: {(64, 64, 3, 1, ops.ACT_RELU), (64, 128, 3, 1, ops.ACT_SILU), (64, 16, 3, 1, ops.ACT_SILU),
@@ -196,6 +198,16 @@ def test_tile_count():
 ])
 def test_conv_every_tile(tile, case):
     N, H, W, cin, cout, k, s, p, act, res, lx, xc = case
+    if tile >= SKN0:
+        if cin % 64 == 0:
+            err, scale = _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx,
+                                    x_coff=xc, tile=tile)
+            assert err <= 0.02 * scale, (tile, case, err, scale)
+        else:
+            with pytest.raises(RuntimeError):
+                _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
+                           tile=tile)
+        return
     if tile >= DE0:
         if _de_takes(tile, cin, cout, k, s, act, res) and p == k // 2:
             err, scale = _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx,
@@ -477,7 +489,7 @@ def test_conv_dual_fused_downsample(tile, geom):
     w = (torch.randn(cout, K1 + K2, generator=g) * 0.05).to(torch.bfloat16)
     b = torch.randn(cout, generator=g)
     ref = ops.conv_dual(x1, x2, w, b, ops.ACT_RELU, s)
-    if tile >= DE0:
+    if DE0 <= tile < SKN0:
         with pytest.raises(RuntimeError):  # the v10 direct forms take no dual-source GEMM
             ops.conv_dual(x1.cuda(), x2.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, s, tile=tile)
         return
@@ -503,7 +515,8 @@ def test_conv_dual_rejects_v1_tiles():
 
 
 @pytest.mark.parametrize("tile", [-1, 1, 6, 7, 12, 13, STREAM0, STREAM0 + 1, STREAM0 + 5, DIRECT0,
-                                  DIRECT0 + 1, XP0, XP0 + 4, SK0, SK0 + 9, DE0, DE0 + 2])
+                                  DIRECT0 + 1, XP0, XP0 + 4, SK0, SK0 + 9, DE0, DE0 + 2,
+                                  SKN0, SKN0 + 4, SKN0 + 6, SKN0 + 8])
 @pytest.mark.parametrize("k", [1, 3])
 def test_conv_poisoned_canary(tile, k):
     """SURVEY §5.2 poisoned-buffer check: the output buffer is NaN-filled, with a NaN
@@ -512,10 +525,10 @@ def test_conv_poisoned_canary(tile, k):
     (a kernel that writes past M/N tails or outside [y_coff, y_coff+cout) fails here)."""
     if STREAM0 <= tile < DIRECT0 and k != 1:
         pytest.skip("v3 tiles take 1x1 GEMMs only")
-    if (DIRECT0 <= tile < XP0 or tile >= DE0) and k != 3:
+    if (DIRECT0 <= tile < XP0 or DE0 <= tile < SKN0) and k != 3:
         pytest.skip("v4 / v10 take 3x3 only here")
     N, H, W, cin, cout, ldy, y_coff = 3, 13, 11, 64, 72, 104, 16
-    if DIRECT0 <= tile < XP0 or tile >= DE0:
+    if DIRECT0 <= tile < XP0 or DE0 <= tile < SKN0:
         cout = 64  # an instantiated direct shape (64 -> 64 ReLU)
     spec = ConvSpec.auto(cin, cout, k, 1, k // 2, ops.ACT_RELU)
     g = torch.Generator().manual_seed(3)
@@ -878,3 +891,35 @@ def test_bneck_fused_exact_small_integers():
     # bf16 rounding of the intermediates is identical on both sides up to summation order
     assert d.max().item() <= 0.5 * ref.float().abs().max().item() * 2 ** -7 + 1e-6, d.max()
     assert (d > 0).float().mean().item() < 0.01
+
+
+@pytest.mark.parametrize("tile", list(range(SKN0, N_TILES)))
+@pytest.mark.parametrize("case", [
+    # (N, H, W, cin, cout, k, stride, pad, act, res): ResNet-50 edge-batch layers
+    (1, 14, 14, 256, 256, 3, 1, 1, ops.ACT_RELU, False),    # stage-3 3x3 (36 chunks)
+    (1, 14, 14, 512, 512, 3, 2, 1, ops.ACT_RELU, False),    # stage-4 entry 3x3/2 (72 chunks)
+    (1, 7, 7, 2048, 512, 1, 1, 0, ops.ACT_RELU, False),     # stage-4 reduce (M = 49 tail)
+    (3, 7, 7, 512, 2048, 1, 1, 0, ops.ACT_RELU, True),      # stage-4 expand + residual
+    (1, 1, 1, 2048, 1000, 1, 1, 0, ops.ACT_NONE, False),    # FC: M = 1, Cout tail
+    (2, 28, 28, 128, 128, 3, 1, 1, ops.ACT_RELU, False),    # stage 2 at b2 (M = 1568)
+])
+def test_skinny_edge_shapes(tile, case):
+    """v12 (conv_skinny.hip) at the layer shapes it is for: multi-pass K (every tile's
+    per-pass reach is below the 4608-deep stage-4 3x3), padding taps, M and Cout tails."""
+    N, H, W, cin, cout, k, s, p, act, res = case
+    err, scale = _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, tile=tile)
+    assert err <= 0.02 * scale, (tile, case, err, scale)
+
+
+@pytest.mark.parametrize("tile", list(range(SKN0, N_TILES)))
+def test_skinny_dual_stage4(tile):
+    """The stage-4 entry's conv3 + downsample (512 @7x7 + 1024 @14x14 / 2 -> 2048) at b1."""
+    g = torch.Generator().manual_seed(tile)
+    x1 = torch.randn(1, 7, 7, 512, generator=g).to(torch.bfloat16)
+    x2 = torch.randn(1, 14, 14, 1024, generator=g).to(torch.bfloat16)
+    w = (torch.randn(2048, 1536, generator=g) * 0.03).to(torch.bfloat16)
+    b = torch.randn(2048, generator=g)
+    ref = ops.conv_dual(x1, x2, w, b, ops.ACT_RELU, 2)
+    got = ops.conv_dual(x1.cuda(), x2.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, 2, tile=tile)
+    torch.cuda.synchronize()
+    _assert_close(got.cpu(), ref, ("skinny dual", tile))

@@ -18,6 +18,9 @@ def main():
     ap.add_argument("--concurrent", type=int, default=1,
                     help="launch each call on this many streams at once (the multi-stream "
                          "engine's situation) and report time per call")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the --iters launches in one hipGraph and time its replay "
+                         "(edge batches: a bare launch loop is host-bound near 7 us per call)")
     a = ap.parse_args()
     import torch
     from kvedge_amd import ops
@@ -45,7 +48,26 @@ def main():
 
     side = [torch.cuda.Stream() for _ in range(a.concurrent)]
 
+    def timeit_graph(fn):
+        fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(a.iters):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        for _ in range(5):
+            g.replay()
+        en.record()
+        torch.cuda.synchronize()
+        return st.elapsed_time(en) / (5 * a.iters) * 1e3
+
     def timeit(fn):
+        if a.graph:
+            return timeit_graph(fn)
         for _ in range(3):
             fn()
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
