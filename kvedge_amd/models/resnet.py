@@ -27,10 +27,11 @@ from .layers import (DeployedConv, DeployedDualConv, calibrate_bn, count_flops, 
                      frames_to_nchw)
 
 ACT_NONE, ACT_RELU = ops.ACT_NONE, ops.ACT_RELU
-# Stage-1 fused tails (v3 streaming tail tile) only from this many output rows (N*Ho*Wo) up;
-# below it conv3 and the next conv1 run as separate launches, which the edge-batch v12 tiles
-# cover (A/B knob; 0 = always fuse)
-TAIL1_MIN_ROWS = int(os.environ.get("KVEDGE_TAIL1_MIN_ROWS", "0"))
+# Stage-1 fused tails (v3 streaming tail tile) only from this many output rows (N*Ho*Wo) up:
+# below it (batch <= 10) conv3 and the next conv1 run as separate launches on the edge-batch
+# v12 / v1 tiles, which is faster there (same-box A/B, profiles/r5_v8_edge_ab.txt: b1 0.351
+# -> 0.336 ms, b8 0.483 -> 0.463 ms with the v12 family's first form).  0 = always fuse.
+TAIL1_MIN_ROWS = int(os.environ.get("KVEDGE_TAIL1_MIN_ROWS", "32768"))
 
 
 # ---------------------------------------------------------------------------
