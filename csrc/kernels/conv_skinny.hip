@@ -12,16 +12,17 @@
 //
 //   - a workgroup owns a (16 MB) x (16 NB) output tile; its WAVES waves split K in 64-wide
 //     chunks (chunk c goes to wave c % WAVES);
-//   - every wave issues the loads of all its chunks of a pass (NCW chunks) before its first
-//     MFMA -- one memory latency per pass instead of one per K step -- as LDS DMA into
-//     wave-private slots (buffer_load ... lds, lane-linear: eight lanes per 128-B row
-//     segment).  The first form loaded the MFMA fragments straight into VGPRs: every 16-lane
-//     group of a load then touched 16 rows, and a 3x3 of stage 4 ran at about a quarter of the
-//     L2 -> CU rate (profiles/r5_v7_skinny_tiles_b1.md);
+//   - every wave streams its chunks through a private ring of R LDS slots (R chunks in
+//     flight per wave, WAVES x R per workgroup: a layer of at most that many chunks costs one
+//     memory latency, not one per K step) as LDS DMA (buffer_load ... lds, lane-linear: eight
+//     lanes per 128-B row segment).  The first form loaded the MFMA fragments straight into
+//     VGPRs: every 16-lane group of a load then touched 16 rows, and a 3x3 of stage 4 ran at
+//     about a quarter of the L2 -> CU rate (profiles/r5_v7_skinny_tiles_b1.md vs
+//     r5_v8_skinny_tiles_b1.md);
 //   - padding taps, rows past M, channels past Cout and chunks past K read an offset beyond
-//     the buffer descriptor and land as zeros, so the load schedule has no branches; a
-//     counted s_waitcnt vmcnt per chunk lets the first chunks' MFMAs run while the later
-//     ones are still in flight (no barrier: each wave reads only its own slots);
+//     the buffer descriptor and land as zeros, so every ring step issues the same DMA count
+//     and one counted s_waitcnt vmcnt per chunk suffices (no barrier: each wave reads only
+//     its own slots);
 //   - the waves' fp32 partial tiles are summed through LDS by the epilogue threads, which
 //     add bias and residual, apply the activation and store bf16 -- no split-K workspace and
 //     no finalize launch.
@@ -30,8 +31,9 @@
 // lane's four accumulators are four consecutive output channels of one pixel, as in
 // conv_nloop.hip.  Within a 64-wide chunk, MFMA step s and lane quarter q cover reduction
 // indices s*32 + q*8 .. +8 of BOTH operands (16-B piece 4s + q of the row's 128 B), read
-// from the slot with an XOR swizzle (piece ^ row % 8) that the DMA source addresses apply.  The blockIdx -> tile map is n-major through xcd_remap, so the
-// m-tiles that share a weight panel run on one XCD and share its L2.
+// from the slot with an XOR swizzle (piece ^ row % 8) that the DMA source addresses apply.
+// The blockIdx -> tile map is n-major through xcd_remap, so the m-tiles that share a weight
+// panel run on one XCD and share its L2.
 #include <algorithm>
 
 #include "common.h"
@@ -63,7 +65,7 @@ __device__ __forceinline__ int skn_qdiv(int n, float inv) {
 
 // MODE: 0 general (KH x KW window, stride, padding), 1 1x1 / stride 1 GEMM, 4 dual 1x1 source
 // (bottleneck conv3 + the downsample folded in as extra K: kvedge_kernels.h, mode 4)
-template <int MODE, int WAVES, int NCW, int MB, int NB>
+template <int MODE, int WAVES, int R, int MB, int NB>
 __global__ __launch_bounds__(WAVES * 64) void conv_skinny_kernel(const KvConvParams p, int mt,
                                                                  int ntiles, float inv_cpt,
                                                                  float inv_kw, FastDiv hw_d,
@@ -71,7 +73,7 @@ __global__ __launch_bounds__(WAVES * 64) void conv_skinny_kernel(const KvConvPar
   extern __shared__ __attribute__((aligned(16))) char skn_lds[];
   constexpr int kChunk = (MB + NB) * 2048;  // one 64-wide chunk: 16 rows x 128 B per block
   constexpr int kDma = 2 * (MB + NB);       // LDS-DMA instructions per chunk
-  static_assert(NCW * kDma <= 63, "vmcnt field");
+  static_assert(R * kDma <= 63, "vmcnt field");
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   if (L >= ntiles) return;
   const int ntile = L / mt, mtile = L - ntile * mt;  // n-major: one weight panel per XCD run
@@ -80,31 +82,42 @@ __global__ __launch_bounds__(WAVES * 64) void conv_skinny_kernel(const KvConvPar
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   constexpr bool dual = MODE == 4;
   constexpr bool gemm = MODE != 0;  // 1x1 / stride 1 sources: pixel index = output row
-  char* const wlds = skn_lds + w * NCW * kChunk;  // this wave's chunk slots
+  char* const wlds = skn_lds + w * R * kChunk;  // this wave's ring of chunk slots
 
   const kv_i32x4 rx = kv_rsrc4(p.x, skn_bytes((long long)p.N * p.H * p.W * p.ldx * 2));
   const kv_i32x4 rx2 =
       kv_rsrc4(dual ? p.x2 : p.x, dual ? skn_bytes((long long)p.N * p.H2 * p.W2 * p.ldx2 * 2) : 0);
   const kv_i32x4 rw = kv_rsrc4(p.w, skn_bytes((long long)p.Cout * p.Kpad * 2));
 
-  // ---- epilogue operands first (the oldest loads: back long before the epilogue)
+  // ---- epilogue operands first (the oldest loads: back long before the epilogue).  Item =
+  // one lane's four output channels of one 16 x 16 block; a thread owns kIter of them
   constexpr int kItems = 64 * MB * NB;
-  const int item = threadIdx.x;
-  const int ej = item >> 6, el = item & 63;
-  const int e_nb = ej / MB, e_mb = ej - e_nb * MB;
-  const int e_n = n0 + e_nb * 16 + (el >> 4) * 4, e_m = m0 + e_mb * 16 + (el & 15);
-  const bool e_ok = item < kItems && e_m < p.M && e_n < p.Cout;
-  floatx4 bias4 = {0.f, 0.f, 0.f, 0.f};
-  skn_u32x2 res2 = {0u, 0u};
-  if (p.bias) {
-    const __amdgpu_buffer_rsrc_t rb = skn_rsrc(p.bias, (long long)p.Cout * 4);
-    bias4 = __builtin_bit_cast(
-        floatx4, __builtin_amdgcn_raw_buffer_load_b128(rb, e_ok ? (unsigned)e_n * 4u : kSknOOB, 0, 0));
-  }
-  if (p.res) {
-    const __amdgpu_buffer_rsrc_t rr = skn_rsrc(p.res, (long long)p.M * p.ldr * 2);
-    res2 = __builtin_amdgcn_raw_buffer_load_b64(
-        rr, e_ok ? (unsigned)(e_m * p.ldr + p.r_coff + e_n) * 2u : kSknOOB, 0, 0);
+  constexpr int kIter = (kItems + WAVES * 64 - 1) / (WAVES * 64);
+  int e_m[kIter], e_n[kIter];
+  bool e_ok[kIter];
+  floatx4 bias4[kIter];
+  skn_u32x2 res2[kIter];
+#pragma unroll
+  for (int it = 0; it < kIter; ++it) {
+    const int item = threadIdx.x + it * WAVES * 64;
+    const int ej = item >> 6, el = item & 63;
+    const int e_nb = ej / MB, e_mb = ej - e_nb * MB;
+    e_n[it] = n0 + e_nb * 16 + (el >> 4) * 4;
+    e_m[it] = m0 + e_mb * 16 + (el & 15);
+    e_ok[it] = item < kItems && e_m[it] < p.M && e_n[it] < p.Cout;
+    bias4[it] = floatx4{0.f, 0.f, 0.f, 0.f};
+    res2[it] = skn_u32x2{0u, 0u};
+    if (p.bias) {
+      const __amdgpu_buffer_rsrc_t rb = skn_rsrc(p.bias, (long long)p.Cout * 4);
+      bias4[it] = __builtin_bit_cast(
+          floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                       rb, e_ok[it] ? (unsigned)e_n[it] * 4u : kSknOOB, 0, 0));
+    }
+    if (p.res) {
+      const __amdgpu_buffer_rsrc_t rr = skn_rsrc(p.res, (long long)p.M * p.ldr * 2);
+      res2[it] = __builtin_amdgcn_raw_buffer_load_b64(
+          rr, e_ok[it] ? (unsigned)(e_m[it] * p.ldr + p.r_coff + e_n[it]) * 2u : kSknOOB, 0, 0);
+    }
   }
 
   // ---- DMA geometry: DMA j (0, 1) of a 16-row block brings rows 8j + (lane >> 3); lane
@@ -136,8 +149,7 @@ __global__ __launch_bounds__(WAVES * 64) void conv_skinny_kernel(const KvConvPar
     }
 
   const int nch = p.K >> 6;
-  const int per_pass = WAVES * NCW;
-  const int npass = (nch + per_pass - 1) / per_pass;
+  const int nloc = (nch - w + WAVES - 1) / WAVES;  // this wave's chunks: c = w + WAVES * i
   floatx4 acc[NB][MB];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb)
@@ -148,79 +160,83 @@ __global__ __launch_bounds__(WAVES * 64) void conv_skinny_kernel(const KvConvPar
   const int frag0 = r16 * 128 + ((q ^ (r16 & 7)) << 4);
   const int frag1 = r16 * 128 + (((4 + q) ^ (r16 & 7)) << 4);
 
-  for (int ps = 0; ps < npass; ++ps) {
-    // the previous pass's fragment reads are consumed by its MFMAs; make sure they have
-    // left the LDS before the DMA overwrites the slots
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // the kDma DMAs of local chunk i into a slot; past the wave's last chunk every offset is
+  // out of range (zero-fill, no memory traffic), so each ring step issues the same count
+  auto issue = [&](int i, char* slot) __attribute__((always_inline)) {
+    const int c = w + WAVES * i;  // wave-uniform
+    const bool cin = i < nloc;
+    const int k0 = c * 64;
+    bool second = false;
+    int tap_off = 0, cin0 = k0, r = 0, s = 0;
+    if constexpr (dual) {
+      second = k0 >= p.K1;
+      cin0 = second ? k0 - p.K1 : k0;
+    } else if constexpr (!gemm) {
+      const int t = skn_qdiv(c, inv_cpt);
+      cin0 = k0 - t * p.Cin;
+      r = skn_qdiv(t, inv_kw);
+      s = t - r * p.KW;
+      tap_off = r * p.W + s;
+    }
 #pragma unroll
-    for (int i = 0; i < NCW; ++i) {
-      const int c = (ps * NCW + i) * WAVES + w;  // wave-uniform
-      const bool cin = c < nch;
-      const int k0 = c * 64;
-      bool second = false;
-      int tap_off = 0, cin0 = k0, r = 0, s = 0;
-      if constexpr (dual) {
-        second = k0 >= p.K1;
-        cin0 = second ? k0 - p.K1 : k0;
-      } else if constexpr (!gemm) {
-        const int t = skn_qdiv(c, inv_cpt);
-        cin0 = k0 - t * p.Cin;
-        r = skn_qdiv(t, inv_kw);
-        s = t - r * p.KW;
-        tap_off = r * p.W + s;
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bool ok = cin && mval[mb][j];
+        int pix = pixb[mb][j] + tap_off;
+        int ld = p.ldx, coff = p.x_coff;
+        if constexpr (!gemm)
+          ok = ok && (unsigned)(hi0[mb][j] + r) < (unsigned)p.H &&
+               (unsigned)(wi0[mb][j] + s) < (unsigned)p.W;
+        if (dual && second) {
+          pix = pix2[mb][j];
+          ld = p.ldx2;
+          coff = 0;
+        }
+        const unsigned off =
+            ok ? (unsigned)(pix * ld + coff + cin0) * 2u + (unsigned)g * 16u : kSknOOB;
+        kv_lds_dma16(dual && second ? rx2 : rx, slot + mb * 2048 + j * 1024, (int)off);
       }
-      char* slot = wlds + i * kChunk;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const unsigned off = cin ? wrow[nb][j] + (unsigned)k0 * 2u : kSknOOB;
+        kv_lds_dma16(rw, slot + MB * 2048 + nb * 2048 + j * 1024, (int)off);
+      }
+  };
+
+  // ring of R chunk slots per wave: R chunks in flight, chunk i consumed once its DMAs have
+  // landed (the (R - 1) x kDma younger ones may still be in flight; this wave's own slots, so
+  // no barrier), its slot refilled with chunk i + R as soon as the fragments are in VGPRs
+  static_range<0, R>([&](auto ic) { issue(decltype(ic)::value, wlds + decltype(ic)::value * kChunk); });
+  int si = 0;
+  for (int i = 0; i < nloc; ++i) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDma * (R - 1)) : "memory");
+    char* slot = wlds + si * kChunk;
+    bf16x8 af[2][MB], bfr[2][NB];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int fo = st ? frag1 : frag0;
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb)
+        af[st][mb] = *reinterpret_cast<const bf16x8*>(slot + mb * 2048 + fo);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          bool ok = cin && mval[mb][j];
-          int pix = pixb[mb][j] + tap_off;
-          int ld = p.ldx, coff = p.x_coff;
-          if constexpr (!gemm)
-            ok = ok && (unsigned)(hi0[mb][j] + r) < (unsigned)p.H &&
-                 (unsigned)(wi0[mb][j] + s) < (unsigned)p.W;
-          if (dual && second) {
-            pix = pix2[mb][j];
-            ld = p.ldx2;
-            coff = 0;
-          }
-          const unsigned off =
-              ok ? (unsigned)(pix * ld + coff + cin0) * 2u + (unsigned)g * 16u : kSknOOB;
-          kv_lds_dma16(dual && second ? rx2 : rx, slot + mb * 2048 + j * 1024, (int)off);
-        }
+      for (int nb = 0; nb < NB; ++nb)
+        bfr[st][nb] = *reinterpret_cast<const bf16x8*>(slot + MB * 2048 + nb * 2048 + fo);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read out: refill it
+    issue(i + R, slot);
+    si = si + 1 == R ? 0 : si + 1;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const unsigned off = cin ? wrow[nb][j] + (unsigned)k0 * 2u : kSknOOB;
-          kv_lds_dma16(rw, slot + MB * 2048 + nb * 2048 + j * 1024, (int)off);
-        }
-    }
-    // consume chunk i once its DMAs have landed: the kDma x (NCW - 1 - i) younger ones may
-    // still be in flight (this wave's own slots: no barrier)
-    static_range<0, NCW>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDma * (NCW - 1 - i)) : "memory");
-      const char* slot = wlds + i * kChunk;
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const int fo = st ? frag1 : frag0;
-        bf16x8 af[MB], bfr[NB];
-#pragma unroll
         for (int mb = 0; mb < MB; ++mb)
-          af[mb] = *reinterpret_cast<const bf16x8*>(slot + mb * 2048 + fo);
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-          bfr[nb] = *reinterpret_cast<const bf16x8*>(slot + MB * 2048 + nb * 2048 + fo);
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-          for (int mb = 0; mb < MB; ++mb)
-            acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nb], af[mb], acc[nb][mb], 0, 0, 0);
-      }
-    });
+          acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[st][nb], af[st][mb], acc[nb][mb], 0, 0, 0);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing zero-fills land first
 
   // ---- sum the waves' partial tiles (over the chunk slots), then bias / residual /
   // activation -> bf16
@@ -231,44 +247,49 @@ __global__ __launch_bounds__(WAVES * 64) void conv_skinny_kernel(const KvConvPar
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) red[(w * MB * NB + nb * MB + mb) * 64 + lane] = acc[nb][mb];
   __syncthreads();
-  if (item >= kItems) return;
-  floatx4 v = red[ej * 64 + el];
-#pragma unroll
-  for (int ww = 1; ww < WAVES; ++ww) v += red[(ww * MB * NB + ej) * 64 + el];
   const int act = p.act & 3;
   const bool after = (p.act & 4) != 0;
-  const bf16x4 r4 = __builtin_bit_cast(bf16x4, res2);
-  bf16x4 o;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float x = v[e] + bias4[e];
-    const float rr = p.res ? (float)r4[e] : 0.f;
-    if (!after) x += rr;
-    x = apply_act(x, act);
-    if (after) x += rr;
-    o[e] = f2bf(x);
-  }
   const __amdgpu_buffer_rsrc_t ry = skn_rsrc(p.y, (long long)p.M * p.ldy * 2);
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(skn_u32x2, o), ry,
-                                        e_ok ? (unsigned)(e_m * p.ldy + p.y_coff + e_n) * 2u : kSknOOB,
-                                        0, 0);
+#pragma unroll
+  for (int it = 0; it < kIter; ++it) {
+    const int item = threadIdx.x + it * WAVES * 64;
+    if (item >= kItems) break;
+    const int ej = item >> 6, el = item & 63;
+    floatx4 v = red[ej * 64 + el];
+#pragma unroll
+    for (int ww = 1; ww < WAVES; ++ww) v += red[(ww * MB * NB + ej) * 64 + el];
+    const bf16x4 r4 = __builtin_bit_cast(bf16x4, res2[it]);
+    bf16x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = v[e] + bias4[it][e];
+      const float rr = p.res ? (float)r4[e] : 0.f;
+      if (!after) x += rr;
+      x = apply_act(x, act);
+      if (after) x += rr;
+      o[e] = f2bf(x);
+    }
+    __builtin_amdgcn_raw_buffer_store_b64(
+        __builtin_bit_cast(skn_u32x2, o), ry,
+        e_ok[it] ? (unsigned)(e_m[it] * p.ldy + p.y_coff + e_n[it]) * 2u : kSknOOB, 0, 0);
+  }
 }
 
 typedef void (*SknFn)(const KvConvParams, int, int, float, float, FastDiv, FastDiv);
 struct SknTile {
   SknFn fn[3];  // general, 1x1 GEMM, dual
-  int waves, ncw, mb, nb;
+  int waves, ring, mb, nb;
 };
-#define KV_SKN(W, C, M, N)                                                             \
-  {{&conv_skinny_kernel<0, W, C, M, N>, &conv_skinny_kernel<1, W, C, M, N>,            \
-    &conv_skinny_kernel<4, W, C, M, N>},                                               \
-   W, C, M, N}
-// (waves, chunks per wave and pass, 16-row blocks, 16-channel blocks).  Per-pass K reach =
-// waves x chunks x 64; LDS = waves x chunks x (MB + NB) x 2 KB (<= 128 KB)
+#define KV_SKN(W, R, M, N)                                                             \
+  {{&conv_skinny_kernel<0, W, R, M, N>, &conv_skinny_kernel<1, W, R, M, N>,            \
+    &conv_skinny_kernel<4, W, R, M, N>},                                               \
+   W, R, M, N}
+// (waves, ring slots per wave, 16-row blocks, 16-channel blocks); LDS = waves x slots x
+// (MB + NB) x 2 KB.  16 x 16 tiles for batch 1-2, 32 x 32 / 64 x 32 / 64 x 64 for batch ~8
 const SknTile kSknTiles[] = {
-    KV_SKN(4, 8, 1, 1), KV_SKN(8, 4, 1, 1), KV_SKN(16, 2, 1, 1), KV_SKN(4, 4, 1, 1),
-    KV_SKN(8, 2, 1, 1), KV_SKN(4, 4, 2, 2), KV_SKN(8, 2, 2, 2), KV_SKN(4, 4, 2, 1),
-    KV_SKN(8, 3, 1, 1),
+    KV_SKN(4, 4, 1, 1), KV_SKN(8, 4, 1, 1), KV_SKN(16, 2, 1, 1), KV_SKN(8, 2, 2, 1),
+    KV_SKN(8, 2, 2, 2), KV_SKN(4, 4, 2, 2), KV_SKN(4, 2, 4, 2), KV_SKN(4, 2, 2, 4),
+    KV_SKN(4, 2, 4, 4),
 };
 #undef KV_SKN
 
@@ -297,7 +318,7 @@ int skinny_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   const FastDiv hw = make_fastdiv(p->Ho * p->Wo);
   const FastDiv wo = make_fastdiv(p->Wo);
   const SknFn fn = e.fn[p->mode == 0 ? 0 : p->mode == 1 ? 1 : 2];
-  const int lds = std::max(e.waves * e.ncw * (e.mb + e.nb) * 2048, e.waves * e.mb * e.nb * 1024);
+  const int lds = std::max(e.waves * e.ring * (e.mb + e.nb) * 2048, e.waves * e.mb * e.nb * 1024);
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
     return -7;
