@@ -631,6 +631,60 @@ int64_t bneck_fused_supported(int64_t C, int64_t H, int64_t W) {
   return kv_bneck_fused_supported((int)C, (int)H, (int)W);
 }
 
+// v13 fused YOLOv8 C2f(32, 32, n=1, shortcut) (csrc/kernels/c2f_fused.hip): x [N, H, W, ldx]
+// channels x_coff .. x_coff + 31 -> y [N, H, W, ldy] channels y_coff .. y_coff + 31
+void c2f16_fused(const at::Tensor& x, int64_t x_coff, const at::Tensor& w1, const at::Tensor& b1,
+                 const at::Tensor& wm1, const at::Tensor& bm1, const at::Tensor& wm2,
+                 const at::Tensor& bm2, const at::Tensor& w2, const at::Tensor& b2, at::Tensor& y,
+                 int64_t y_coff, int64_t S) {
+  check_bf16(x, "x");
+  check_bf16(y, "y");
+  for (const at::Tensor* w : {&w1, &wm1, &wm2, &w2}) check_bf16(*w, "w");
+  for (const at::Tensor* b : {&b1, &bm1, &bm2, &b2}) {
+    check_dev(*b, "bias");
+    TORCH_CHECK(b->scalar_type() == at::kFloat && b->is_contiguous(), "kvedge: c2f16 biases fp32");
+  }
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(0) == y.size(0) && x.size(1) == y.size(1) &&
+                  x.size(2) == y.size(2), "kvedge: c2f16 x / y [N, H, W, C]");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2);
+  TORCH_CHECK(x_coff >= 0 && x_coff + 32 <= x.size(3) && y_coff >= 0 && y_coff + 32 <= y.size(3),
+              "kvedge: c2f16 channel slices");
+  TORCH_CHECK(w1.dim() == 2 && w1.size(0) == 32 && w1.size(1) >= 32 && wm1.dim() == 2 &&
+                  wm1.size(0) == 16 && wm1.size(1) >= 144 && wm2.sizes() == wm1.sizes() &&
+                  w2.dim() == 2 && w2.size(0) == 32 && w2.size(1) >= 48,
+              "kvedge: c2f16 weights w1 [32, >=32], wm [16, >=144], w2 [32, >=48]");
+  TORCH_CHECK(b1.numel() == 32 && bm1.numel() == 16 && bm2.numel() == 16 && b2.numel() == 32,
+              "kvedge: c2f16 bias sizes");
+  TORCH_CHECK(kv_c2f16_supported((int)H, (int)W, (int)S), "kvedge: c2f16 has no form for H=", H,
+              " W=", W, " S=", S);
+  TORCH_CHECK(x.numel() * 2 < (1ll << 31) - (1 << 20) && y.numel() * 2 < (1ll << 31) - (1 << 20),
+              "kvedge: c2f16 operands exceed 2 GiB");
+  TORCH_CHECK(x.data_ptr() != y.data_ptr(), "kvedge: c2f16 cannot run in place");
+  const c10::DeviceGuard g(x.device());
+  KvC2fParams p{};
+  p.x = x.data_ptr();
+  p.y = y.data_ptr();
+  p.w1 = w1.data_ptr();
+  p.b1 = b1.data_ptr<float>();
+  p.wm1 = wm1.data_ptr();
+  p.bm1 = bm1.data_ptr<float>();
+  p.wm2 = wm2.data_ptr();
+  p.bm2 = bm2.data_ptr<float>();
+  p.w2 = w2.data_ptr();
+  p.b2 = b2.data_ptr<float>();
+  p.N = (int)N; p.H = (int)H; p.W = (int)W;
+  p.ldx = (int)x.size(3); p.x_coff = (int)x_coff;
+  p.ldy = (int)y.size(3); p.y_coff = (int)y_coff;
+  p.ldw1 = (int)w1.size(1); p.ldwm = (int)wm1.size(1); p.ldw2 = (int)w2.size(1);
+  p.S = (int)S;
+  const int rc = kv_c2f16_fused(&p, cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: c2f16_fused failed rc=", rc);
+}
+
+int64_t c2f16_supported(int64_t H, int64_t W, int64_t S) {
+  return kv_c2f16_supported((int)H, (int)W, (int)S);
+}
+
 }  // namespace
 
 TORCH_LIBRARY(kvedge, m) {
@@ -673,6 +727,9 @@ TORCH_LIBRARY(kvedge, m) {
   m.def("bneck_fused(Tensor x, Tensor w1, Tensor b1, Tensor w2, Tensor b2, Tensor w3, Tensor b3, "
         "Tensor(a!) y, int dbg=0) -> ()");
   m.def("bneck_fused_supported(int C, int H, int W) -> int", bneck_fused_supported);
+  m.def("c2f16_fused(Tensor x, int x_coff, Tensor w1, Tensor b1, Tensor wm1, Tensor bm1, "
+        "Tensor wm2, Tensor bm2, Tensor w2, Tensor b2, Tensor(a!) y, int y_coff, int S) -> ()");
+  m.def("c2f16_supported(int H, int W, int S) -> int", c2f16_supported);
   m.def("set_conv_chunk_bytes(int bytes) -> int", set_conv_chunk_bytes);
 }
 
@@ -685,6 +742,7 @@ TORCH_LIBRARY_IMPL(kvedge, CUDA, m) {
   m.impl("conv_tail", conv_tail);
   m.impl("conv_pair", conv_pair);
   m.impl("bneck_fused", bneck_fused);
+  m.impl("c2f16_fused", c2f16_fused);
   m.impl("sppf_pool", sppf_pool);
   m.impl("global_avgpool", global_avgpool);
   m.impl("softmax_rows", softmax_rows);

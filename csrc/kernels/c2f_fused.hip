@@ -1,0 +1,277 @@
+// v13: YOLOv8 C2f block with one 16-channel shortcut bottleneck as ONE launch (the b2 block
+// of YOLOv8n: C2f(32, 32, n=1, shortcut) at 160 x 160):
+//
+//   t = SiLU(W1 . x + b1)                      1x1 32 -> 32;  a = t[:16], s = t[16:]
+//   u = SiLU(conv3x3(s; Wm1) + bm1)            3x3 16 -> 16
+//   v = s + SiLU(conv3x3(u; Wm2) + bm2)        3x3 16 -> 16, shortcut after the activation
+//   y = SiLU(W2 . [a, s, v] + b2)              1x1 48 -> 32
+//
+// Unfused, the block is four launches that move 224 channels per pixel through HBM (t, u, v
+// written and re-read, the 48-channel concat read): the in-graph table of the YOLOv8n bench
+// step (profiles/r5_v6_graph_layers_yolo_b512.md, rows 1-4) puts it at ~2 ms of the 10.8 ms
+// step against ~0.3 ms of compulsory traffic (x read, y written: 64 channels per pixel).
+// Here x is read once and y written once; t / u stay in LDS rings.
+//
+// Decomposition: a workgroup sweeps a strip of S output rows of one image top to bottom, one
+// row per iteration, with row rings in LDS (s: 5 rows, u: 3 rows, a: 4 rows; zero columns
+// either side for the 3x3 padding, zero rows outside the image):
+//   A(o + 2): t of row o + 2 from x (prefetched PF rows ahead into registers)
+//   barrier
+//   B(o + 1): u of row o + 1 from s rows o .. o + 2
+//   barrier
+//   C(o):     v from u rows o - 1 .. o + 1 and s row o; y from a, s (LDS) and v (registers)
+// Two barriers per row suffice: every slot a step overwrites was last read two steps and at
+// least one barrier earlier (ring sizes chosen for that).  The strip's first rows repeat two
+// rows of t and one of u of the strip above (halo).
+//
+// MFMA: v_mfma_f32_16x16x32_bf16, weights as the first operand (D = W . X^T: a lane's four
+// accumulators are four consecutive output channels of one pixel).  The 3x3s run K = 9 taps
+// x 16 channels as five 32-wide steps, lane quarter q of step j reading tap 2j + q / 2 (the
+// tenth tap's weights are zero; its activations are read from a real pixel, so never NaN).
+// The concat's v part is fed to cv2 straight from the 3x3's accumulators: lane (pixel, q)
+// holds v channels 4q .. 4q + 3, so cv2's second K step takes them as k = 8q .. 8q + 3 with
+// zeros in k = 8q + 4 .. 8q + 7, and the weights are read in that permuted order -- v never
+// goes through LDS.
+#include "common.h"
+#include "kvedge_kernels.h"
+
+namespace kvedge {
+namespace {
+
+constexpr int kC2fWaves = 5;  // 160 = 5 waves x 2 blocks of 16 pixels, 80 = 5 x 1
+constexpr int kC2fPF = 2;     // x rows in flight ahead of step A (VGPR budget: 3 waves per SIMD)
+constexpr int kC2fRS = 5, kC2fRU = 3, kC2fRA = 4;
+typedef unsigned int c2f_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int c2f_u32x2 __attribute__((ext_vector_type(2)));
+constexpr unsigned kC2fOOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t c2f_rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(bytes > 0x7fffffffLL ? 0x7fffffffLL : bytes),
+                                           0x00020000);
+}
+
+__device__ __forceinline__ bf16x4 c2f_silu4(floatx4 acc, floatx4 b) {
+  bf16x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = f2bf(act_c<kActSilu>(acc[e] + b[e]));
+  return o;
+}
+
+template <int BPW>
+__global__ __launch_bounds__(kC2fWaves * 64, 3) void c2f16_kernel(const KvC2fParams p) {
+  extern __shared__ __attribute__((aligned(16))) char c2f_lds[];
+  constexpr int W = 16 * kC2fWaves * BPW;
+  constexpr int WP = W + 2;  // one zero column either side
+  bf16* const sring = reinterpret_cast<bf16*>(c2f_lds);  // [RS][WP][16]
+  bf16* const uring = sring + kC2fRS * WP * 16;          // [RU][WP][16]
+  bf16* const aring = uring + kC2fRU * WP * 16;          // [RA][W][16]
+
+  const int strips = p.H / p.S;
+  const int img = blockIdx.x / strips;
+  const int s0 = (blockIdx.x - img * strips) * p.S, s1 = s0 + p.S;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r16 = lane & 15, q = lane >> 4;
+  const int H = p.H;
+
+  // ---- zero the padding columns of the s / u rings (never written by the steps)
+  for (int i = threadIdx.x; i < (kC2fRS + kC2fRU) * 2 * 2; i += kC2fWaves * 64) {
+    const int slot = i >> 2, side = (i >> 1) & 1, half = i & 1;
+    bf16* row = slot < kC2fRS ? sring + slot * WP * 16 : uring + (slot - kC2fRS) * WP * 16;
+    *reinterpret_cast<c2f_u32x4*>(row + (side ? WP - 1 : 0) * 16 + half * 8) = c2f_u32x4{0, 0, 0, 0};
+  }
+
+  // ---- weights and biases in registers (every wave needs all of them)
+  const __amdgpu_buffer_rsrc_t rw1 = c2f_rsrc(p.w1, 32LL * p.ldw1 * 2);
+  const __amdgpu_buffer_rsrc_t rwm1 = c2f_rsrc(p.wm1, 16LL * p.ldwm * 2);
+  const __amdgpu_buffer_rsrc_t rwm2 = c2f_rsrc(p.wm2, 16LL * p.ldwm * 2);
+  const __amdgpu_buffer_rsrc_t rw2 = c2f_rsrc(p.w2, 32LL * p.ldw2 * 2);
+  bf16x8 w1f[2], wm1f[5], wm2f[5], w2f0[2], w2f1[2];
+  floatx4 b1v[2], b2v[2], bm1v, bm2v;
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    const int row = nb * 16 + r16;
+    w1f[nb] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                             rw1, (unsigned)(row * p.ldw1 + q * 8) * 2u, 0, 0));
+    w2f0[nb] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rw2, (unsigned)(row * p.ldw2 + q * 8) * 2u, 0, 0));
+    // cv2's v columns in the accumulator order: k = 8q + e <- v channel 4q + e (e < 4)
+    const c2f_u32x2 lo = __builtin_amdgcn_raw_buffer_load_b64(
+        rw2, (unsigned)(row * p.ldw2 + 32 + q * 4) * 2u, 0, 0);
+    w2f1[nb] = __builtin_bit_cast(bf16x8, c2f_u32x4{lo[0], lo[1], 0u, 0u});
+    b1v[nb] = *reinterpret_cast<const floatx4*>(p.b1 + nb * 16 + q * 4);
+    b2v[nb] = *reinterpret_cast<const floatx4*>(p.b2 + nb * 16 + q * 4);
+  }
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int tap = 2 * j + (q >> 1);
+    const unsigned off = tap < 9 ? (unsigned)(r16 * p.ldwm + tap * 16 + (q & 1) * 8) * 2u : kC2fOOB;
+    wm1f[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rwm1, off, 0, 0));
+    wm2f[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rwm2, off, 0, 0));
+  }
+  bm1v = *reinterpret_cast<const floatx4*>(p.bm1 + q * 4);
+  bm2v = *reinterpret_cast<const floatx4*>(p.bm2 + q * 4);
+
+  // 3x3 tap of lane quarter q in step j (the tenth tap re-reads tap 8: finite, weight 0)
+  int tdy[5], tdx[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const int tap = min(2 * j + (q >> 1), 8);
+    tdy[j] = tap / 3;
+    tdx[j] = tap % 3;
+  }
+
+  // ---- x rows: lane (pixel r16 of block b, quarter q) loads channels 8q .. 8q + 7
+  const __amdgpu_buffer_rsrc_t rx = c2f_rsrc(p.x, (long long)p.N * H * W * p.ldx * 2);
+  const __amdgpu_buffer_rsrc_t ry = c2f_rsrc(p.y, (long long)p.N * H * W * p.ldy * 2);
+  auto load_x = [&](int r, c2f_u32x4 (&dst)[BPW]) __attribute__((always_inline)) {
+    const bool ok = r >= 0 && r < H && r <= s1 + 1;
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) {
+      const int px = (w + kC2fWaves * b) * 16 + r16;
+      const unsigned off =
+          ok ? (unsigned)(((img * H + r) * W + px) * p.ldx + p.x_coff + q * 8) * 2u : kC2fOOB;
+      dst[b] = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
+    }
+  };
+  auto slot_s = [](int r) { return (r + 2 * kC2fRS) % kC2fRS; };
+  auto slot_u = [](int r) { return (r + 2 * kC2fRU) % kC2fRU; };
+  auto slot_a = [](int r) { return (r + 2 * kC2fRA) % kC2fRA; };
+
+  // step A: t of row r -> a ring (channels 0-15) and s ring (16-31; zero outside the image)
+  auto stepA = [&](int r, const c2f_u32x4 (&xr)[BPW]) __attribute__((always_inline)) {
+    const bool in = r >= 0 && r < H;
+    bf16* srow = sring + slot_s(r) * WP * 16;
+    bf16* arow = aring + slot_a(r) * W * 16;
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) {
+      const int px = (w + kC2fWaves * b) * 16 + r16;
+      const bf16x8 xf = __builtin_bit_cast(bf16x8, xr[b]);
+      const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+      const floatx4 ta = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[0], xf, z, 0, 0, 0);
+      const floatx4 ts = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[1], xf, z, 0, 0, 0);
+      bf16x4 sv = c2f_silu4(ts, b1v[1]);
+      if (!in) sv = bf16x4{0, 0, 0, 0};
+      *reinterpret_cast<bf16x4*>(arow + px * 16 + q * 4) = c2f_silu4(ta, b1v[0]);
+      *reinterpret_cast<bf16x4*>(srow + (px + 1) * 16 + q * 4) = sv;
+    }
+  };
+  // 3x3 16 -> 16 over three rows of a ring (rows r - 1 .. r + 1 at slots sl[0..2])
+  auto conv3 = [&](const bf16* ring, const int (&sl)[3], const bf16x8 (&wf)[5], int px)
+      __attribute__((always_inline)) -> floatx4 {
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const bf16* src = ring + (sl[tdy[j]] * WP + px + tdx[j]) * 16 + (q & 1) * 8;
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], *reinterpret_cast<const bf16x8*>(src),
+                                                    acc, 0, 0, 0);
+    }
+    return acc;
+  };
+  // step B: u of row r from s rows r - 1 .. r + 1 (zero outside the image)
+  auto stepB = [&](int r) __attribute__((always_inline)) {
+    const bool in = r >= 0 && r < H;
+    const int sl[3] = {slot_s(r - 1), slot_s(r), slot_s(r + 1)};
+    bf16* urow = uring + slot_u(r) * WP * 16;
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) {
+      const int px = (w + kC2fWaves * b) * 16 + r16;
+      bf16x4 uv = c2f_silu4(conv3(sring, sl, wm1f, px), bm1v);
+      if (!in) uv = bf16x4{0, 0, 0, 0};
+      *reinterpret_cast<bf16x4*>(urow + (px + 1) * 16 + q * 4) = uv;
+    }
+  };
+  // step C: v and y of output row o
+  auto stepC = [&](int o) __attribute__((always_inline)) {
+    const int sl[3] = {slot_u(o - 1), slot_u(o), slot_u(o + 1)};
+    const bf16* srow = sring + slot_s(o) * WP * 16;
+    const bf16* arow = aring + slot_a(o) * W * 16;
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) {
+      const int px = (w + kC2fWaves * b) * 16 + r16;
+      const floatx4 m = conv3(uring, sl, wm2f, px);
+      const bf16x4 sres = *reinterpret_cast<const bf16x4*>(srow + (px + 1) * 16 + q * 4);
+      bf16x8 vf;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // rounded to bf16 before and after the shortcut add, as the four-launch path does
+        vf[e] = f2bf((float)f2bf(act_c<kActSilu>(m[e] + bm2v[e])) + (float)sres[e]);
+        vf[4 + e] = (bf16)0.f;
+      }
+      // cv2's first K step: [a | s] channels 8q .. 8q + 7 of the concat
+      const bf16x8 as = q < 2 ? *reinterpret_cast<const bf16x8*>(arow + px * 16 + q * 8)
+                              : *reinterpret_cast<const bf16x8*>(srow + (px + 1) * 16 + (q - 2) * 8);
+      const size_t ybase = ((size_t)(img * H + o) * W + px) * p.ldy + p.y_coff;
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f0[nb], as, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f1[nb], vf, acc, 0, 0, 0);
+        const bf16x4 yv = c2f_silu4(acc, b2v[nb]);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(c2f_u32x2, yv), ry,
+                                              (unsigned)(ybase + nb * 16 + q * 4) * 2u, 0, 0);
+      }
+    }
+  };
+
+  // ---- prologue: t of rows s0 - 2 .. s0 + 1, u of rows s0 - 1, s0
+  {
+    c2f_u32x4 xp[4][BPW];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) load_x(s0 - 2 + i, xp[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) stepA(s0 - 2 + i, xp[i]);
+  }
+  c2f_u32x4 xr[kC2fPF][BPW];  // x of rows o + 2 .. o + 2 + PF - 1
+#pragma unroll
+  for (int i = 0; i < kC2fPF; ++i) load_x(s0 + 2 + i, xr[i]);
+  __syncthreads();
+  stepB(s0 - 1);
+  stepB(s0);
+  // ---- sweep: S is a multiple of PF, so the register ring index is static
+  for (int o = s0; o < s1; o += kC2fPF) {
+    static_range<0, kC2fPF>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      stepA(o + k + 2, xr[k]);
+      load_x(o + k + 2 + kC2fPF, xr[k]);
+      __syncthreads();
+      stepB(o + k + 1);
+      __syncthreads();
+      stepC(o + k);
+    });
+  }
+}
+
+}  // namespace
+
+int c2f16_lds_bytes(int W) {
+  return ((kC2fRS + kC2fRU) * (W + 2) + kC2fRA * W) * 16 * 2;
+}
+
+}  // namespace kvedge
+
+using namespace kvedge;
+
+extern "C" int kv_c2f16_supported(int H, int W, int S) {
+  return (W == 160 || W == 80) && S > 0 && S % kC2fPF == 0 && H % S == 0;
+}
+
+extern "C" int kv_c2f16_fused(const KvC2fParams* p, hipStream_t stream) {
+  if (!kv_c2f16_supported(p->H, p->W, p->S)) return -8;
+  if (p->ldx % 8 || p->x_coff % 8 || p->ldy % 4 || p->y_coff % 4 || p->ldw1 < 32 ||
+      p->ldw2 < 48 || p->ldwm < 144)
+    return -3;
+  const int lds = c2f16_lds_bytes(p->W);
+  const unsigned grid = (unsigned)(p->N * (p->H / p->S));
+  if (grid == 0) return 0;
+  const void* fn = p->W == 160 ? reinterpret_cast<const void*>(&c2f16_kernel<2>)
+                               : reinterpret_cast<const void*>(&c2f16_kernel<1>);
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+    return -7;
+  if (p->W == 160)
+    hipLaunchKernelGGL(c2f16_kernel<2>, dim3(grid), dim3(kC2fWaves * 64), (unsigned)lds, stream, *p);
+  else
+    hipLaunchKernelGGL(c2f16_kernel<1>, dim3(grid), dim3(kC2fWaves * 64), (unsigned)lds, stream, *p);
+  return hipGetLastError() == hipSuccess ? 0 : -7;
+}

@@ -166,6 +166,31 @@ typedef struct KvBneckParams {
 int kv_bneck_fused_supported(int C, int H, int W);
 int kv_bneck_fused(const KvBneckParams* p, hipStream_t stream);
 
+// ---------------------------------------------------------------------------
+// v13 fused YOLOv8 C2f(32, 32, n=1, shortcut) (c2f_fused.hip): t = SiLU(W1 . x + b1) (a =
+// t[:16], s = t[16:]), u = SiLU(conv3x3(s) + bm1), v = s + SiLU(conv3x3(u) + bm2),
+// y = SiLU(W2 . [a, s, v] + b2); NHWC bf16, x [N, H, W, ldx] at x_coff (32 channels), y at
+// y_coff (32); packed weights w1 [32][ldw1], wm1 / wm2 [16][ldwm] (tap-major, cin minor),
+// w2 [32][ldw2]; fp32 biases.  S: output rows per workgroup (a multiple of 4 dividing H).
+// ---------------------------------------------------------------------------
+typedef struct KvC2fParams {
+  const void* x;
+  void* y;
+  const void* w1;
+  const float* b1;
+  const void* wm1;
+  const float* bm1;
+  const void* wm2;
+  const float* bm2;
+  const void* w2;
+  const float* b2;
+  int N, H, W, ldx, x_coff, ldy, y_coff;
+  int ldw1, ldwm, ldw2;
+  int S;
+} KvC2fParams;
+int kv_c2f16_supported(int H, int W, int S);
+int kv_c2f16_fused(const KvC2fParams* p, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

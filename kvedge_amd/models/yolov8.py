@@ -186,9 +186,21 @@ class DC2f:
                 c2.spec.act |= ops.RES_AFTER_ACT
             self.m.append((_dc(b.cv1, device), c2, b.add))
 
+    def fused_ok(self, x) -> bool:
+        """The whole block as ONE v13 launch (ops.c2f16): C2f(32, 32, n=1, shortcut) -- the
+        b2 block at 160 x 160 -- on the GPU."""
+        N, H, W, _ = x.shape
+        return (ops.C2F_ENABLED and x.is_cuda and self.c == 16 and self.n == 1 and
+                self.m[0][2] and self.cv1.spec.cin == 32 and self.cv2.spec.cout == 32 and
+                ops.c2f16_strip(H, W) > 0)
+
     def __call__(self, x, x_coff=0, out=None, y_coff=0):
         N, H, W, _ = x.shape
         c, n = self.c, self.n
+        if self.fused_ok(x):
+            b1, b2, _ = self.m[0]
+            return ops.c2f16(x, self.cv1.w, self.cv1.b, b1.w, b1.b, b2.w, b2.b, self.cv2.w,
+                             self.cv2.b, out=out, x_coff=x_coff, y_coff=y_coff)
         cat = ops.empty(N, H, W, (2 + n) * c, dtype=torch.bfloat16, device=x.device)
         self.cv1(x, x_coff=x_coff, out=cat, y_coff=0)
         for i, (b1, b2, add) in enumerate(self.m):

@@ -389,6 +389,49 @@ def bottleneck_fused(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: to
     return out
 
 
+# v13 fused YOLOv8 C2f(32, 32, n=1, shortcut) (csrc/kernels/c2f_fused.hip): the b2 block at
+# 160 x 160.  KVEDGE_C2F=0 = the four-launch path (A/B knob)
+C2F_ENABLED = os.environ.get("KVEDGE_C2F", "1") != "0"
+
+
+def c2f16_strip(H: int, W: int) -> int:
+    """Output rows per workgroup of the fused C2f kernel (0 = no form for this shape)."""
+    for S in (40, 32, 20, 16, 8, 4):
+        if H % S == 0 and W in (80, 160):
+            return S
+    return 0
+
+
+def c2f16(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, wm1: torch.Tensor,
+          bm1: torch.Tensor, wm2: torch.Tensor, bm2: torch.Tensor, w2: torch.Tensor,
+          b2: torch.Tensor, out: Optional[torch.Tensor] = None, x_coff: int = 0,
+          y_coff: int = 0, S: int = 0) -> torch.Tensor:
+    """YOLOv8 C2f(32, 32, n=1, shortcut) as one pass: t = SiLU(W1 . x + b1) (a = t[:16],
+    s = t[16:]), u = SiLU(conv3x3(s) + bm1), v = s + SiLU(conv3x3(u) + bm2),
+    y = SiLU(W2 . [a, s, v] + b2).  Packed bf16 weights w1 [32, >=32], wm1 / wm2 [16, >=144]
+    (tap-major), w2 [32, >=48]; fp32 biases.  GPU: one launch, t / u / v never leave the chip.
+    CPU: the four reference convs with bf16 intermediates (what the kernel keeps in LDS and
+    registers, and what the four-launch path writes)."""
+    N, H, W, _ = x.shape
+    if out is None:
+        out = empty(N, H, W, 32, dtype=torch.bfloat16, device=x.device)
+    if x.is_cuda:
+        _native().c2f16_fused(x, x_coff, w1, b1, wm1, bm1, wm2, bm2, w2, b2, out, y_coff,
+                              S or c2f16_strip(H, W))
+        return out
+    s1 = ConvSpec.auto(32, 32, 1, 1, 0, ACT_SILU)
+    sm1 = ConvSpec.auto(16, 16, 3, 1, 1, ACT_SILU)
+    sm2 = ConvSpec.auto(16, 16, 3, 1, 1, ACT_SILU | RES_AFTER_ACT)
+    s2 = ConvSpec.auto(48, 32, 1, 1, 0, ACT_SILU)
+    cat = torch.empty(N, H, W, 48, dtype=torch.bfloat16)
+    u = torch.empty(N, H, W, 16, dtype=torch.bfloat16)
+    _ref.conv2d(x, s1, w1, b1, None, cat, x_coff, 0, 0)
+    _ref.conv2d(cat, sm1, wm1, bm1, None, u, 16, 0, 0)
+    _ref.conv2d(u, sm2, wm2, bm2, cat, cat, 0, 32, 16)
+    _ref.conv2d(cat, s2, w2, b2, None, out, 0, y_coff, 0)
+    return out
+
+
 def stem_pool(x: torch.Tensor, spec: "ConvSpec", w: torch.Tensor, bias: torch.Tensor,
               out: Optional[torch.Tensor] = None, y_coff: int = 0) -> torch.Tensor:
     """Fused ResNet stem + max pool: maxpool3x3/2(relu(conv_s2d(x) + bias)).

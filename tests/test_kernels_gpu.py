@@ -923,3 +923,83 @@ def test_skinny_dual_stage4(tile):
     got = ops.conv_dual(x1.cuda(), x2.cuda(), w.cuda(), b.cuda(), ops.ACT_RELU, 2, tile=tile)
     torch.cuda.synchronize()
     _assert_close(got.cpu(), ref, ("skinny dual", tile))
+
+
+def _c2f_weights(seed, exact=False):
+    g = torch.Generator().manual_seed(seed)
+    s1 = ConvSpec.auto(32, 32, 1, 1, 0, ops.ACT_SILU)
+    sm = ConvSpec.auto(16, 16, 3, 1, 1, ops.ACT_SILU)
+    s2 = ConvSpec.auto(48, 32, 1, 1, 0, ops.ACT_SILU)
+
+    def w(co, ci, k, spec, fan):
+        if exact:
+            return ops.pack_conv_weight(torch.randint(-1, 2, (co, ci, k, k), generator=g).float() / 8,
+                                        spec)
+        return ops.pack_conv_weight(torch.randn(co, ci, k, k, generator=g) * (2.0 / fan) ** 0.5, spec)
+
+    def b(n):
+        return (torch.randint(-2, 3, (n,), generator=g).float() / 4 if exact
+                else torch.randn(n, generator=g) * 0.1)
+
+    return (w(32, 32, 1, s1, 32), b(32), w(16, 16, 3, sm, 144), b(16), w(16, 16, 3, sm, 144),
+            b(16), w(32, 48, 1, s2, 48), b(32))
+
+
+@pytest.mark.parametrize("geom", [
+    # (N, H, W, ldx, x_coff, ldy, y_coff)
+    (2, 160, 160, 32, 0, 32, 0),     # YOLOv8n b2 as the model runs it
+    (3, 80, 80, 48, 8, 64, 16),      # the 80-wide form, channel slices in and out
+    (1, 40, 160, 32, 0, 32, 0),      # one strip per image
+])
+def test_c2f16_fused(geom):
+    """v13 fused C2f(32, 32, n=1, shortcut) (ops.c2f16: cv1 -> 3x3 -> 3x3 + shortcut -> cv2
+    over the concat, one launch) vs the four reference convs with the same bf16
+    intermediates.  The output is NaN-poisoned first: a pixel or channel the kernel skips
+    fails, and channels outside the written slice must stay NaN."""
+    N, H, W, ldx, xc, ldy, yc = geom
+    wts = _c2f_weights(H + N)
+    x = _rand((N, H, W, ldx), 7, scale=2.0)
+    ref = ops.c2f16(x, *wts, x_coff=xc)
+    out = torch.full((N, H, W, ldy), float("nan"), dtype=torch.bfloat16, device="cuda")
+    ops.c2f16(x.cuda(), *(t.cuda() for t in wts), out=out, x_coff=xc, y_coff=yc)
+    torch.cuda.synchronize()
+    got = out.cpu().float()
+    inside = got[..., yc:yc + 32]
+    assert not torch.isnan(inside).any()
+    mask = torch.ones(ldy, dtype=torch.bool)
+    mask[yc:yc + 32] = False
+    assert torch.isnan(got[..., mask]).all()
+    _assert_close(inside, ref, ("c2f16", geom))
+
+
+def test_c2f16_fused_exact_small_integers():
+    """Layout check with exactly representable data: any swapped tap, channel, row-ring slot or
+    pixel mapping changes a result by far more than the summation-order noise."""
+    N, H, W = 2, 80, 80
+    wts = _c2f_weights(11, exact=True)
+    g = torch.Generator().manual_seed(3)
+    x = torch.randint(-2, 3, (N, H, W, 32), generator=g).to(torch.bfloat16)
+    ref = ops.c2f16(x, *wts)
+    got = ops.c2f16(x.cuda(), *(t.cuda() for t in wts)).cpu()
+    torch.cuda.synchronize()
+    d = (got.float() - ref.float()).abs()
+    assert d.max().item() <= 2 ** -6 * ref.float().abs().max().item() + 1e-3, d.max()
+    assert (d > 0).float().mean().item() < 0.02
+
+
+def test_c2f16_matches_four_launch_block():
+    """The YOLOv8n b2 block: DC2f's fused launch vs its own four-launch path on the GPU."""
+    from kvedge_amd.models.yolov8 import DC2f, C2f
+    torch.manual_seed(0)
+    blk = DC2f(C2f(32, 32, 1, True).eval(), "cuda")
+    x = _rand((2, 160, 160, 32), 9).cuda()
+    assert blk.fused_ok(x)
+    fused = blk(x)
+    old = ops.C2F_ENABLED
+    ops.C2F_ENABLED = False
+    try:
+        four = blk(x)
+    finally:
+        ops.C2F_ENABLED = old
+    torch.cuda.synchronize()
+    _assert_close(fused.cpu(), four.cpu(), "c2f16 vs four launches")

@@ -144,3 +144,18 @@ def test_mfma_frag_major_layout():
                 r, h = lane % 32, lane // 32
                 want = w[32 * cs + r, 16 * ks + 8 * h:16 * ks + 8 * h + 8]
                 assert torch.equal(f[cs, ks, lane], want)
+
+
+def test_c2f16_reference_matches_block():
+    """ops.c2f16's CPU reference is the DC2f four-conv path (same bf16 intermediates)."""
+    import torch
+    from kvedge_amd import ops
+    from kvedge_amd.models.yolov8 import C2f, DC2f
+    torch.manual_seed(1)
+    blk = DC2f(C2f(32, 32, 1, True).eval(), "cpu")
+    x = (torch.randn(1, 8, 16, 40) * 2).to(torch.bfloat16)
+    four = blk(x, x_coff=8)
+    b1, b2, _ = blk.m[0]
+    one = ops.c2f16(x, blk.cv1.w, blk.cv1.b, b1.w, b1.b, b2.w, b2.b, blk.cv2.w, blk.cv2.b,
+                    x_coff=8)
+    assert torch.equal(four, one)
