@@ -17,7 +17,7 @@ import torch
 
 from .. import ops
 
-_OPS = ("conv2d", "conv_dual", "conv_tail", "conv_pair", "bottleneck_fused", "stem_pool", "stem_pool_frames", "stem_from_frames", "maxpool2d", "sppf_pool", "global_avgpool",
+_OPS = ("conv2d", "conv_dual", "conv_tail", "conv_pair", "bottleneck_fused", "c2f16", "stem_pool", "stem_pool_frames", "stem_from_frames", "maxpool2d", "sppf_pool", "global_avgpool",
         "softmax_rows", "upsample2x", "yolo_decode", "nms", "synth_frames", "preprocess",
         "batchnorm_nhwc")
 

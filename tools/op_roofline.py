@@ -122,6 +122,15 @@ def bneck_cost(x, w1, b1, w2, b2, w3, b3, out=None):
             2.0 * m * 17 * C * C, None)
 
 
+def c2f16_cost(x, w1, b1, wm1, bm1, wm2, bm2, w2, b2, out=None, x_coff=0, y_coff=0, S=0):
+    N, H, W, _ = x.shape
+    m = N * H * W
+    wb = _b(w1) + _b(wm1) + _b(wm2) + _b(w2)
+    # x (32 channels) read once, y (32) written once; MACs 32*32 + 2*144*16 + 48*32 per pixel
+    return (f"c2f fused 32>[16|16+3x3x2]>32 @{H}x{W}", m * 64 * 2 + wb,
+            2.0 * m * (1024 + 2 * 2304 + 1536), None)
+
+
 def sppf_cost(buf, C):
     return f"sppf pools c{C}", _b(buf, C) * 4, 0.0, None
 
@@ -150,7 +159,7 @@ def softmax_cost(x, out=None, argmax=None):
 
 
 COSTS = {"conv2d": conv2d_cost, "conv_dual": conv_dual_cost, "conv_tail": conv_tail_cost,
-         "conv_pair": conv_pair_cost, "bottleneck_fused": bneck_cost,
+         "conv_pair": conv_pair_cost, "bottleneck_fused": bneck_cost, "c2f16": c2f16_cost,
          "stem_from_frames": stem_from_frames_cost, "stem12_pool_frames": stem12_cost,
          "yolo_stem2": yolo_stem2_cost,
          "sppf_pool": sppf_cost, "upsample2x": upsample_cost, "yolo_decode": decode_cost,
