@@ -12,9 +12,10 @@
 // step against ~0.3 ms of compulsory traffic (x read, y written: 64 channels per pixel).
 // Here x is read once and y written once; t / u stay in LDS rings.
 //
-// Decomposition: a workgroup sweeps a strip of S output rows of one image top to bottom, one
-// row per iteration, with row rings in LDS (s: 5 rows, u: 3 rows, a: 4 rows; zero columns
-// either side for the 3x3 padding, zero rows outside the image):
+// Decomposition: a workgroup (W / 16 waves, one 16-pixel block each) sweeps a strip of S
+// output rows of one image top to bottom, one row per iteration, with row rings in LDS (s: 5
+// rows, u: 3 rows, a: 4 rows; zero columns either side for the 3x3 padding, zero rows
+// outside the image):
 //   A(o + 2): t of row o + 2 from x (prefetched PF rows ahead into registers)
 //   barrier
 //   B(o + 1): u of row o + 1 from s rows o .. o + 2
@@ -32,13 +33,14 @@
 // holds v channels 4q .. 4q + 3, so cv2's second K step takes them as k = 8q .. 8q + 3 with
 // zeros in k = 8q + 4 .. 8q + 7, and the weights are read in that permuted order -- v never
 // goes through LDS.
+#include <stdlib.h>
+
 #include "common.h"
 #include "kvedge_kernels.h"
 
 namespace kvedge {
 namespace {
 
-constexpr int kC2fWaves = 5;  // 160 = 5 waves x 2 blocks of 16 pixels, 80 = 5 x 1
 constexpr int kC2fPF = 2;     // x rows in flight ahead of step A (VGPR budget: 3 waves per SIMD)
 constexpr int kC2fRS = 5, kC2fRU = 3, kC2fRA = 4;
 typedef unsigned int c2f_u32x4 __attribute__((ext_vector_type(4)));
@@ -58,14 +60,17 @@ __device__ __forceinline__ bf16x4 c2f_silu4(floatx4 acc, floatx4 b) {
   return o;
 }
 
-template <int BPW>
-__global__ __launch_bounds__(kC2fWaves * 64, 3) void c2f16_kernel(const KvC2fParams p) {
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams p, int diag) {
+  constexpr int BPW = 1;  // one 16-pixel block per wave: W = 16 x WAVES
   extern __shared__ __attribute__((aligned(16))) char c2f_lds[];
-  constexpr int W = 16 * kC2fWaves * BPW;
+  constexpr int W = 16 * WAVES;
   constexpr int WP = W + 2;  // one zero column either side
   bf16* const sring = reinterpret_cast<bf16*>(c2f_lds);  // [RS][WP][16]
   bf16* const uring = sring + kC2fRS * WP * 16;          // [RU][WP][16]
   bf16* const aring = uring + kC2fRU * WP * 16;          // [RA][W][16]
+  // diag bit 8: y staged per wave ([BPW][16 px][32 ch]) and stored as whole 64-B pixels
+  bf16* const ystage = aring + kC2fRA * W * 16;
 
   const int strips = p.H / p.S;
   const int img = blockIdx.x / strips;
@@ -76,7 +81,7 @@ __global__ __launch_bounds__(kC2fWaves * 64, 3) void c2f16_kernel(const KvC2fPar
   const int H = p.H;
 
   // ---- zero the padding columns of the s / u rings (never written by the steps)
-  for (int i = threadIdx.x; i < (kC2fRS + kC2fRU) * 2 * 2; i += kC2fWaves * 64) {
+  for (int i = threadIdx.x; i < (kC2fRS + kC2fRU) * 2 * 2; i += WAVES * 64) {
     const int slot = i >> 2, side = (i >> 1) & 1, half = i & 1;
     bf16* row = slot < kC2fRS ? sring + slot * WP * 16 : uring + (slot - kC2fRS) * WP * 16;
     *reinterpret_cast<c2f_u32x4*>(row + (side ? WP - 1 : 0) * 16 + half * 8) = c2f_u32x4{0, 0, 0, 0};
@@ -113,6 +118,17 @@ __global__ __launch_bounds__(kC2fWaves * 64, 3) void c2f16_kernel(const KvC2fPar
   bm1v = *reinterpret_cast<const floatx4*>(p.bm1 + q * 4);
   bm2v = *reinterpret_cast<const floatx4*>(p.bm2 + q * 4);
 
+  // diag bit 1: identity instead of SiLU (timing only)
+  auto c2f_act4 = [&](floatx4 acc, floatx4 b) __attribute__((always_inline)) -> bf16x4 {
+    if (diag & 1) {
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[e] + b[e]);
+      return o;
+    }
+    return c2f_silu4(acc, b);
+  };
+
   // 3x3 tap of lane quarter q in step j (the tenth tap re-reads tap 8: finite, weight 0)
   int tdy[5], tdx[5];
 #pragma unroll
@@ -126,10 +142,10 @@ __global__ __launch_bounds__(kC2fWaves * 64, 3) void c2f16_kernel(const KvC2fPar
   const __amdgpu_buffer_rsrc_t rx = c2f_rsrc(p.x, (long long)p.N * H * W * p.ldx * 2);
   const __amdgpu_buffer_rsrc_t ry = c2f_rsrc(p.y, (long long)p.N * H * W * p.ldy * 2);
   auto load_x = [&](int r, c2f_u32x4 (&dst)[BPW]) __attribute__((always_inline)) {
-    const bool ok = r >= 0 && r < H && r <= s1 + 1;
+    const bool ok = r >= 0 && r < H && r <= s1 + 1 && !(diag & 2);
 #pragma unroll
     for (int b = 0; b < BPW; ++b) {
-      const int px = (w + kC2fWaves * b) * 16 + r16;
+      const int px = (w + WAVES * b) * 16 + r16;
       const unsigned off =
           ok ? (unsigned)(((img * H + r) * W + px) * p.ldx + p.x_coff + q * 8) * 2u : kC2fOOB;
       dst[b] = __builtin_amdgcn_raw_buffer_load_b128(rx, off, 0, 0);
@@ -146,38 +162,49 @@ __global__ __launch_bounds__(kC2fWaves * 64, 3) void c2f16_kernel(const KvC2fPar
     bf16* arow = aring + slot_a(r) * W * 16;
 #pragma unroll
     for (int b = 0; b < BPW; ++b) {
-      const int px = (w + kC2fWaves * b) * 16 + r16;
+      const int px = (w + WAVES * b) * 16 + r16;
       const bf16x8 xf = __builtin_bit_cast(bf16x8, xr[b]);
       const floatx4 z = {0.f, 0.f, 0.f, 0.f};
       const floatx4 ta = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[0], xf, z, 0, 0, 0);
       const floatx4 ts = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[1], xf, z, 0, 0, 0);
-      bf16x4 sv = c2f_silu4(ts, b1v[1]);
+      bf16x4 sv = c2f_act4(ts, b1v[1]);
       if (!in) sv = bf16x4{0, 0, 0, 0};
-      *reinterpret_cast<bf16x4*>(arow + px * 16 + q * 4) = c2f_silu4(ta, b1v[0]);
+      *reinterpret_cast<bf16x4*>(arow + px * 16 + q * 4) = c2f_act4(ta, b1v[0]);
       *reinterpret_cast<bf16x4*>(srow + (px + 1) * 16 + q * 4) = sv;
     }
   };
   // 3x3 16 -> 16 over three rows of a ring (rows r - 1 .. r + 1 at slots sl[0..2])
-  auto conv3 = [&](const bf16* ring, const int (&sl)[3], const bf16x8 (&wf)[5], int px)
-      __attribute__((always_inline)) -> floatx4 {
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  // 3x3 16 -> 16: the five fragment reads of a block (rows r - 1 .. r + 1 of a ring at slots
+  // sl[0..2]) are issued for every block of the wave before the first MFMA (hipcc otherwise
+  // serialises read -> wait -> MFMA per tap: ~5 LDS round trips per block and step)
+  auto frags3 = [&](const bf16* ring, const int (&sl)[3], int px, bf16x8 (&fr)[5])
+      __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const bf16* src = ring + (sl[tdy[j]] * WP + px + tdx[j]) * 16 + (q & 1) * 8;
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], *reinterpret_cast<const bf16x8*>(src),
-                                                    acc, 0, 0, 0);
-    }
-    return acc;
+    for (int j = 0; j < 5; ++j)
+      fr[j] = *reinterpret_cast<const bf16x8*>(ring + (sl[tdy[j]] * WP + px + tdx[j]) * 16 +
+                                               (q & 1) * 8);
   };
   // step B: u of row r from s rows r - 1 .. r + 1 (zero outside the image)
   auto stepB = [&](int r) __attribute__((always_inline)) {
     const bool in = r >= 0 && r < H;
     const int sl[3] = {slot_s(r - 1), slot_s(r), slot_s(r + 1)};
     bf16* urow = uring + slot_u(r) * WP * 16;
+    bf16x8 fr[BPW][5];
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) frags3(sring, sl, (w + WAVES * b) * 16 + r16, fr[b]);
+    __builtin_amdgcn_sched_barrier(0);
+    floatx4 acc[BPW];
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) acc[b] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+#pragma unroll
+      for (int b = 0; b < BPW; ++b)  // independent chains, interleaved
+        acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm1f[j], fr[b][j], acc[b], 0, 0, 0);
 #pragma unroll
     for (int b = 0; b < BPW; ++b) {
-      const int px = (w + kC2fWaves * b) * 16 + r16;
-      bf16x4 uv = c2f_silu4(conv3(sring, sl, wm1f, px), bm1v);
+      const int px = (w + WAVES * b) * 16 + r16;
+      bf16x4 uv = c2f_act4(acc[b], bm1v);
       if (!in) uv = bf16x4{0, 0, 0, 0};
       *reinterpret_cast<bf16x4*>(urow + (px + 1) * 16 + q * 4) = uv;
     }
@@ -187,30 +214,63 @@ __global__ __launch_bounds__(kC2fWaves * 64, 3) void c2f16_kernel(const KvC2fPar
     const int sl[3] = {slot_u(o - 1), slot_u(o), slot_u(o + 1)};
     const bf16* srow = sring + slot_s(o) * WP * 16;
     const bf16* arow = aring + slot_a(o) * W * 16;
+    bf16x8 fr[BPW][5], as[BPW];
+    bf16x4 sres[BPW];
 #pragma unroll
     for (int b = 0; b < BPW; ++b) {
-      const int px = (w + kC2fWaves * b) * 16 + r16;
-      const floatx4 m = conv3(uring, sl, wm2f, px);
-      const bf16x4 sres = *reinterpret_cast<const bf16x4*>(srow + (px + 1) * 16 + q * 4);
+      const int px = (w + WAVES * b) * 16 + r16;
+      frags3(uring, sl, px, fr[b]);
+      sres[b] = *reinterpret_cast<const bf16x4*>(srow + (px + 1) * 16 + q * 4);
+      // cv2's first K step: [a | s] channels 8q .. 8q + 7 of the concat
+      as[b] = q < 2 ? *reinterpret_cast<const bf16x8*>(arow + px * 16 + q * 8)
+                    : *reinterpret_cast<const bf16x8*>(srow + (px + 1) * 16 + (q - 2) * 8);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    floatx4 m[BPW];
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) m[b] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+#pragma unroll
+      for (int b = 0; b < BPW; ++b)
+        m[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm2f[j], fr[b][j], m[b], 0, 0, 0);
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) {
+      const int px = (w + WAVES * b) * 16 + r16;
       bf16x8 vf;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         // rounded to bf16 before and after the shortcut add, as the four-launch path does
-        vf[e] = f2bf((float)f2bf(act_c<kActSilu>(m[e] + bm2v[e])) + (float)sres[e]);
+        const float mv = (diag & 1) ? m[b][e] + bm2v[e] : act_c<kActSilu>(m[b][e] + bm2v[e]);
+        vf[e] = f2bf((float)f2bf(mv) + (float)sres[b][e]);
         vf[4 + e] = (bf16)0.f;
       }
-      // cv2's first K step: [a | s] channels 8q .. 8q + 7 of the concat
-      const bf16x8 as = q < 2 ? *reinterpret_cast<const bf16x8*>(arow + px * 16 + q * 8)
-                              : *reinterpret_cast<const bf16x8*>(srow + (px + 1) * 16 + (q - 2) * 8);
       const size_t ybase = ((size_t)(img * H + o) * W + px) * p.ldy + p.y_coff;
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f0[nb], as, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f0[nb], as[b], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f1[nb], vf, acc, 0, 0, 0);
-        const bf16x4 yv = c2f_silu4(acc, b2v[nb]);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(c2f_u32x2, yv), ry,
-                                              (unsigned)(ybase + nb * 16 + q * 4) * 2u, 0, 0);
+        const bf16x4 yv = c2f_act4(acc, b2v[nb]);
+        if (diag & 8) {
+          *reinterpret_cast<bf16x4*>(ystage + ((w * BPW + b) * 16 + r16) * 32 + nb * 16 + q * 4) = yv;
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b64(
+              __builtin_bit_cast(c2f_u32x2, yv), ry,
+              (diag & 4) ? kC2fOOB : (unsigned)(ybase + nb * 16 + q * 4) * 2u, 0, 0);
+        }
+      }
+    }
+    if (diag & 8) {  // lane-linear re-read of the wave's staged pixels: 1 KB per store
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int b = 0; b < BPW; ++b) {
+        const int px = (w + WAVES * b) * 16 + (lane >> 2);
+        const c2f_u32x4 v =
+            *reinterpret_cast<const c2f_u32x4*>(ystage + (w * BPW + b) * 512 + lane * 8);
+        const size_t yoff = ((size_t)(img * H + o) * W + px) * p.ldy + p.y_coff + (lane & 3) * 8;
+        __builtin_amdgcn_raw_buffer_store_b128(v, ry, (diag & 4) ? kC2fOOB : (unsigned)yoff * 2u,
+                                               0, 0);
       }
     }
   };
@@ -246,7 +306,14 @@ __global__ __launch_bounds__(kC2fWaves * 64, 3) void c2f16_kernel(const KvC2fPar
 }  // namespace
 
 int c2f16_lds_bytes(int W) {
-  return ((kC2fRS + kC2fRU) * (W + 2) + kC2fRA * W) * 16 * 2;
+  return ((kC2fRS + kC2fRU) * (W + 2) + kC2fRA * W) * 16 * 2 + W * 32 * 2;  // + y staging
+}
+
+// KVEDGE_C2F_DIAG (timing experiments, tools/c2f_probe.py): 1 identity activations, 2 no x
+// loads, 4 no y stores, 8 y staged through LDS and stored as whole pixels
+int c2f_diag() {
+  const char* e = getenv("KVEDGE_C2F_DIAG");
+  return e ? atoi(e) : 0;
 }
 
 }  // namespace kvedge
@@ -263,15 +330,17 @@ extern "C" int kv_c2f16_fused(const KvC2fParams* p, hipStream_t stream) {
       p->ldw2 < 48 || p->ldwm < 144)
     return -3;
   const int lds = c2f16_lds_bytes(p->W);
+  int diag = c2f_diag();
+  if ((p->ldy % 8) || (p->y_coff % 8)) diag &= ~8;  // whole-pixel stores need 16-B alignment
   const unsigned grid = (unsigned)(p->N * (p->H / p->S));
   if (grid == 0) return 0;
-  const void* fn = p->W == 160 ? reinterpret_cast<const void*>(&c2f16_kernel<2>)
-                               : reinterpret_cast<const void*>(&c2f16_kernel<1>);
+  const void* fn = p->W == 160 ? reinterpret_cast<const void*>(&c2f16_kernel<10>)
+                               : reinterpret_cast<const void*>(&c2f16_kernel<5>);
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
     return -7;
   if (p->W == 160)
-    hipLaunchKernelGGL(c2f16_kernel<2>, dim3(grid), dim3(kC2fWaves * 64), (unsigned)lds, stream, *p);
+    hipLaunchKernelGGL(c2f16_kernel<10>, dim3(grid), dim3(10 * 64), (unsigned)lds, stream, *p, diag);
   else
-    hipLaunchKernelGGL(c2f16_kernel<1>, dim3(grid), dim3(kC2fWaves * 64), (unsigned)lds, stream, *p);
+    hipLaunchKernelGGL(c2f16_kernel<5>, dim3(grid), dim3(5 * 64), (unsigned)lds, stream, *p, diag);
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }

@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--hw", type=int, default=160)
     ap.add_argument("--strips", default="40,20,8")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--diags", default="", help="KVEDGE_C2F_DIAG values to time at the first S "
+                    "(1 identity act, 2 no x loads, 4 no y stores, 8 y via LDS staging)")
     a = ap.parse_args()
     import torch
     from kvedge_amd import ops
@@ -52,6 +54,13 @@ def main():
         us = timeit(lambda: ops.c2f16(x, blk.cv1.w, blk.cv1.b, b1.w, b1.b, b2.w, b2.b,
                                       blk.cv2.w, blk.cv2.b, out=y, S=S))
         print(f"  fused S={S}: {us:.1f} us  {byts / us / 1e3:.0f} GB/s", flush=True)
+    S0 = int(a.strips.split(",")[0])
+    for d in [int(v) for v in a.diags.split(",") if v]:
+        os.environ["KVEDGE_C2F_DIAG"] = str(d)
+        us = timeit(lambda: ops.c2f16(x, blk.cv1.w, blk.cv1.b, b1.w, b1.b, b2.w, b2.b,
+                                      blk.cv2.w, blk.cv2.b, out=y, S=S0))
+        print(f"  fused S={S0} diag={d}: {us:.1f} us", flush=True)
+    os.environ.pop("KVEDGE_C2F_DIAG", None)
     ops.C2F_ENABLED = False
     us = timeit(lambda: blk(x, out=y))
     print(f"  four launches: {us:.1f} us", flush=True)
