@@ -13,17 +13,20 @@
 // Here x is read once and y written once; t / u stay in LDS rings.
 //
 // Decomposition: a workgroup (W / 16 waves, one 16-pixel block each) sweeps a strip of S
-// output rows of one image top to bottom, one row per iteration, with row rings in LDS (s: 5
-// rows, u: 3 rows, a: 4 rows; zero columns either side for the 3x3 padding, zero rows
-// outside the image):
-//   A(o + 2): t of row o + 2 from x (prefetched PF rows ahead into registers)
+// output rows of one image top to bottom, two rows per iteration, with row rings in LDS (s and
+// a: 6 rows, u: 4 rows; zero columns either side for the 3x3 padding, zero rows outside the
+// image):
+//   phase 1: u of rows o + 1, o + 2 from s rows o .. o + 3
 //   barrier
-//   B(o + 1): u of row o + 1 from s rows o .. o + 2
+//   phase 2: t of rows o + 4, o + 5 from x (in registers, loaded an iteration ahead);
+//            v from u rows o - 1 .. o + 2 and s; y of rows o, o + 1 from a, s and v
 //   barrier
-//   C(o):     v from u rows o - 1 .. o + 1 and s row o; y from a, s (LDS) and v (registers)
-// Two barriers per row suffice: every slot a step overwrites was last read two steps and at
-// least one barrier earlier (ring sizes chosen for that).  The strip's first rows repeat two
-// rows of t and one of u of the strip above (halo).
+// One barrier per row: every slot a phase writes was last read in the other phase of the
+// previous iteration.  In each phase a wave has two rows' independent MFMA chains, and their
+// LDS fragment reads are all issued first.  The strip's first rows repeat two rows of t and
+// one of u of the strip above (halo).  (The first form ran one row per iteration with three
+// steps and two barriers per row: 469 us at b256 vs 441 us with the reads hoisted;
+// profiles/r5_v10_c2f_probe.md, r5_v11_c2f_probe_wave_per_block.txt.)
 //
 // MFMA: v_mfma_f32_16x16x32_bf16, weights as the first operand (D = W . X^T: a lane's four
 // accumulators are four consecutive output channels of one pixel).  The 3x3s run K = 9 taps
@@ -41,8 +44,7 @@
 namespace kvedge {
 namespace {
 
-constexpr int kC2fPF = 2;     // x rows in flight ahead of step A (VGPR budget: 3 waves per SIMD)
-constexpr int kC2fRS = 5, kC2fRU = 3, kC2fRA = 4;
+constexpr int kC2fRS = 6, kC2fRU = 4, kC2fRA = 6;  // two rows per iteration (below)
 typedef unsigned int c2f_u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int c2f_u32x2 __attribute__((ext_vector_type(2)));
 constexpr unsigned kC2fOOB = 0x80000000u;
@@ -69,8 +71,6 @@ __global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams 
   bf16* const sring = reinterpret_cast<bf16*>(c2f_lds);  // [RS][WP][16]
   bf16* const uring = sring + kC2fRS * WP * 16;          // [RU][WP][16]
   bf16* const aring = uring + kC2fRU * WP * 16;          // [RA][W][16]
-  // diag bit 8: y staged per wave ([BPW][16 px][32 ch]) and stored as whole 64-B pixels
-  bf16* const ystage = aring + kC2fRA * W * 16;
 
   const int strips = p.H / p.S;
   const int img = blockIdx.x / strips;
@@ -93,7 +93,13 @@ __global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams 
   const __amdgpu_buffer_rsrc_t rwm2 = c2f_rsrc(p.wm2, 16LL * p.ldwm * 2);
   const __amdgpu_buffer_rsrc_t rw2 = c2f_rsrc(p.w2, 32LL * p.ldw2 * 2);
   bf16x8 w1f[2], wm1f[5], wm2f[5], w2f0[2], w2f1[2];
-  floatx4 b1v[2], b2v[2], bm1v, bm2v;
+  // biases live in LDS (96 floats; registers are the limit: 3 waves per SIMD)
+  float* const bias_lds = reinterpret_cast<float*>(aring + kC2fRA * W * 16);  // b1 | bm1 | bm2 | b2
+  for (int i = threadIdx.x; i < 96; i += WAVES * 64)
+    bias_lds[i] = i < 32 ? p.b1[i] : i < 48 ? p.bm1[i - 32] : i < 64 ? p.bm2[i - 48] : p.b2[i - 64];
+  auto bias4 = [&](int off) __attribute__((always_inline)) -> floatx4 {
+    return *reinterpret_cast<const floatx4*>(bias_lds + off + q * 4);
+  };
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb) {
     const int row = nb * 16 + r16;
@@ -105,8 +111,6 @@ __global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams 
     const c2f_u32x2 lo = __builtin_amdgcn_raw_buffer_load_b64(
         rw2, (unsigned)(row * p.ldw2 + 32 + q * 4) * 2u, 0, 0);
     w2f1[nb] = __builtin_bit_cast(bf16x8, c2f_u32x4{lo[0], lo[1], 0u, 0u});
-    b1v[nb] = *reinterpret_cast<const floatx4*>(p.b1 + nb * 16 + q * 4);
-    b2v[nb] = *reinterpret_cast<const floatx4*>(p.b2 + nb * 16 + q * 4);
   }
 #pragma unroll
   for (int j = 0; j < 5; ++j) {
@@ -115,8 +119,6 @@ __global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams 
     wm1f[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rwm1, off, 0, 0));
     wm2f[j] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rwm2, off, 0, 0));
   }
-  bm1v = *reinterpret_cast<const floatx4*>(p.bm1 + q * 4);
-  bm2v = *reinterpret_cast<const floatx4*>(p.bm2 + q * 4);
 
   // diag bit 1: identity instead of SiLU (timing only)
   auto c2f_act4 = [&](floatx4 acc, floatx4 b) __attribute__((always_inline)) -> bf16x4 {
@@ -142,7 +144,7 @@ __global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams 
   const __amdgpu_buffer_rsrc_t rx = c2f_rsrc(p.x, (long long)p.N * H * W * p.ldx * 2);
   const __amdgpu_buffer_rsrc_t ry = c2f_rsrc(p.y, (long long)p.N * H * W * p.ldy * 2);
   auto load_x = [&](int r, c2f_u32x4 (&dst)[BPW]) __attribute__((always_inline)) {
-    const bool ok = r >= 0 && r < H && r <= s1 + 1 && !(diag & 2);
+    const bool ok = r >= 0 && r < H && r <= s1 + 3 && !(diag & 2);
 #pragma unroll
     for (int b = 0; b < BPW; ++b) {
       const int px = (w + WAVES * b) * 16 + r16;
@@ -167,9 +169,9 @@ __global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams 
       const floatx4 z = {0.f, 0.f, 0.f, 0.f};
       const floatx4 ta = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[0], xf, z, 0, 0, 0);
       const floatx4 ts = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[1], xf, z, 0, 0, 0);
-      bf16x4 sv = c2f_act4(ts, b1v[1]);
+      bf16x4 sv = c2f_act4(ts, bias4(16));
       if (!in) sv = bf16x4{0, 0, 0, 0};
-      *reinterpret_cast<bf16x4*>(arow + px * 16 + q * 4) = c2f_act4(ta, b1v[0]);
+      *reinterpret_cast<bf16x4*>(arow + px * 16 + q * 4) = c2f_act4(ta, bias4(0));
       *reinterpret_cast<bf16x4*>(srow + (px + 1) * 16 + q * 4) = sv;
     }
   };
@@ -184,121 +186,113 @@ __global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams 
       fr[j] = *reinterpret_cast<const bf16x8*>(ring + (sl[tdy[j]] * WP + px + tdx[j]) * 16 +
                                                (q & 1) * 8);
   };
-  // step B: u of row r from s rows r - 1 .. r + 1 (zero outside the image)
+  // step B: u of rows r, r + 1 from s rows r - 1 .. r + 2 (zero outside the image); the two
+  // rows' fragment reads go first, then their MFMA chains interleaved
   auto stepB = [&](int r) __attribute__((always_inline)) {
-    const bool in = r >= 0 && r < H;
-    const int sl[3] = {slot_s(r - 1), slot_s(r), slot_s(r + 1)};
-    bf16* urow = uring + slot_u(r) * WP * 16;
-    bf16x8 fr[BPW][5];
+    const int px = w * 16 + r16;
+    bf16x8 fr[2][5];
 #pragma unroll
-    for (int b = 0; b < BPW; ++b) frags3(sring, sl, (w + WAVES * b) * 16 + r16, fr[b]);
+    for (int i = 0; i < 2; ++i) {
+      const int sl[3] = {slot_s(r + i - 1), slot_s(r + i), slot_s(r + i + 1)};
+      frags3(sring, sl, px, fr[i]);
+    }
     __builtin_amdgcn_sched_barrier(0);
-    floatx4 acc[BPW];
-#pragma unroll
-    for (int b = 0; b < BPW; ++b) acc[b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    floatx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int j = 0; j < 5; ++j)
 #pragma unroll
-      for (int b = 0; b < BPW; ++b)  // independent chains, interleaved
-        acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm1f[j], fr[b][j], acc[b], 0, 0, 0);
+      for (int i = 0; i < 2; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm1f[j], fr[i][j], acc[i], 0, 0, 0);
 #pragma unroll
-    for (int b = 0; b < BPW; ++b) {
-      const int px = (w + WAVES * b) * 16 + r16;
-      bf16x4 uv = c2f_act4(acc[b], bm1v);
+    for (int i = 0; i < 2; ++i) {
+      const bool in = r + i >= 0 && r + i < H;
+      bf16x4 uv = c2f_act4(acc[i], bias4(32));
       if (!in) uv = bf16x4{0, 0, 0, 0};
-      *reinterpret_cast<bf16x4*>(urow + (px + 1) * 16 + q * 4) = uv;
+      *reinterpret_cast<bf16x4*>(uring + slot_u(r + i) * WP * 16 + (px + 1) * 16 + q * 4) = uv;
     }
   };
-  // step C: v and y of output row o
+  // step C: v and y of output rows o, o + 1
   auto stepC = [&](int o) __attribute__((always_inline)) {
-    const int sl[3] = {slot_u(o - 1), slot_u(o), slot_u(o + 1)};
-    const bf16* srow = sring + slot_s(o) * WP * 16;
-    const bf16* arow = aring + slot_a(o) * W * 16;
-    bf16x8 fr[BPW][5], as[BPW];
-    bf16x4 sres[BPW];
+    const int px = w * 16 + r16;
+    bf16x8 fr[2][5], as[2];
+    bf16x4 sres[2];
 #pragma unroll
-    for (int b = 0; b < BPW; ++b) {
-      const int px = (w + WAVES * b) * 16 + r16;
-      frags3(uring, sl, px, fr[b]);
-      sres[b] = *reinterpret_cast<const bf16x4*>(srow + (px + 1) * 16 + q * 4);
+    for (int i = 0; i < 2; ++i) {
+      const int sl[3] = {slot_u(o + i - 1), slot_u(o + i), slot_u(o + i + 1)};
+      const bf16* srow = sring + slot_s(o + i) * WP * 16;
+      const bf16* arow = aring + slot_a(o + i) * W * 16;
+      frags3(uring, sl, px, fr[i]);
+      sres[i] = *reinterpret_cast<const bf16x4*>(srow + (px + 1) * 16 + q * 4);
       // cv2's first K step: [a | s] channels 8q .. 8q + 7 of the concat
-      as[b] = q < 2 ? *reinterpret_cast<const bf16x8*>(arow + px * 16 + q * 8)
+      as[i] = q < 2 ? *reinterpret_cast<const bf16x8*>(arow + px * 16 + q * 8)
                     : *reinterpret_cast<const bf16x8*>(srow + (px + 1) * 16 + (q - 2) * 8);
     }
     __builtin_amdgcn_sched_barrier(0);
-    floatx4 m[BPW];
-#pragma unroll
-    for (int b = 0; b < BPW; ++b) m[b] = floatx4{0.f, 0.f, 0.f, 0.f};
+    floatx4 m[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int j = 0; j < 5; ++j)
 #pragma unroll
-      for (int b = 0; b < BPW; ++b)
-        m[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm2f[j], fr[b][j], m[b], 0, 0, 0);
+      for (int i = 0; i < 2; ++i)
+        m[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm2f[j], fr[i][j], m[i], 0, 0, 0);
+    const floatx4 bm2 = bias4(48);
 #pragma unroll
-    for (int b = 0; b < BPW; ++b) {
-      const int px = (w + WAVES * b) * 16 + r16;
+    for (int i = 0; i < 2; ++i) {
       bf16x8 vf;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         // rounded to bf16 before and after the shortcut add, as the four-launch path does
-        const float mv = (diag & 1) ? m[b][e] + bm2v[e] : act_c<kActSilu>(m[b][e] + bm2v[e]);
-        vf[e] = f2bf((float)f2bf(mv) + (float)sres[b][e]);
+        const float mv = (diag & 1) ? m[i][e] + bm2[e] : act_c<kActSilu>(m[i][e] + bm2[e]);
+        vf[e] = f2bf((float)f2bf(mv) + (float)sres[i][e]);
         vf[4 + e] = (bf16)0.f;
       }
-      const size_t ybase = ((size_t)(img * H + o) * W + px) * p.ldy + p.y_coff;
+      const size_t ybase = ((size_t)(img * H + o + i) * W + px) * p.ldy + p.y_coff;
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f0[nb], as[b], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f0[nb], as[i], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f1[nb], vf, acc, 0, 0, 0);
-        const bf16x4 yv = c2f_act4(acc, b2v[nb]);
-        if (diag & 8) {
-          *reinterpret_cast<bf16x4*>(ystage + ((w * BPW + b) * 16 + r16) * 32 + nb * 16 + q * 4) = yv;
-        } else {
-          __builtin_amdgcn_raw_buffer_store_b64(
-              __builtin_bit_cast(c2f_u32x2, yv), ry,
-              (diag & 4) ? kC2fOOB : (unsigned)(ybase + nb * 16 + q * 4) * 2u, 0, 0);
-        }
-      }
-    }
-    if (diag & 8) {  // lane-linear re-read of the wave's staged pixels: 1 KB per store
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int b = 0; b < BPW; ++b) {
-        const int px = (w + WAVES * b) * 16 + (lane >> 2);
-        const c2f_u32x4 v =
-            *reinterpret_cast<const c2f_u32x4*>(ystage + (w * BPW + b) * 512 + lane * 8);
-        const size_t yoff = ((size_t)(img * H + o) * W + px) * p.ldy + p.y_coff + (lane & 3) * 8;
-        __builtin_amdgcn_raw_buffer_store_b128(v, ry, (diag & 4) ? kC2fOOB : (unsigned)yoff * 2u,
-                                               0, 0);
+        const bf16x4 yv = c2f_act4(acc, bias4(64 + nb * 16));
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(c2f_u32x2, yv), ry,
+            (diag & 4) ? kC2fOOB : (unsigned)(ybase + nb * 16 + q * 4) * 2u, 0, 0);
       }
     }
   };
 
-  // ---- prologue: t of rows s0 - 2 .. s0 + 1, u of rows s0 - 1, s0
+  __syncthreads();  // biases and the zero columns are in LDS
+  // ---- prologue: t of rows s0 - 2 .. s0 + 3, u of rows s0 - 1, s0
   {
-    c2f_u32x4 xp[4][BPW];
+    c2f_u32x4 xp[6][BPW];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) load_x(s0 - 2 + i, xp[i]);
+    for (int i = 0; i < 6; ++i) load_x(s0 - 2 + i, xp[i]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) stepA(s0 - 2 + i, xp[i]);
+    for (int i = 0; i < 6; ++i) stepA(s0 - 2 + i, xp[i]);
   }
-  c2f_u32x4 xr[kC2fPF][BPW];  // x of rows o + 2 .. o + 2 + PF - 1
+  c2f_u32x4 xr[2][2][BPW];  // x of rows o + 4, o + 5 for this and the next iteration
 #pragma unroll
-  for (int i = 0; i < kC2fPF; ++i) load_x(s0 + 2 + i, xr[i]);
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) load_x(s0 + 4 + 2 * k + i, xr[k][i]);
   __syncthreads();
   stepB(s0 - 1);
-  stepB(s0);
-  // ---- sweep: S is a multiple of PF, so the register ring index is static
-  for (int o = s0; o < s1; o += kC2fPF) {
-    static_range<0, kC2fPF>([&](auto kc) {
+  // ---- sweep, two output rows per iteration and one barrier per row:
+  //   phase 1: u of rows o + 1, o + 2          (s rows o .. o + 3 are in the ring)
+  //   phase 2: t of rows o + 4, o + 5; v and y of rows o, o + 1
+  // Every slot a phase writes was last read in the other phase of the previous iteration
+  // (ring sizes: s 6, a 6, u 4).  S is a multiple of 4, so the x register ring is static.
+  for (int o = s0; o < s1; o += 4) {
+    static_range<0, 2>([&](auto kc) {
       constexpr int k = decltype(kc)::value;
-      stepA(o + k + 2, xr[k]);
-      load_x(o + k + 2 + kC2fPF, xr[k]);
+      const int oo = o + 2 * k;
+      stepB(oo + 1);
       __syncthreads();
-      stepB(o + k + 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        stepA(oo + 4 + i, xr[k][i]);
+        load_x(oo + 8 + i, xr[k][i]);
+      }
+      stepC(oo);
       __syncthreads();
-      stepC(o + k);
     });
   }
 }
@@ -306,11 +300,12 @@ __global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams 
 }  // namespace
 
 int c2f16_lds_bytes(int W) {
-  return ((kC2fRS + kC2fRU) * (W + 2) + kC2fRA * W) * 16 * 2 + W * 32 * 2;  // + y staging
+  return ((kC2fRS + kC2fRU) * (W + 2) + kC2fRA * W) * 16 * 2 + 96 * 4;  // + biases
 }
 
 // KVEDGE_C2F_DIAG (timing experiments, tools/c2f_probe.py): 1 identity activations, 2 no x
-// loads, 4 no y stores, 8 y staged through LDS and stored as whole pixels
+// loads, 4 no y stores (bit 8, y staged through LDS for whole-pixel stores, measured slower:
+// profiles/r5_v10_c2f_probe.md, removed)
 int c2f_diag() {
   const char* e = getenv("KVEDGE_C2F_DIAG");
   return e ? atoi(e) : 0;
@@ -321,7 +316,7 @@ int c2f_diag() {
 using namespace kvedge;
 
 extern "C" int kv_c2f16_supported(int H, int W, int S) {
-  return (W == 160 || W == 80) && S > 0 && S % kC2fPF == 0 && H % S == 0;
+  return (W == 160 || W == 80) && S > 0 && S % 4 == 0 && H % S == 0;
 }
 
 extern "C" int kv_c2f16_fused(const KvC2fParams* p, hipStream_t stream) {
@@ -330,8 +325,7 @@ extern "C" int kv_c2f16_fused(const KvC2fParams* p, hipStream_t stream) {
       p->ldw2 < 48 || p->ldwm < 144)
     return -3;
   const int lds = c2f16_lds_bytes(p->W);
-  int diag = c2f_diag();
-  if ((p->ldy % 8) || (p->y_coff % 8)) diag &= ~8;  // whole-pixel stores need 16-B alignment
+  const int diag = c2f_diag();
   const unsigned grid = (unsigned)(p->N * (p->H / p->S));
   if (grid == 0) return 0;
   const void* fn = p->W == 160 ? reinterpret_cast<const void*>(&c2f16_kernel<10>)
