@@ -55,10 +55,28 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t c2f_rsrc(const void* base, lon
                                            0x00020000);
 }
 
-__device__ __forceinline__ bf16x4 c2f_silu4(floatx4 acc, floatx4 b) {
+// SiLU of four accumulators (the bias is already in them: the MFMA chains start from it),
+// two at a time in packed fp32 (v_pk_mul / v_pk_add): per element one exp and one rcp plus
+// 1.5 packed ops.  The kernel is VALU-issue-bound (profiles/r5_v12_c2f_probe_two_rows.txt)
+typedef float c2f_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ floatx4 c2f_silu4f(floatx4 v) {
+  floatx4 o;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const c2f_f2 x = {v[2 * h], v[2 * h + 1]};
+    const c2f_f2 t = x * c2f_f2{-1.4426950408889634f, -1.4426950408889634f};
+    c2f_f2 d = {__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])};
+    d = d + c2f_f2{1.f, 1.f};
+    const c2f_f2 y = x * c2f_f2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+    o[2 * h] = y[0];
+    o[2 * h + 1] = y[1];
+  }
+  return o;
+}
+__device__ __forceinline__ bf16x4 c2f_pack4(floatx4 v) {
   bf16x4 o;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) o[e] = f2bf(act_c<kActSilu>(acc[e] + b[e]));
+  for (int e = 0; e < 4; ++e) o[e] = f2bf(v[e]);
   return o;
 }
 
@@ -121,14 +139,9 @@ __global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams 
   }
 
   // diag bit 1: identity instead of SiLU (timing only)
-  auto c2f_act4 = [&](floatx4 acc, floatx4 b) __attribute__((always_inline)) -> bf16x4 {
-    if (diag & 1) {
-      bf16x4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = f2bf(acc[e] + b[e]);
-      return o;
-    }
-    return c2f_silu4(acc, b);
+  // bias-seeded accumulator -> SiLU (diag bit 1: identity, timing only) -> bf16
+  auto c2f_act4 = [&](floatx4 acc) __attribute__((always_inline)) -> bf16x4 {
+    return c2f_pack4((diag & 1) ? acc : c2f_silu4f(acc));
   };
 
   // 3x3 tap of lane quarter q in step j (the tenth tap re-reads tap 8: finite, weight 0)
@@ -166,12 +179,11 @@ __global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams 
     for (int b = 0; b < BPW; ++b) {
       const int px = (w + WAVES * b) * 16 + r16;
       const bf16x8 xf = __builtin_bit_cast(bf16x8, xr[b]);
-      const floatx4 z = {0.f, 0.f, 0.f, 0.f};
-      const floatx4 ta = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[0], xf, z, 0, 0, 0);
-      const floatx4 ts = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[1], xf, z, 0, 0, 0);
-      bf16x4 sv = c2f_act4(ts, bias4(16));
+      const floatx4 ta = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[0], xf, bias4(0), 0, 0, 0);
+      const floatx4 ts = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[1], xf, bias4(16), 0, 0, 0);
+      bf16x4 sv = c2f_act4(ts);
       if (!in) sv = bf16x4{0, 0, 0, 0};
-      *reinterpret_cast<bf16x4*>(arow + px * 16 + q * 4) = c2f_act4(ta, bias4(0));
+      *reinterpret_cast<bf16x4*>(arow + px * 16 + q * 4) = c2f_act4(ta);
       *reinterpret_cast<bf16x4*>(srow + (px + 1) * 16 + q * 4) = sv;
     }
   };
@@ -179,12 +191,23 @@ __global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams 
   // 3x3 16 -> 16: the five fragment reads of a block (rows r - 1 .. r + 1 of a ring at slots
   // sl[0..2]) are issued for every block of the wave before the first MFMA (hipcc otherwise
   // serialises read -> wait -> MFMA per tap: ~5 LDS round trips per block and step)
-  auto frags3 = [&](const bf16* ring, const int (&sl)[3], int px, bf16x8 (&fr)[5])
+  // Step j's taps are 2j (lanes q < 2) and 2j + 1 (q >= 2): both halves read the same ring row
+  // except in step 1 (taps 2 and 3), so the row base is a scalar and the per-lane part of the
+  // address (pixel, tap column, channel half) is precomputed once
+  const int px_w = w * 16 + r16;
+  const bool qhi = q >= 2;
+  const int fbase = px_w * 16 + (q & 1) * 8;  // bf16 units: pixel + channel half
+  const int fhi = qhi ? 16 : 0;               // one pixel further for the high half
+  auto frags3 = [&](const bf16* ring, const int (&sl)[3], int /*px*/, bf16x8 (&fr)[5])
       __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < 5; ++j)
-      fr[j] = *reinterpret_cast<const bf16x8*>(ring + (sl[tdy[j]] * WP + px + tdx[j]) * 16 +
-                                               (q & 1) * 8);
+    static_range<0, 5>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      constexpr int tlo = 2 * j, thi = 2 * j + 1 < 9 ? 2 * j + 1 : 8;
+      constexpr int dlo = tlo / 3, dhi = thi / 3, xlo = tlo % 3, xhi = thi % 3;
+      const bf16* row = ring + sl[dlo] * WP * 16;
+      if constexpr (dhi != dlo) row = qhi ? ring + sl[dhi] * WP * 16 : row;
+      fr[j] = *reinterpret_cast<const bf16x8*>(row + fbase + xlo * 16 + (xhi - xlo) * fhi);
+    });
   };
   // step B: u of rows r, r + 1 from s rows r - 1 .. r + 2 (zero outside the image); the two
   // rows' fragment reads go first, then their MFMA chains interleaved
@@ -197,7 +220,7 @@ __global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams 
       frags3(sring, sl, px, fr[i]);
     }
     __builtin_amdgcn_sched_barrier(0);
-    floatx4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    floatx4 acc[2] = {bias4(32), bias4(32)};
 #pragma unroll
     for (int j = 0; j < 5; ++j)
 #pragma unroll
@@ -206,7 +229,7 @@ __global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams 
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const bool in = r + i >= 0 && r + i < H;
-      bf16x4 uv = c2f_act4(acc[i], bias4(32));
+      bf16x4 uv = c2f_act4(acc[i]);
       if (!in) uv = bf16x4{0, 0, 0, 0};
       *reinterpret_cast<bf16x4*>(uring + slot_u(r + i) * WP * 16 + (px + 1) * 16 + q * 4) = uv;
     }
@@ -228,30 +251,29 @@ __global__ __launch_bounds__(WAVES * 64, 3) void c2f16_kernel(const KvC2fParams 
                     : *reinterpret_cast<const bf16x8*>(srow + (px + 1) * 16 + (q - 2) * 8);
     }
     __builtin_amdgcn_sched_barrier(0);
-    floatx4 m[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    floatx4 m[2] = {bias4(48), bias4(48)};
 #pragma unroll
     for (int j = 0; j < 5; ++j)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
         m[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm2f[j], fr[i][j], m[i], 0, 0, 0);
-    const floatx4 bm2 = bias4(48);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       bf16x8 vf;
+      const bf16x4 mv = c2f_act4(m[i]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         // rounded to bf16 before and after the shortcut add, as the four-launch path does
-        const float mv = (diag & 1) ? m[i][e] + bm2[e] : act_c<kActSilu>(m[i][e] + bm2[e]);
-        vf[e] = f2bf((float)f2bf(mv) + (float)sres[i][e]);
+        vf[e] = f2bf((float)mv[e] + (float)sres[i][e]);
         vf[4 + e] = (bf16)0.f;
       }
       const size_t ybase = ((size_t)(img * H + o + i) * W + px) * p.ldy + p.y_coff;
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
-        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f0[nb], as[i], acc, 0, 0, 0);
+        floatx4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f0[nb], as[i], bias4(64 + nb * 16),
+                                                              0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2f1[nb], vf, acc, 0, 0, 0);
-        const bf16x4 yv = c2f_act4(acc, bias4(64 + nb * 16));
+        const bf16x4 yv = c2f_act4(acc);
         __builtin_amdgcn_raw_buffer_store_b64(
             __builtin_bit_cast(c2f_u32x2, yv), ry,
             (diag & 4) ? kC2fOOB : (unsigned)(ybase + nb * 16 + q * 4) * 2u, 0, 0);
