@@ -125,11 +125,12 @@ class InferenceEngine:
         return self.outputs
 
     def prepare(self, warmup: int = 2, autotune: bool = True, verbose: bool = False,
-                tune_cache: Optional[str] = None):
+                tune_cache: Optional[str] = None, refine_s: Optional[float] = None):
         """Autotune conv tiles for this batch, warm up (code objects load, allocator
         pools fill), then capture the step into a hipGraph.  ``tune_cache``: JSON file of
         earlier picks (autotune.autotune), so a restarted module skips the timing sweep.
-        ``self.prep_s`` keeps the phase times (tune / warmup / capture)."""
+        ``self.prep_s`` keeps the phase times (tune / warmup / capture).  ``refine_s``: budget
+        of the in-graph tile refinement (None = KVEDGE_GRAPH_REFINE_S, default 30 s; 0 = off)."""
         self.tuning = {}
         self.prep_s = {}
         t0 = time.perf_counter()
@@ -163,7 +164,9 @@ class InferenceEngine:
         self.graph, self.outputs = self.capture(warm=False)
         self.prep_s["capture"] = time.perf_counter() - t2
         self.refine = None
-        if (autotune and self.tuning and
+        if refine_s is None:
+            refine_s = float(os.environ.get("KVEDGE_GRAPH_REFINE_S", "30"))
+        if (autotune and self.tuning and refine_s > 0 and
                 os.environ.get("KVEDGE_GRAPH_REFINE", "1") != "0"):
             # in-graph pick of the tiles (autotune.graph_refine): per-layer timing alone
             # does not see the neighbouring layers and the other slice's kernels
@@ -171,7 +174,7 @@ class InferenceEngine:
 
             t3 = time.perf_counter()
             self.refine = graph_refine(
-                self, budget_s=float(os.environ.get("KVEDGE_GRAPH_REFINE_S", "30")),
+                self, budget_s=refine_s,
                 verbose=verbose)
             self.prep_s["graph_refine"] = time.perf_counter() - t3
         return self

@@ -79,6 +79,8 @@ def main(argv=None):
     ap.add_argument("--source", default=d.source, choices=["synthetic", "camera"])
     ap.add_argument("--no-native-loop", action="store_true")
     ap.add_argument("--steps-per-poll", type=int, default=d.steps_per_poll)
+    ap.add_argument("--refine-s", type=float, default=d.refine_s,
+                    help="seconds of in-graph tile refinement at engine build (0 = off)")
     ap.add_argument("--steps", type=int, default=None, help="stop after N steps")
     ap.add_argument("--duration-s", type=float, default=None)
     ap.add_argument("--sync-every", type=int, default=d.sync_every,
@@ -97,7 +99,8 @@ def main(argv=None):
                        report_interval_s=a.report_interval_s, image_size=a.image_size,
                        fps=a.fps, use_graph=not a.no_graph, world_size=di.world_size,
                        source=a.source, native_loop=not a.no_native_loop,
-                       steps_per_poll=a.steps_per_poll, sync_every=a.sync_every).validate()
+                       steps_per_poll=a.steps_per_poll, sync_every=a.sync_every,
+                       refine_s=a.refine_s).validate()
     # one IoT Edge identity per VM: only local rank 0 talks to edgeHub
     kind = a.transport if di.local_rank == 0 or a.transport != "azure" else "null"
     app = ModuleApp(make_transport(kind), cfg, state_path=a.state,

@@ -389,7 +389,8 @@ class ModuleApp:
                                       synthetic=not camera,
                                       streams=edge_streams(cfg.batch) if dev.type == "cuda" else 1)
         self.engine.prepare(warmup=1, autotune=dev.type == "cuda",
-                            tune_cache=self.tune_cache if dev.type == "cuda" else None)
+                            tune_cache=self.tune_cache if dev.type == "cuda" else None,
+                            refine_s=cfg.refine_s)
         if not self.build_phases:
             # cold-start legs (tools/module_cold_start.py): model built -> tiles tuned
             # (or read from the cache) -> warmed -> graph captured

@@ -35,6 +35,11 @@ class ModuleConfig:
     source: str = "synthetic"
     native_loop: bool = True     # GPU: replay the graph from the C++ serve loop
     steps_per_poll: int = 1      # graph replays per module step (native loop)
+    # seconds of in-graph tile refinement when the engine is built (engine.prepare refine_s;
+    # 0 = off).  It times runner-up tiles inside the captured step: worth 2-3 % on YOLOv8n,
+    # ~0.1 % on ResNet-50, and it was 8.9 of the 12.6 s cold start at the bench's 30 s
+    # budget (profiles/r5_v14_module_cold_start.json)
+    refine_s: float = 3.0
     # multi-replica lockstep: module steps between control boundaries (0 = auto: every
     # step at world 1, 16 otherwise).  Twin patches, collective direct methods, report
     # decisions and stop requests are exchanged ONLY at these boundaries, so every rank
@@ -69,6 +74,8 @@ class ModuleConfig:
             raise ValueError(f"source must be one of {SOURCES}, got {self.source!r}")
         if not 1 <= self.steps_per_poll <= 1000:
             raise ValueError("steps_per_poll must be 1..1000")
+        if not 0.0 <= self.refine_s <= 600.0:
+            raise ValueError("refine_s must be 0..600")
         if not 0 <= self.sync_every <= 10000:
             raise ValueError("sync_every must be 0..10000")
         return self

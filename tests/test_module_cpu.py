@@ -347,3 +347,13 @@ def test_azure_transport_against_stub_sdk(tmp_path, monkeypatch):
     assert resp["r2"].status == 404 and resp["r3"].status == 200
     app.stop()
     assert sdk.calls[-1] == "shutdown"
+
+
+def test_refine_budget_config():
+    """The module's in-graph refine budget is a validated twin/CLI key (0 = off)."""
+    import pytest
+    from kvedge_amd.module.config import ModuleConfig
+    assert ModuleConfig().refine_s == 3.0
+    ModuleConfig(refine_s=0.0).validate()
+    with pytest.raises(ValueError):
+        ModuleConfig(refine_s=-1.0).validate()
