@@ -46,3 +46,18 @@ def test_inflight_asm_loads_flag_ad7a357_and_pass_head():
     assert ok.returncode == 0, ok.stderr[-2000:]
     rows = [l for l in ok.stdout.splitlines() if l.startswith("| conv_seam")]
     assert len(rows) >= 8 and all(l.rstrip(" |").endswith("| 0") for l in rows)
+
+
+@pytest.mark.skipif(not (os.path.exists(HIPCC) or shutil.which("hipcc")), reason="no hipcc")
+def test_round5_kernels_no_spill_no_inflight_reads():
+    """The v12 edge-batch family (LDS-DMA rings behind asm waits) and the v13 fused C2f
+    kernel (3 waves per SIMD at <= 168 VGPRs): every instantiation spill-free, and no read of
+    an asm load's destination before its wait."""
+    k = os.path.join(ROOT, "csrc", "kernels")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_lint.py"),
+                        os.path.join(k, "conv_skinny.hip"), os.path.join(k, "c2f_fused.hip"),
+                        "--no-spill", "--inflight"],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-2000:] + r.stdout[-2000:]
+    rows = [l for l in r.stdout.splitlines() if l.startswith(("| conv_skinny", "| c2f_fused"))]
+    assert len(rows) == 27 + 2, len(rows)  # 9 tiles x 3 modes, 2 widths
