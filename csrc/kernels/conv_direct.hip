@@ -29,6 +29,7 @@
 //  * Bands are dealt XCD-aware: concurrently running neighbour bands of one image sit on
 //    one XCD, so their shared halo rows come from one L2.
 #include <stdlib.h>
+#include <string.h>
 
 #include "common.h"
 #include "kvedge_kernels.h"
@@ -800,6 +801,7 @@ static const DirectEntry kDirect[] = {
     KV_DIRECT_DE(64, 64, 1, 3, kActRelu),     // ResNet-50 layer1 conv2
     KV_DIRECT_DE(64, 128, 1, 3, kActSilu),    // Detect P3 merged stem 64 -> 144 = 128 + 16
     KV_DIRECT_DE(64, 16, 1, 3, kActSilu),
+    KV_DIRECT_DE(64, 80, 1, 3, kActSilu),     // ... or 80 + 64 (KVEDGE_DIRECT_SPLIT=balanced)
     KV_DIRECT_DE(64, 64, 1, 3, kActSilu),     // bottleneck cv1 / Detect a1
     KV_DIRECT_DE(80, 80, 1, 3, kActSilu),
     KV_DIRECT_DE(64, 128, 2, 3, kActSilu),    // b5
@@ -819,6 +821,7 @@ static const DirectEntry kDirect[] = {
     KV_DIRECT_DER(16, 16, 2), KV_DIRECT_DER(32, 32, 2),
     KV_DIRECT_SB(64, 64, 1, 3, kActRelu), KV_DIRECT_SB(64, 128, 1, 3, kActSilu),
     KV_DIRECT_SB(64, 16, 1, 3, kActSilu), KV_DIRECT_SB(64, 64, 1, 3, kActSilu),
+    KV_DIRECT_SB(64, 80, 1, 3, kActSilu),
     KV_DIRECT_SB(64, 128, 2, 3, kActSilu), KV_DIRECT_SB(64, 64, 2, 3, kActSilu),
     KV_DIRECT_SB(32, 64, 2, 3, kActSilu), KV_DIRECT_SB(32, 32, 1, 3, kActSilu),
     KV_DIRECT_SB(80, 80, 1, 3, kActSilu),
@@ -948,15 +951,38 @@ static int direct_launch_one(const KvConvParams* p, int tile, hipStream_t stream
 }
 
 // A Cout with no instantiation of its own is covered by consecutive output-channel slices
-// that have one (largest first), e.g. YOLO's merged Detect stem 64 -> 144 = 128 + 16: each
-// slice re-reads the input (cheap: the layer is MFMA-bound) and writes its y_coff range.
+// that have one, e.g. YOLO's merged Detect stem 64 -> 144: each slice re-reads the input and
+// writes its y_coff range, largest first (144 = 128 + 16).  KVEDGE_DIRECT_SPLIT=balanced
+// takes the most balanced two-slice split instead (144 = 80 + 64 with the 64 -> 80 forms):
+// the 16-wide slice does a ninth of the work at a fifth of the MFMA rate
+// (profiles/r5_v10_graph_layers_yolo_b512_c2f.md: 137 vs 206 us per b256 slice), but the
+// balanced pair measured level on the bench (profiles/r5_v15_direct_split_ab.txt).
 int direct_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   if (tile < 0 || tile >= 16) return -6;
   int kR, PW, rows, lds;
   if (direct_plan(p, tile, &kR, &PW, &rows, &lds) >= 0) return direct_launch_one(p, tile, stream);
   if (p->res || p->Cout % 16 || p->pair_1x1) return -8;
+  static const bool greedy =
+      !(getenv("KVEDGE_DIRECT_SPLIT") && strcmp(getenv("KVEDGE_DIRECT_SPLIT"), "balanced") == 0);
   // validate the whole split before launching anything
   int cuts[8], ncut = 0, done = 0;
+  auto fits = [&](int cout) {
+    KvConvParams q = *p;
+    q.Cout = cout;
+    return direct_plan(&q, tile, &kR, &PW, &rows, &lds) >= 0;
+  };
+  if (!greedy) {
+    int best = 0;
+    for (const DirectEntry& e : kDirect) {
+      const int a = e.cout, b = p->Cout - e.cout;
+      if (a >= b && b > 0 && (best == 0 || a < best) && fits(a) && fits(b)) best = a;
+    }
+    if (best) {
+      cuts[ncut++] = best;
+      cuts[ncut++] = p->Cout - best;
+      done = p->Cout;
+    }
+  }
   while (done < p->Cout && ncut < 8) {
     int best = 0;
     for (const DirectEntry& e : kDirect) {

@@ -116,6 +116,7 @@ SKN0 = 108  # v12: skinny edge-batch implicit GEMM (conv_skinny.hip kSknTiles): 
 # (cin, cout, k, stride, act) instantiated as v10 tile 0 / 1 / 2 (no residual, no fallback)
 DE_SHAPES = {
     0: {(64, 64, 3, 1, ops.ACT_RELU), (64, 128, 3, 1, ops.ACT_SILU), (64, 16, 3, 1, ops.ACT_SILU),
+        (64, 80, 3, 1, ops.ACT_SILU),
         (64, 64, 3, 1, ops.ACT_SILU), (80, 80, 3, 1, ops.ACT_SILU), (64, 128, 3, 2, ops.ACT_SILU),
         (64, 64, 3, 2, ops.ACT_SILU), (32, 64, 3, 2, ops.ACT_SILU), (16, 32, 3, 2, ops.ACT_SILU),
         (32, 32, 3, 1, ops.ACT_SILU), (16, 16, 3, 1, ops.ACT_SILU), (32, 32, 1, 1, ops.ACT_SILU),
@@ -126,7 +127,7 @@ DE_SHAPES = {
     1: {(16, 32, 3, 2, ops.ACT_SILU), (16, 16, 3, 1, ops.ACT_SILU), (32, 64, 3, 2, ops.ACT_SILU),
         (32, 32, 3, 1, ops.ACT_SILU), (32, 32, 1, 1, ops.ACT_SILU), (48, 32, 1, 1, ops.ACT_SILU)},
     2: {(64, 64, 3, 1, ops.ACT_RELU), (64, 128, 3, 1, ops.ACT_SILU), (64, 16, 3, 1, ops.ACT_SILU),
-        (64, 64, 3, 1, ops.ACT_SILU), (64, 128, 3, 2, ops.ACT_SILU), (64, 64, 3, 2, ops.ACT_SILU),
+        (64, 80, 3, 1, ops.ACT_SILU), (64, 64, 3, 1, ops.ACT_SILU), (64, 128, 3, 2, ops.ACT_SILU), (64, 64, 3, 2, ops.ACT_SILU),
         (32, 64, 3, 2, ops.ACT_SILU), (32, 32, 3, 1, ops.ACT_SILU), (80, 80, 3, 1, ops.ACT_SILU)},
 }
 
@@ -568,6 +569,7 @@ def test_conv_poisoned_canary(tile, k):
     (2, 10, 10, 64, 64, 2, ops.ACT_SILU, False, 0, 0, 0, 0),     # h16
     (1, 160, 160, 16, 16, 1, ops.ACT_SILU, False, 0, 0, 0, 0),   # full YOLO row width
     (2, 20, 20, 64, 144, 1, ops.ACT_SILU, False, 0, 0, 16, 8),   # Detect stem: 128 + 16 split
+    (2, 23, 21, 64, 80, 1, ops.ACT_SILU, False, 0, 0, 8, 8),     # its 80-wide slice alone
     (2, 80, 80, 80, 80, 1, ops.ACT_SILU, False, 64, 64, 0, 0),   # Detect P3 cls 3x3 (NCB = 3)
     (3, 13, 11, 80, 80, 1, ops.ACT_SILU, False, 0, 0, 8, 8),     # pixel-block tails, y slice
     (2, 40, 40, 80, 80, 1, ops.ACT_SILU, False, 64, 64, 0, 0),   # Detect P4 cls
