@@ -180,6 +180,66 @@ void conv_dual(const at::Tensor& x1, const at::Tensor& x2, const at::Tensor& w,
   TORCH_CHECK(rc == 0, "kvedge: conv_dual failed rc=", rc);
 }
 
+// Dual-source 1x1 GEMM over channel slices (YOLO neck): y[.., y_coff : y_coff + Cout] =
+//   act( x[.., x_coff : x_coff + K1] . W[:, :K1] + x2'[.., x2_coff : x2_coff + K2] . W[:, K1:] + b )
+// with x2' = x2 at stride s2 (up2 = 0) or x2 upsampled 2x nearest (up2 = 1: x2 is [N, Ho/2,
+// Wo/2, ..]; the concat of an upsampled map and a skip tensor never materialises).
+void conv_dual2(const at::Tensor& x, int64_t x_coff, int64_t K1, const at::Tensor& x2,
+                int64_t x2_coff, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                at::Tensor& y, int64_t y_coff, int64_t stride2, int64_t up2, int64_t act,
+                int64_t tile, const c10::optional<at::Tensor>& ws) {
+  check_bf16(x, "x");
+  check_bf16(x2, "x2");
+  check_bf16(w, "w");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.dim() == 4 && x2.dim() == 4 && y.dim() == 4 && w.dim() == 2, "kvedge: NHWC tensors");
+  const int64_t N = x.size(0), Ho = x.size(1), Wo = x.size(2);
+  const int64_t Cout = w.size(0), K2 = w.size(1) - K1;
+  TORCH_CHECK(K1 > 0 && K2 > 0 && K1 % 64 == 0 && K2 % 64 == 0, "kvedge: K1, K2 multiples of 64");
+  TORCH_CHECK(x_coff >= 0 && x_coff % 8 == 0 && x_coff + K1 <= x.size(3), "kvedge: x slice");
+  TORCH_CHECK(x2_coff >= 0 && x2_coff % 8 == 0 && x2_coff + K2 <= x2.size(3), "kvedge: x2 slice");
+  TORCH_CHECK(y_coff >= 0 && y_coff % 8 == 0 && y_coff + Cout <= y.size(3), "kvedge: y slice");
+  TORCH_CHECK(x.size(3) % 8 == 0 && x2.size(3) % 8 == 0 && y.size(3) % 8 == 0, "kvedge: pitches");
+  TORCH_CHECK(y.size(0) == N && y.size(1) == Ho && y.size(2) == Wo && x2.size(0) == N, "kvedge: y shape");
+  if (up2) {
+    TORCH_CHECK(x2.size(1) * 2 == Ho && x2.size(2) * 2 == Wo, "kvedge: up2 needs x2 at half size");
+  } else {
+    TORCH_CHECK(stride2 >= 1 && (x2.size(1) + stride2 - 1) / stride2 == Ho &&
+                    (x2.size(2) + stride2 - 1) / stride2 == Wo,
+                "kvedge: x2 geometry vs stride");
+  }
+  TORCH_CHECK(x.numel() * 2 < (1ll << 31) && x2.numel() * 2 < (1ll << 31) && y.numel() * 2 < (1ll << 31),
+              "kvedge: conv_dual2 operands exceed 2 GiB");
+  const c10::DeviceGuard g(x.device());
+  KvConvParams p{};
+  p.x = x.data_ptr();
+  p.w = w.data_ptr();
+  p.bias = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    check_dev(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= Cout, "kvedge: bias fp32[Cout]");
+    p.bias = bias->data_ptr<float>();
+  }
+  p.y = y.data_ptr();
+  p.N = (int)N; p.H = (int)Ho; p.W = (int)Wo; p.Cin = (int)K1; p.ldx = (int)x.size(3);
+  p.x_coff = (int)x_coff;
+  p.Ho = (int)Ho; p.Wo = (int)Wo; p.Cout = (int)Cout;
+  p.KH = 1; p.KW = 1; p.stride = 1; p.pad = 0;
+  p.K = (int)(K1 + K2); p.Kpad = (int)(K1 + K2);
+  p.M = (int)(N * Ho * Wo);
+  p.ldy = (int)y.size(3); p.y_coff = (int)y_coff; p.ldr = 0; p.r_coff = 0;
+  p.act = (int)act; p.mode = 4;
+  p.x2 = x2.data_ptr(); p.K1 = (int)K1; p.H2 = (int)x2.size(1); p.W2 = (int)x2.size(2);
+  p.ldx2 = (int)x2.size(3); p.stride2 = (int)stride2; p.x2_coff = (int)x2_coff; p.up2 = (int)up2;
+  if (ws.has_value() && ws->defined()) {
+    check_dev(*ws, "ws");
+    TORCH_CHECK(ws->scalar_type() == at::kFloat, "kvedge: split-K workspace fp32");
+    set_splitk_ws(p, *ws);
+  }
+  const int rc = kv_conv2d(&p, (int)tile, cur_stream(x));
+  TORCH_CHECK(rc == 0, "kvedge: conv_dual2 failed rc=", rc);
+}
+
 // Fused bottleneck tail: y = act(x . W^T [+ x2 . W2^T] + bias [+ res]) (conv3, optionally
 // with the fused downsample), then z = ReLU(y . w1^T + b1) -- the next block's 1x1 reduce --
 // from the y tile still in LDS, so y is written once and never re-read.
@@ -730,6 +790,8 @@ TORCH_LIBRARY(kvedge, m) {
   m.def("c2f16_fused(Tensor x, int x_coff, Tensor w1, Tensor b1, Tensor wm1, Tensor bm1, "
         "Tensor wm2, Tensor bm2, Tensor w2, Tensor b2, Tensor(a!) y, int y_coff, int S) -> ()");
   m.def("c2f16_supported(int H, int W, int S) -> int", c2f16_supported);
+  m.def("conv_dual2(Tensor x, int x_coff, int K1, Tensor x2, int x2_coff, Tensor w, Tensor? bias, "
+        "Tensor(a!) y, int y_coff, int stride2, int up2, int act, int tile, Tensor(b!)? ws=None) -> ()");
   m.def("set_conv_chunk_bytes(int bytes) -> int", set_conv_chunk_bytes);
 }
 
@@ -743,6 +805,7 @@ TORCH_LIBRARY_IMPL(kvedge, CUDA, m) {
   m.impl("conv_pair", conv_pair);
   m.impl("bneck_fused", bneck_fused);
   m.impl("c2f16_fused", c2f16_fused);
+  m.impl("conv_dual2", conv_dual2);
   m.impl("sppf_pool", sppf_pool);
   m.impl("global_avgpool", global_avgpool);
   m.impl("softmax_rows", softmax_rows);

@@ -407,7 +407,8 @@ int nloop_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   const NlTile& e = kNlTiles[tile];
   if (p->n_t || p->in_u8) return -8;
   if (e.dual) {  // conv3 + fused downsample only
-    if (p->mode != 4 || p->res || !p->x2 || p->K1 % 64 || (p->Kpad - p->K1) % 64 ||
+    if (p->mode != 4 || p->res || !p->x2 || p->up2 || p->x2_coff || p->K1 % 64 ||
+        (p->Kpad - p->K1) % 64 ||
         (long long)p->N * p->H2 * p->W2 * p->ldx2 * 2 >= kNlOOB)
       return -8;
   } else if (p->mode != 1) {

@@ -304,7 +304,8 @@ int skinny_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   if (p->K % 64 || p->Cout % 4 || p->Kpad % 64) return -8;
   if (p->mode == 0 && (p->Cin % 64 || p->K != p->KH * p->KW * p->Cin)) return -8;
   if (p->mode == 1 && (p->Cin % 64 || p->K != p->Cin)) return -8;
-  if (p->mode == 4 && (p->K1 % 64 || (p->K - p->K1) % 64 || p->ldx2 % 8 || p->K - p->K1 > p->ldx2))
+  if (p->mode == 4 && (p->K1 % 64 || (p->K - p->K1) % 64 || p->ldx2 % 8 || p->K - p->K1 > p->ldx2 ||
+                       p->up2 || p->x2_coff))
     return -8;
   if (p->M >= (1 << 16)) return -8;  // FastDiv is exact below 2^16 (edge batches only)
   const SknTile& e = kSknTiles[tile];

@@ -530,7 +530,7 @@ int stream_tail_tile(int n_t) {
 int stream_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   if (tile < 0 || tile >= stream_num_tiles()) return -6;
   if (p->mode != 1 && p->mode != 4) return -8;  // 1x1 stride-1 GEMM or fused dual only
-  if (p->mode == 4 && p->res) return -8;
+  if (p->mode == 4 && (p->res || p->up2 || p->x2_coff)) return -8;  // plain dual sources only
   if ((long long)p->M * p->ldy * 2 >= kOOB || (p->res && (long long)p->M * p->ldr * 2 >= kOOB))
     return -9;
   const long long xb = (long long)p->N * p->H * p->W * p->ldx * 2;

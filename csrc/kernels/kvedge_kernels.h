@@ -60,6 +60,12 @@ typedef struct KvConvParams {
   float* ws;
   int ksplit;
   long long ws_elems;  // floats in ws
+  // mode 4, second source extras (YOLO neck): channel offset of x2's slice, and up2 = 1: x2
+  // is a half-resolution map read at (ho / 2, wo / 2) -- the nearest 2x upsample of the
+  // concat folded into the GEMM (H2 = Ho / 2).  v2 LDS-DMA tiles (and their v7 / v8 forms)
+  // only; every other family refuses.
+  int x2_coff;
+  int up2;
 } KvConvParams;
 
 // tile: -1 = heuristic; otherwise an index into the tile table (kv_conv_num_tiles()).

@@ -173,6 +173,34 @@ def _dc(m: Conv, device) -> DeployedConv:
     return DeployedConv.from_modules(m.conv, m.bn, ACT_SILU, device)
 
 
+class DeployedUpDual:
+    """A neck C2f's cv1 over [upsample2x(low) | skip] as ONE dual-source GEMM (ops.conv_dual2,
+    up2): the skip tensor is read at full resolution, the low-resolution map at (h / 2, w / 2)
+    -- no upsample launch, and the concat's upsampled half is never written or read.  The
+    packed weight's columns are permuted to [skip | upsampled]."""
+
+    def __init__(self, cv1: DeployedConv, c_up: int):
+        w = cv1.w[:, :cv1.spec.K]
+        self.c_up, self.c_skip = c_up, cv1.spec.K - c_up
+        self.w = torch.cat([w[:, c_up:], w[:, :c_up]], 1).contiguous()
+        self.b = cv1.b
+        self.act = cv1.spec.act
+        self.tile = -1
+
+    def __call__(self, skip, skip_coff, low, low_coff, out, y_coff=0, tile=None):
+        ops.conv_dual2(skip, self.c_skip, low, self.w, self.b, self.act, out, x_coff=skip_coff,
+                       x2_coff=low_coff, y_coff=y_coff, up2=True,
+                       tile=self.tile if tile is None else tile)
+        if _recorder_active():
+            key = ("dual_up", tuple(skip.shape), skip_coff, tuple(low.shape), low_coff,
+                   tuple(out.shape), y_coff, tuple(self.w.shape))
+            fn = lambda t, o=out: ops.conv_dual2(  # noqa: E731
+                skip, self.c_skip, low, self.w, self.b, self.act, o, x_coff=skip_coff,
+                x2_coff=low_coff, y_coff=y_coff, up2=True, tile=t)
+            _record(self, key, fn)
+        return out
+
+
 class DC2f:
     def __init__(self, m: C2f, device):
         self.c = m.c
@@ -194,6 +222,25 @@ class DC2f:
                 self.m[0][2] and self.cv1.spec.cin == 32 and self.cv2.spec.cout == 32 and
                 ops.c2f16_strip(H, W) > 0)
 
+    def up_call(self, skip, skip_coff, low, low_coff, c_up, out=None, y_coff=0):
+        """The block over [upsample2x(low[..., low_coff : + c_up]) | skip[..., skip_coff :]]
+        with cv1 as one dual-source GEMM (DeployedUpDual): same result as writing the
+        upsampled map into the concat and calling the block on it."""
+        if getattr(self, "_up", None) is None:
+            self._up = DeployedUpDual(self.cv1, c_up)
+        N, H, W, _ = skip.shape
+        c, n = self.c, self.n
+        cat = ops.empty(N, H, W, (2 + n) * c, dtype=torch.bfloat16, device=skip.device)
+        self._up(skip, skip_coff, low, low_coff, cat, 0)
+        return self._rest(cat, out, y_coff)
+
+    def _rest(self, cat, out, y_coff):
+        c = self.c
+        for i, (b1, b2, add) in enumerate(self.m):
+            t = b1(cat, x_coff=(1 + i) * c)
+            b2(t, res=cat if add else None, r_coff=(1 + i) * c, out=cat, y_coff=(2 + i) * c)
+        return self.cv2(cat, out=out, y_coff=y_coff)
+
     def __call__(self, x, x_coff=0, out=None, y_coff=0):
         N, H, W, _ = x.shape
         c, n = self.c, self.n
@@ -203,10 +250,7 @@ class DC2f:
                              self.cv2.b, out=out, x_coff=x_coff, y_coff=y_coff)
         cat = ops.empty(N, H, W, (2 + n) * c, dtype=torch.bfloat16, device=x.device)
         self.cv1(x, x_coff=x_coff, out=cat, y_coff=0)
-        for i, (b1, b2, add) in enumerate(self.m):
-            t = b1(cat, x_coff=(1 + i) * c)
-            b2(t, res=cat if add else None, r_coff=(1 + i) * c, out=cat, y_coff=(2 + i) * c)
-        return self.cv2(cat, out=out, y_coff=y_coff)
+        return self._rest(cat, out, y_coff)
 
     def convs(self):
         out = [self.cv1, self.cv2]
@@ -374,6 +418,10 @@ class KvYoloV8n:
             return ops.yolo_stem2(frames_u8, b0.spec, b0.w, b0.b, b1.spec, b1.w, b1.b)
         return self.b1(self.stem(frames_u8))
 
+    # GPU: the neck's two upsample + concat steps folded into h12 / h15's cv1
+    # (DeployedUpDual); KVEDGE_YOLO_FUSE_UP=0 = A/B off
+    fuse_up: bool = os.environ.get("KVEDGE_YOLO_FUSE_UP", "1") != "0"
+
     def heads(self, x: torch.Tensor, stem_done: bool = False, b1_done: bool = False):
         """x: preprocessed bf16 s2d [N,320,320,16] (or, with stem_done, the b0 output; with
         b1_done, the b1 output) -> three [N,h,w,144] head outputs."""
@@ -396,10 +444,16 @@ class KvYoloV8n:
         x = self.b7(cat11, x_coff=256)                             # [N,20,20,256]
         x = self.b8(x)
         self.b9(x, out=cat20, y_coff=128)                          # p5b
-        ops.upsample2x(cat20, cat11, C=256, x_coff=128, y_coff=0)
-        self.h12(cat11, out=cat17, y_coff=64)                      # h12
-        ops.upsample2x(cat17, cat14, C=128, x_coff=64, y_coff=0)
-        p3 = self.h15(cat14)                                       # [N,80,80,64]
+        if self.fuse_up and dev.type == "cuda":
+            # the upsampled halves of cat11 / cat14 are never written: h12 / h15 read p5b and
+            # h12 at half resolution inside their cv1 GEMM (DeployedUpDual)
+            self.h12.up_call(cat11, 256, cat20, 128, 256, out=cat17, y_coff=64)     # h12
+            p3 = self.h15.up_call(cat14, 128, cat17, 64, 128)                     # [N,80,80,64]
+        else:
+            ops.upsample2x(cat20, cat11, C=256, x_coff=128, y_coff=0)
+            self.h12(cat11, out=cat17, y_coff=64)                      # h12
+            ops.upsample2x(cat17, cat14, C=128, x_coff=64, y_coff=0)
+            p3 = self.h15(cat14)                                       # [N,80,80,64]
         self.h16(p3, out=cat17, y_coff=0)
         p4 = self.h18(cat17)                                       # [N,40,40,128]
         self.h19(p4, out=cat20, y_coff=0)

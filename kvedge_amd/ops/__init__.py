@@ -296,6 +296,25 @@ def conv_dual(x1: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, bias: Optiona
     return out
 
 
+def conv_dual2(x: torch.Tensor, K1: int, x2: torch.Tensor, w: torch.Tensor,
+               bias: Optional[torch.Tensor], act: int, out: torch.Tensor, x_coff: int = 0,
+               x2_coff: int = 0, y_coff: int = 0, stride2: int = 1, up2: bool = False,
+               tile: int = -1) -> torch.Tensor:
+    """Dual-source 1x1 GEMM over channel slices: out[..., y_coff : y_coff + Cout] =
+    act(x[..., x_coff : x_coff + K1] . W[:, :K1]^T + x2'[..., x2_coff : x2_coff + K2] . W[:, K1:]^T
+    + bias), x2' = x2 at ``stride2``, or with ``up2`` x2 (half resolution) upsampled 2x
+    nearest -- YOLO's neck C2f cv1 reads its [upsampled | skip] concat without the upsample
+    launch or the concat's upsampled half (v2 LDS-DMA tiles and their v7 / v8 forms only)."""
+    if x.is_cuda:
+        N, Ho, Wo, _ = x.shape
+        ws = splitk_workspace(x.device, N * Ho * Wo * w.shape[0]) if is_splitk(tile) else None
+        _native().conv_dual2(x, x_coff, K1, x2, x2_coff, w, bias, out, y_coff, stride2,
+                             1 if up2 else 0, act, tile, ws)
+    else:
+        _ref.conv_dual2(x, x_coff, K1, x2, x2_coff, w, bias, act, stride2, up2, out, y_coff)
+    return out
+
+
 def conv_tail(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], act: int,
               w1: torch.Tensor, b1: Optional[torch.Tensor], res: Optional[torch.Tensor] = None,
               x2: Optional[torch.Tensor] = None, stride2: int = 1,

@@ -164,6 +164,19 @@ def preprocess(x, out, mean, std):
     return out
 
 
+def conv_dual2(x, x_coff, K1, x2, x2_coff, w, bias, act, stride2, up2, out, y_coff):
+    K2 = w.shape[1] - K1
+    a = x[..., x_coff:x_coff + K1].float()
+    b = x2[..., x2_coff:x2_coff + K2].float()
+    b = b.repeat_interleave(2, 1).repeat_interleave(2, 2) if up2 else b[:, ::stride2, ::stride2]
+    wf = w.float()
+    y = a @ wf[:, :K1].t() + b @ wf[:, K1:].t()
+    if bias is not None:
+        y = y + bias.float()
+    out[..., y_coff:y_coff + w.shape[0]] = _act(y, act & 3).to(out.dtype)
+    return out
+
+
 def conv_dual(x1, x2, w, bias, act, stride2, out):
     K1 = x1.shape[-1]
     wf = w.float()

@@ -1005,3 +1005,39 @@ def test_c2f16_matches_four_launch_block():
         ops.C2F_ENABLED = old
     torch.cuda.synchronize()
     _assert_close(fused.cpu(), four.cpu(), "c2f16 vs four launches")
+
+
+@pytest.mark.parametrize("tile", [-1] + list(range(6, DIRECT0)) + [NLOOP0, 63, 64] +
+                         list(range(XP0, DE0)) + [DE0, SKN0, SKN0 + 8])
+@pytest.mark.parametrize("geom", [
+    # (N, H, W, skip ld, skip coff, K1, low ld, low coff, K2, Cout, y ld, y coff): YOLO h15 / h12
+    (2, 20, 20, 192, 128, 64, 192, 64, 128, 64, 96, 0),
+    (1, 10, 12, 384, 256, 128, 384, 128, 256, 128, 192, 64),
+])
+def test_conv_dual2_up2(tile, geom):
+    """The neck's [upsample2x(low) | skip] concat folded into cv1 (ops.conv_dual2, up2): the
+    v2 LDS-DMA tiles and their v7 / v8 forms compute it (vs the fp32 reference; channels
+    outside the output slice stay untouched), every other family refuses it."""
+    N, H, W, lds, sc, K1, ldl, lc, K2, cout, ldy, yc = geom
+    g = torch.Generator().manual_seed(tile + 100)
+    skip = torch.randn(N, H, W, lds, generator=g).to(torch.bfloat16)
+    low = torch.randn(N, H // 2, W // 2, ldl, generator=g).to(torch.bfloat16)
+    w = (torch.randn(cout, K1 + K2, generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(cout, generator=g)
+    ref = torch.full((N, H, W, ldy), 7.0, dtype=torch.bfloat16)
+    ops.conv_dual2(skip, K1, low, w, b, ops.ACT_SILU, ref, x_coff=sc, x2_coff=lc, y_coff=yc,
+                   up2=True)
+    out = torch.full((N, H, W, ldy), 7.0, dtype=torch.bfloat16, device="cuda")
+    args = (skip.cuda(), K1, low.cuda(), w.cuda(), b.cuda(), ops.ACT_SILU, out)
+    kw = dict(x_coff=sc, x2_coff=lc, y_coff=yc, up2=True, tile=tile)
+    if not (tile == -1 or 6 <= tile < STREAM0 or XP0 <= tile < DE0):
+        with pytest.raises(RuntimeError):
+            ops.conv_dual2(*args, **kw)
+        return
+    ops.conv_dual2(*args, **kw)
+    torch.cuda.synchronize()
+    got = out.cpu()
+    mask = torch.ones(ldy, dtype=torch.bool)
+    mask[yc:yc + cout] = False
+    assert (got[..., mask].float() == 7.0).all()
+    _assert_close(got[..., yc:yc + cout], ref[..., yc:yc + cout], ("dual2 up2", tile, geom))

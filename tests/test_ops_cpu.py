@@ -159,3 +159,44 @@ def test_c2f16_reference_matches_block():
     one = ops.c2f16(x, blk.cv1.w, blk.cv1.b, b1.w, b1.b, b2.w, b2.b, blk.cv2.w, blk.cv2.b,
                     x_coff=8)
     assert torch.equal(four, one)
+
+
+def test_conv_dual2_up2_reference_matches_upsample_concat():
+    """ops.conv_dual2 with up2 (the neck's upsample + concat folded into cv1) equals the
+    1x1 conv over the materialised [upsample2x(low) | skip] concat, weights permuted."""
+    import torch
+    from kvedge_amd import ops
+    from kvedge_amd.ops import ConvSpec
+    g = torch.Generator().manual_seed(4)
+    N, H, W, c_up, c_skip, cout = 2, 6, 8, 128, 64, 72
+    low = (torch.randn(N, H // 2, W // 2, 8 + c_up, generator=g)).to(torch.bfloat16)
+    skip = (torch.randn(N, H, W, 16 + c_skip, generator=g)).to(torch.bfloat16)
+    spec = ConvSpec.auto(c_up + c_skip, cout, 1, 1, 0, ops.ACT_SILU)
+    w = ops.pack_conv_weight(torch.randn(cout, c_up + c_skip, 1, 1, generator=g) * 0.05, spec)
+    b = torch.randn(cout, generator=g)
+    cat = torch.cat([low[..., 8:].repeat_interleave(2, 1).repeat_interleave(2, 2),
+                     skip[..., 16:]], -1)
+    ref = ops.conv2d(cat, spec, w, b)
+    wd = torch.cat([w[:, c_up:], w[:, :c_up]], 1).contiguous()
+    out = torch.zeros(N, H, W, cout + 8, dtype=torch.bfloat16)
+    ops.conv_dual2(skip, c_skip, low, wd, b, ops.ACT_SILU, out, x_coff=16, x2_coff=8, y_coff=8,
+                   up2=True)
+    assert (out[..., :8] == 0).all()
+    assert (out[..., 8:].float() - ref.float()).abs().max() <= 0.02 * ref.float().abs().max()
+
+
+def test_c2f_up_call_matches_upsample_path():
+    """DC2f.up_call (cv1 as the up2 dual GEMM) == upsample2x into the concat + the block."""
+    import torch
+    from kvedge_amd import ops
+    from kvedge_amd.models.yolov8 import C2f, DC2f
+    torch.manual_seed(2)
+    blk = DC2f(C2f(192, 64, 1, False).eval(), "cpu")
+    N, H, W = 1, 8, 6
+    low = torch.randn(N, H // 2, W // 2, 192).to(torch.bfloat16)      # up source at channel 64
+    cat = torch.randn(N, H, W, 192).to(torch.bfloat16)               # [up 128 | skip 64]
+    ops.upsample2x(low, cat, C=128, x_coff=64, y_coff=0)
+    ref = blk(cat)
+    got = blk.up_call(cat, 128, low, 64, 128)
+    d = (got.float() - ref.float()).abs().max().item()
+    assert d <= 0.03 * ref.float().abs().max().item(), d
