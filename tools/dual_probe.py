@@ -14,6 +14,7 @@ def main():
     ap.add_argument("--batch", type=int, default=640)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tiles", default="30")
+    ap.add_argument("--only", default="", help="comma list of layer names (s2.dual, ...)")
     a = ap.parse_args()
     import torch
     from kvedge_amd import ops
@@ -24,6 +25,8 @@ def main():
     # (name, Ho, K1 (conv2 out ch), K2 (block input ch), Cout), stride 2 downsample
     layers = [("s2.dual", 28, 128, 256, 512), ("s3.dual", 14, 256, 512, 1024),
               ("s4.dual", 7, 512, 1024, 2048)]
+    if a.only:
+        layers = [l for l in layers if l[0] in a.only.split(",")]
     print("| layer | " + " | ".join(str(t) for t in tiles) + " | GB |")
     print("|---" * (len(tiles) + 2) + "|")
     for name, ho, k1, k2, co in layers:
