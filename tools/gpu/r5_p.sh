@@ -1,4 +1,4 @@
-# Round 5 (p): in-graph tables of the YOLOv8n bench step (with the fused C2f) and the b64 edge step
+# Round 5 (p): in-graph tables of the YOLOv8n bench step and the ResNet-50 b1280 bench step
 set -o pipefail
 mkdir -p gpurun_out; export TMPDIR=/tmp
 T=${TAG:-r5p}
@@ -11,4 +11,4 @@ run() {  # tag model batch streams
   head -4 gpurun_out/${T}_$1.md | tail -1
   rm -rf gpurun_out/${T}_$1
 }
-run yolo_b512 yolov8n 512 2 && run rn_b64 resnet50 64 1
+run yolo_b512 yolov8n 512 2 && run rn_b1280 resnet50 1280 2
