@@ -99,6 +99,10 @@ void conv_stream_kernel(const KvConvParams p) {
   static_assert(NT1 == 0 || (BM == 64 && BRES && NT1 % 64 == 0 && PERZ >= 1), "tail tile");
   // cache policy of the streamed (read-once / write-once) bytes: 0 default, 2 = nt
   constexpr int SP = POL;
+  // fused bottleneck tails (NT1 > 0): y (this block's output, re-read only two launches later
+  // as the next residual, by then long out of the 256 MB Infinity Cache) is stored and the
+  // residual loaded non-temporal, so z -- read by the very next launch (the 3x3) -- stays there
+  constexpr int YP = NT1 > 0 ? 2 : SP;
   static_assert(TM >= 1 && TN >= 1 && PER >= 1 && D >= 2 && D <= 6, "tile");
   // one LDS array (guide §5 trap (a)): [D ring slots: A | B] [resident B] [C tile]
   extern __shared__ __attribute__((aligned(16))) bf16 smem[];
@@ -187,7 +191,7 @@ void conv_stream_kernel(const KvConvParams p) {
         const int idx = tid + 256 * j;
         const int m = m0 + idx / CPR, n = n0 + (idx % CPR) * 8;
         const int off = (last && m < p.M && n < p.Cout) ? (m * p.ldr + p.r_coff + n) * 2 : kOOB;
-        rdst[j] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, SP);
+        rdst[j] = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, YP);
       }
     }
   };
@@ -378,7 +382,7 @@ void conv_stream_kernel(const KvConvParams p) {
         for (int e = 0; e < 8; ++e) v[e] = f2bf(act_c<act2>((float)v[e] + (float)rv[e]));
       }
       const int off = (m < p.M && n < p.Cout) ? (m * p.ldy + p.y_coff + n) * 2 : kOOB;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ry, off, 0, SP);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ry, off, 0, YP);
       if constexpr (NT1 > 0) *reinterpret_cast<bf16x8*>(Cs + ml * CS + ch * 8) = v;
     }
     if constexpr (NT1 > 0) tail(m0);
