@@ -68,6 +68,14 @@ __device__ __forceinline__ void kv_lds_dma16(kv_i32x4 rs, void* lds, int voff) {
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
                :: "s"(m0), "v"(voff), "s"(rs) : "memory", "m0");
 }
+// ... non-temporal: a once-read stream (a fused tail's residual) that should not displace the
+// next launch's input from the Infinity Cache
+__device__ __forceinline__ void kv_lds_dma16_nt(kv_i32x4 rs, void* lds, int voff) {
+  const unsigned m0 = __builtin_amdgcn_readfirstlane(
+      (unsigned)(unsigned long long)(__attribute__((address_space(3))) void*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds"
+               :: "s"(m0), "v"(voff), "s"(rs) : "memory", "m0");
+}
 #pragma clang diagnostic pop
 
 // Registers loaded once per kernel (weights, biases) and read inside a loop that also has

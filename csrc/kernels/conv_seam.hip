@@ -246,7 +246,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(con
     for (int i = 0; i < 2; ++i) {
       const int n = tt * 64 + lc8[i];
       const int v = (tt < ntiles && n < Cout && r_src[i] != kSmOOB) ? r_src[i] + tt * 128 : kSmOOB;
-      kv_lds_dma16(rr, dst + (wv * 2 + i) * 1024, v);
+      kv_lds_dma16_nt(rr, dst + (wv * 2 + i) * 1024, v);  // see the y store
     }
   };
 
@@ -449,7 +449,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(con
             const bf16x8 v = *reinterpret_cast<const bf16x8*>(Rs + row * 128 + ((c ^ sm_sw(row)) << 4));
             const int m = m0 + row, n = t * 64 + c * 8;
             const int off = (m < p.M && n < Cout) ? (m * p.ldy + p.y_coff + n) * 2 : kSmOOB;
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(kv_i32x4, v), ry, off, 0, 0);
+            // y non-temporal: re-read only as the residual two launches later (by then out
+            // of the Infinity Cache anyway); z, read by the very next launch, stays cached
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(kv_i32x4, v), ry, off, 0, 2);
           }
         }
         if constexpr (j == 0) {
