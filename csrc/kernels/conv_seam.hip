@@ -288,7 +288,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void conv_seam_kernel(con
       for (int i = 0; i < 2; ++i) {
         char* dst = lds + kc * (BM * 128) + (wv * 2 + i) * 1024;
         const int v = (arow_off[i] != kSmOOB && kc * 64 + lc8[i] < p.Cin) ? arow_off[i] + kc * 128 : kSmOOB;
-        kv_lds_dma16(rx, dst, v);
+        kv_lds_dma16_nt(rx, dst, v);  // A: read here for the last time (see the y store)
       }
   }
 #pragma unroll

@@ -100,8 +100,9 @@ void conv_stream_kernel(const KvConvParams p) {
   // cache policy of the streamed (read-once / write-once) bytes: 0 default, 2 = nt
   constexpr int SP = POL;
   // fused bottleneck tails (NT1 > 0): y (this block's output, re-read only two launches later
-  // as the next residual, by then long out of the 256 MB Infinity Cache) is stored and the
-  // residual loaded non-temporal, so z -- read by the very next launch (the 3x3) -- stays there
+  // as the next residual, by then long out of the 256 MB Infinity Cache) is stored, and the
+  // activations read here for the last time (A, the downsample source, the residual) are
+  // loaded non-temporal, so z -- read by the very next launch (the 3x3) -- stays there
   constexpr int YP = NT1 > 0 ? 2 : SP;
   static_assert(TM >= 1 && TN >= 1 && PER >= 1 && D >= 2 && D <= 6, "tile");
   // one LDS array (guide §5 trap (a)): [D ring slots: A | B] [resident B] [C tile]
@@ -167,7 +168,7 @@ void conv_stream_kernel(const KvConvParams p) {
           const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
           v = (((img * p.H2 + ho * p.stride2) * p.W2 + wo * p.stride2) * p.ldx2 + a_lc[i] * 8) * 2;
         }
-        dma16<SP>(rx2, As + (wv * A_INS + i) * 512, v, (kbase - p.K1) * 2);
+        dma16<YP>(rx2, As + (wv * A_INS + i) * 512, v, (kbase - p.K1) * 2);
       }
     } else {
 #pragma unroll
@@ -175,7 +176,7 @@ void conv_stream_kernel(const KvConvParams p) {
         const int m = m0 + (wv * A_INS + i) * 8 + lrow;
         const bool ok = tv && m < p.M && (MODE == 4 || kbase + a_lc[i] * 8 < p.Cin);
         const int v = ok ? (m * p.ldx + p.x_coff + a_lc[i] * 8) * 2 : kOOB;
-        dma16<SP>(rx, As + (wv * A_INS + i) * 512, v, kbase * 2);
+        dma16<YP>(rx, As + (wv * A_INS + i) * 512, v, kbase * 2);
       }
     }
     if (!BRES) {
