@@ -135,18 +135,24 @@ write_files:
     permissions: "0755"
     content: |
       #!/bin/sh
-      # Wait for the VFIO-passed MI355X to be bound by amdgpu inside the guest.
-      want=${1:-1}; wait_s=${2:-120}; t=0
+      # Wait for the VFIO-passed MI355X to be bound by amdgpu inside the guest.  Runs on
+      # EVERY boot (kvedge-gpu.service), so gpu.json and the gpu_ready / gpu_missing stamp
+      # describe this boot: after a cold migration the re-attached GPU is proven here, not
+      # by the scheduler's allocation.
+      want=${1:-1}; wait_s=${2:-120}; t=0; n=0
+      boot=$(cat /proc/sys/kernel/random/boot_id 2>/dev/null)
+      mkdir -p /var/lib/kvedge
       while [ "$t" -lt "$wait_s" ]; do
         n=$(ls /dev/dri/renderD* 2>/dev/null | wc -l)
         if [ "$want" -eq 0 ] || { [ -e /dev/kfd ] && [ "$n" -ge "$want" ]; }; then
-          echo "{\"kfd\": $([ -e /dev/kfd ] && echo true || echo false), \"render_nodes\": $n, \"wanted\": $want, \"waited_s\": $t}" > /var/lib/kvedge/gpu.json
+          echo "{\"kfd\": $([ -e /dev/kfd ] && echo true || echo false), \"render_nodes\": $n, \"wanted\": $want, \"waited_s\": $t, \"boot_id\": \"$boot\"}" > /var/lib/kvedge/gpu.json
           /usr/local/sbin/kvedge-stamp gpu_ready
           exit 0
         fi
         sleep 1; t=$((t+1))
       done
-      echo "{\"kfd\": false, \"render_nodes\": $n, \"wanted\": $want, \"waited_s\": $t, \"error\": \"timeout\"}" > /var/lib/kvedge/gpu.json
+      echo "{\"kfd\": $([ -e /dev/kfd ] && echo true || echo false), \"render_nodes\": $n, \"wanted\": $want, \"waited_s\": $t, \"boot_id\": \"$boot\", \"error\": \"timeout\"}" > /var/lib/kvedge/gpu.json
+      /usr/local/sbin/kvedge-stamp gpu_missing
       exit 1
   - path: /usr/local/sbin/kvedge-ready
     permissions: "0755"
@@ -179,18 +185,27 @@ write_files:
       # heartbeat and boot-timing live on the persistent boot disk, so a previous boot's
       # fresh heartbeat or iotedge_check_pass line must not make a restarted VMI Ready.
       #   ready = this boot's module heartbeat is fresh (or, with no module, this boot's
-      #           iotedge check passed)
+      #           iotedge check passed); with gpu.count > 0 also this boot's gpu_ready
+      #           stamp and a heartbeat from a module serving on the GPU
       #   live  = no STALE heartbeat of this boot (none yet, or a previous boot's: booting)
-      hb=/var/lib/kvedge/heartbeat; max={{ $v.health.heartbeatMaxAgeS }}
+      hb=/var/lib/kvedge/heartbeat; bt=/var/lib/kvedge/boot-timing; max={{ $v.health.heartbeatMaxAgeS }}
       boot=$(cat /proc/sys/kernel/random/boot_id 2>/dev/null)
       age() { echo $(( $(date +%s) - $(stat -c %Y "$hb") )); }
       this_boot() { [ -n "$boot" ] && [ -f "$hb" ] && grep -qF "\"boot_id\": \"$boot\"" "$hb"; }
+      stamped() { [ -n "$boot" ] && awk -v s="$1" -v b="$boot" '$1==s && $3==b {f=1} END{exit !f}' "$bt" 2>/dev/null; }
+      {{- if gt (int $v.gpu.count) 0 }}
+      gpu_ok() { stamped gpu_ready; }
+      module_gpu() { grep -qF '"device": "cuda"' "$hb"; }
+      {{- else }}
+      gpu_ok() { true; }
+      module_gpu() { true; }
+      {{- end }}
       case "$1" in
         ready)
       {{- if $v.module.enabled }}
-          this_boot && [ "$(age)" -le "$max" ] ;;
+          this_boot && [ "$(age)" -le "$max" ] && gpu_ok && module_gpu ;;
       {{- else }}
-          [ -n "$boot" ] && awk -v b="$boot" '$1=="iotedge_check_pass" && $3==b {f=1} END{exit !f}' /var/lib/kvedge/boot-timing 2>/dev/null ;;
+          stamped iotedge_check_pass && gpu_ok ;;
       {{- end }}
         live)
           ! this_boot || [ "$(age)" -le "$max" ] ;;
@@ -208,6 +223,18 @@ write_files:
       RemainAfterExit=yes
       Restart=on-failure
       RestartSec=5
+      [Install]
+      WantedBy=multi-user.target
+  - path: /etc/systemd/system/kvedge-gpu.service
+    content: |
+      [Unit]
+      Description=kvedge: wait for the passed-through MI355X on every boot (gpu_ready stamp)
+      After=systemd-modules-load.service systemd-udev-settle.service
+      Before=aziot-edged.service kvedge-ready.service
+      [Service]
+      Type=oneshot
+      ExecStart=/usr/local/sbin/kvedge-gpu-check {{ $v.gpu.count }} {{ $v.guest.gpuWaitSeconds }}
+      RemainAfterExit=yes
       [Install]
       WantedBy=multi-user.target
   - path: /etc/systemd/system/kvedge-ready.service
@@ -234,7 +261,7 @@ runcmd:
   # exec probes run through the QEMU guest agent (pre-baked; apt only without the image)
   - [sh, -c, "command -v qemu-ga >/dev/null || {{ if $v.image.prebaked }}true{{ else }}apt-get install -y qemu-guest-agent{{ end }}; systemctl enable --now qemu-guest-agent || true"]
 {{- end }}
-  - [/usr/local/sbin/kvedge-gpu-check, "{{ $v.gpu.count }}", "{{ $v.guest.gpuWaitSeconds }}"]
+  - [systemctl, enable, --now, kvedge-gpu.service]
   - [/usr/local/sbin/kvedge-stamp, runcmd_done]
 final_message: "kvedge guest {{ $v.guest.hostname }}{{ include "kvedge.sfx" . }} up after $UPTIME s"
 {{- end -}}

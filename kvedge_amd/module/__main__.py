@@ -13,7 +13,7 @@ import sys
 import time
 
 from .. import parallel
-from .app import ModuleApp
+from .app import GpuUnavailableError, ModuleApp
 from .config import ModuleConfig
 from .transport import make_transport
 
@@ -93,6 +93,9 @@ def main(argv=None):
     ap.add_argument("--tune-cache", default=os.environ.get("KVEDGE_TUNE_CACHE",
                                                            "/var/lib/kvedge/tune-cache.json"),
                     help="autotuner picks on the persistent disk ('' = always re-tune)")
+    ap.add_argument("--require-gpu", type=int, default=int(os.environ.get("KVEDGE_REQUIRE_GPU", "0") or 0),
+                    help="exit non-zero unless at least this many GPUs are visible (the chart "
+                         "sets KVEDGE_REQUIRE_GPU from gpu.count; 0 = allow the CPU)")
     a = ap.parse_args(argv)
     di = parallel.init_from_env(prefer_gpu=True)
     cfg = ModuleConfig(model=a.model, batch=a.batch, dtype=a.dtype, seed=a.seed,
@@ -103,11 +106,19 @@ def main(argv=None):
                        refine_s=a.refine_s).validate()
     # one IoT Edge identity per VM: only local rank 0 talks to edgeHub
     kind = a.transport if di.local_rank == 0 or a.transport != "azure" else "null"
-    app = ModuleApp(make_transport(kind), cfg, state_path=a.state,
-                    stamp_path=a.stamps or None, heartbeat_path=a.heartbeat or None,
-                    tune_cache=a.tune_cache or None)
-    # cold-start legs: this process's start (kernel start time) and the end of imports
-    app._stamp("module_process_start", _process_start_epoch())
+    try:
+        app = ModuleApp(make_transport(kind), cfg, state_path=a.state,
+                        stamp_path=a.stamps or None, heartbeat_path=a.heartbeat or None,
+                        tune_cache=a.tune_cache or None, require_gpus=a.require_gpu)
+    except GpuUnavailableError as e:
+        print(str(e), file=sys.stderr, flush=True)
+        parallel.shutdown()
+        return 3
+    # cold-start legs: this process's start (kernel start time) and the end of imports; no
+    # process-start stamp when /proc cannot say (a stamp at "now" would corrupt the legs)
+    t_start = _process_start_epoch()
+    if t_start is not None:
+        app._stamp("module_process_start", t_start)
     app._stamp("module_imported", _T_IMPORTED)
     # SIGTERM (edgeAgent stop, VM shutdown) only votes to stop: the replicas leave the
     # loop together at the next control boundary, so the final report's collectives match

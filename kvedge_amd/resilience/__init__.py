@@ -93,6 +93,10 @@ class PVC:
     # the module heartbeat file on the boot disk (/var/lib/kvedge/heartbeat): (boot id of
     # the boot that wrote it, time).  It PERSISTS across VMI restarts, like the disk.
     heartbeat: Optional[Tuple[int, float]] = None
+    # device the module of that boot serves on ("cuda" / "cpu"), as in the heartbeat JSON
+    heartbeat_device: str = ""
+    # boot id whose kvedge-gpu-check stamped gpu_ready (boot-timing on this disk)
+    gpu_ready_boot: Optional[int] = None
 
 
 @dataclass
@@ -112,6 +116,7 @@ class VMI:
     phase: str = "Running"
     boot_id: int = 0        # /proc/sys/kernel/random/boot_id of this boot
     booted_at: float = 0.0
+    gpus_visible: int = 0   # MI355X the guest's amdgpu bound (/dev/kfd + render nodes)
 
 
 @dataclass
@@ -147,6 +152,8 @@ class Cluster(Protocol):
 
     def wait_module_ready(self, vm_name: str) -> bool: ...
 
+    def why_not_ready(self, vm_name: str) -> str: ...
+
 
 # event name -> phase it ends (Recovery.phases): the time since the previous event
 PHASES = {"stopped": "stop", "scheduled": "schedule", "pvc_attached": "pvc_attach",
@@ -166,6 +173,12 @@ class FakeCluster:
         self.timings = timings or Timings()
         self.events: List[Event] = []
         self.unhealthy: set = set()  # fault injection: modules that never turn healthy
+        # fault injection: nodes whose VFIO hand-over leaves the guest without its GPU (the
+        # scheduler allocates the device, the guest's amdgpu never binds it)
+        self.reattach_fails: set = set()
+        # the module's KVEDGE_REQUIRE_GPU (chart: set from gpu.count).  False models the
+        # round-5 module that silently served on the CPU without a GPU
+        self.require_gpu = True
         self._boots = 0
 
     def log(self, vm, what, detail=""):
@@ -195,18 +208,43 @@ class FakeCluster:
         self.node_down(node)
 
     def module_heartbeat(self, vm_name: str) -> None:
-        """The running module rewrites its heartbeat (with this boot's id) on the disk."""
+        """The running module rewrites its heartbeat (with this boot's id and the device it
+        serves on) on the disk."""
         vmi = self.vmis[vm_name]
-        self.pvcs[self.vms[vm_name].pvc].heartbeat = (vmi.boot_id, self.t)
+        pvc = self.pvcs[self.vms[vm_name].pvc]
+        pvc.heartbeat = (vmi.boot_id, self.t)
+        pvc.heartbeat_device = "cuda" if vmi.gpus_visible > 0 else "cpu"
+
+    def _module_serves(self, vm_name: str) -> bool:
+        """Whether this boot's module starts at all: one that requires its GPU exits
+        non-zero when the guest shows fewer devices than the VM was given."""
+        vmi, vm = self.vmis[vm_name], self.vms[vm_name]
+        return not (self.require_gpu and vmi.gpus_visible < vm.gpus)
 
     def probe_ready(self, vm_name: str, max_age_s: float = 120.0) -> bool:
         """``kvedge-health ready`` (chart _helpers.tpl): a heartbeat written during THIS
         boot and no older than ``max_age_s``.  A fresh heartbeat left on the persistent
-        disk by the previous boot does not count (VERDICT r4 next #3)."""
+        disk by the previous boot does not count.  A GPU VM also
+        needs this boot's gpu_ready stamp and a heartbeat from a module on the GPU
+        (VERDICT r5 next #2)."""
         vmi = self.vmis.get(vm_name)
-        hb = self.pvcs[self.vms[vm_name].pvc].heartbeat
-        return (vmi is not None and hb is not None and hb[0] == vmi.boot_id
-                and self.t - hb[1] <= max_age_s)
+        pvc = self.pvcs[self.vms[vm_name].pvc]
+        hb = pvc.heartbeat
+        ok = (vmi is not None and hb is not None and hb[0] == vmi.boot_id
+              and self.t - hb[1] <= max_age_s)
+        if ok and self.vms[vm_name].gpus > 0:
+            ok = pvc.gpu_ready_boot == vmi.boot_id and pvc.heartbeat_device == "cuda"
+        return ok
+
+    def why_not_ready(self, vm_name: str) -> str:
+        vmi = self.vmis.get(vm_name)
+        if vmi is None:
+            return "no VMI"
+        pvc = self.pvcs[self.vms[vm_name].pvc]
+        if self.vms[vm_name].gpus > 0 and pvc.gpu_ready_boot != vmi.boot_id:
+            return (f"GPU not re-attached: the guest on {vmi.node} shows {vmi.gpus_visible} of "
+                    f"{self.vms[vm_name].gpus} MI355X (gpu_missing this boot)")
+        return "readiness probe failing"
 
     def wait_module_ready(self, vm_name: str) -> bool:
         """Poll the VMI's readiness probe until it passes, or the timeout.  The module of
@@ -217,15 +255,16 @@ class FakeCluster:
             self.log(vm_name, "module_not_ready", "no VMI")
             return False
         t_end = self.t + self.timings.module_ready_timeout
-        t_hb = (None if vm_name in self.unhealthy
+        t_hb = (None if vm_name in self.unhealthy or not self._module_serves(vm_name)
                 else vmi.booted_at + self.timings.module_ready)
         while not self.probe_ready(vm_name):
             if t_hb is not None and t_hb <= t_end:
                 self.t = max(self.t, t_hb)
                 self.module_heartbeat(vm_name)
-                continue
+                t_hb = None  # the heartbeat stays fresh; if the probe still fails, it is
+                continue     # for another reason (no GPU evidence): wait out the timeout
             self.t = t_end
-            self.log(vm_name, "module_not_ready", "readiness probe failing")
+            self.log(vm_name, "module_not_ready", self.why_not_ready(vm_name))
             return False
         self.log(vm_name, "module_ready", vmi.node)
         return True
@@ -281,9 +320,18 @@ class FakeCluster:
         self.log(vm_name, "gpu_attached", ",".join(ids))
         self.advance(tm.guest_boot)
         self._boots += 1
-        vmi = VMI(vm_name, node.name, ids, boot_id=self._boots, booted_at=self.t)
+        seen = 0 if node.name in self.reattach_fails else len(ids)
+        vmi = VMI(vm_name, node.name, ids, boot_id=self._boots, booted_at=self.t,
+                  gpus_visible=seen)
         self.vmis[vm_name] = vmi
         self.log(vm_name, "running", node.name)
+        # kvedge-gpu.service of this boot (inside guest_boot): stamps what the guest sees
+        if vm.gpus > 0:
+            if seen >= vm.gpus:
+                pvc.gpu_ready_boot = vmi.boot_id
+                self.log(vm_name, "gpu_ready", f"{seen} visible")
+            else:
+                self.log(vm_name, "gpu_missing", f"{seen} of {vm.gpus} visible on {node.name}")
         return vmi
 
     def stop(self, vm_name: str, graceful: bool = True):
@@ -315,6 +363,11 @@ class FakeCluster:
         inside the guest, ...): the readiness probe keeps failing."""
         self.unhealthy.add(vm_name)
 
+    def fail_reattach(self, node: str):
+        """VFIO hand-over on ``node`` leaves guests without their GPU: the scheduler still
+        allocates the device (``gpu_attached``), but kvedge-gpu-check times out."""
+        self.reattach_fails.add(node)
+
     def gpu_failure(self, gpu_id: str):
         node = self.nodes[gpu_id.split("/")[0]]
         vm = node.used.get(gpu_id)
@@ -335,6 +388,10 @@ class Recovery:
     reason: str = ""
     gpu_ids: List[str] = field(default_factory=list)
     module_ready: bool = False
+    # placements tried: a boot whose guest never showed its GPU is retried once on
+    # another node (GPU evidence from inside the guest, not the scheduler's allocation)
+    attempts: int = 1
+    gpu_ready: bool = False
     # seconds per phase, in order (keys of PHASES' values): stop, schedule, pvc_attach,
     # gpu_attach, vmi_running, module_ready -- the phases this cluster can observe
     phases: Dict[str, float] = field(default_factory=dict)
@@ -346,17 +403,50 @@ class ResilienceController:
     counts as done only when the module is healthy again (``Cluster.wait_module_ready``:
     the VMI's readiness probe), not when the VMI is merely Running."""
 
-    def __init__(self, cluster: Cluster):
+    def __init__(self, cluster: Cluster, retry_gpu_missing: bool = True):
         self.c = cluster
+        self.retry_gpu_missing = retry_gpu_missing
+
+    def _gpu_missing(self, name: str, since: float) -> bool:
+        return any(e.vm == name and e.what == "gpu_missing" and e.t >= since
+                   for e in self.c.events)
 
     def _finish(self, name: str, vmi: Optional[VMI], t0: float, from_node: Optional[str],
                 refused: bool = False) -> Recovery:
         ready = vmi is not None and self.c.wait_module_ready(name)
-        reason = "" if ready else (self._why(name) if vmi is None else
-                                   "module not ready: readiness probe failing")
+        attempts = 1
+        if (not ready and vmi is not None and self.retry_gpu_missing
+                and self._gpu_missing(name, t0)):
+            # the guest booted without its MI355X: release it and place the VM elsewhere
+            bad = vmi.node
+            self.c.log(name, "retry", f"GPU not visible in the guest on {bad}")
+            self.c.stop(name, graceful=False)
+            vmi = self.c.start(name, exclude=(bad,))
+            attempts = 2
+            ready = vmi is not None and self.c.wait_module_ready(name)
+        if ready:
+            reason = ""
+        elif vmi is None:
+            reason = self._why(name)
+        else:
+            why = getattr(self.c, "why_not_ready", None)
+            reason = "module not ready: " + (why(name) if why else "readiness probe failing")
         return Recovery(name, ready, from_node, vmi.node if vmi else None, self.c.now() - t0,
                         refused, reason, vmi.gpu_ids if vmi else [], module_ready=ready,
+                        attempts=attempts, gpu_ready=ready or self._gpu_ready(name, t0),
                         phases=self.phases(name, t0))
+
+    def _gpu_ready(self, name: str, since: float) -> bool:
+        """The last boot since ``since`` stamped gpu_ready (a Ready VMI implies it: the
+        chart's readiness probe requires this boot's stamp on a GPU VM)."""
+        ok = False
+        for e in self.c.events:
+            if e.vm == name and e.t >= since:
+                if e.what == "running":
+                    ok = False
+                elif e.what in ("gpu_ready", "gpu_missing"):
+                    ok = e.what == "gpu_ready"
+        return ok
 
     def phases(self, vm: str, t0: float) -> Dict[str, float]:
         """Per-phase seconds of the recovery of ``vm`` that started at ``t0``."""

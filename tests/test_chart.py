@@ -108,7 +108,13 @@ def test_cloudinit_contract():
     assert "apt" not in ci  # pre-baked image: nothing to install at boot
     flat = [" ".join(map(str, c)) if isinstance(c, list) else c for c in ci["runcmd"]]
     assert any("enable --now kvedge-config.service" in c for c in flat)
-    assert any("kvedge-gpu-check 1" in c for c in flat)
+    # the GPU check is a per-boot systemd oneshot, not a once-per-
+    # instance runcmd line
+    assert any("enable --now kvedge-gpu.service" in c for c in flat)
+    assert not any("kvedge-gpu-check" in c for c in flat)
+    unit = files_of(ci)["/etc/systemd/system/kvedge-gpu.service"]
+    assert "ExecStart=/usr/local/sbin/kvedge-gpu-check 1 120" in unit
+    assert "WantedBy=multi-user.target" in unit and "Before=aziot-edged.service" in unit
     # not pre-baked: jammy/noble Microsoft repo + installs, never bionic
     _, objs2 = render(sets=["image.prebaked=false"])
     txt2, ci2 = _cloudinit(objs2)
@@ -234,6 +240,10 @@ def test_template_language_subset():
         r.render("{{ eq 1 \"1\" }}", {})
 
 
+def files_of(ci):
+    return {f["path"]: f["content"] for f in ci["write_files"]}
+
+
 def _fake_root_script(script: str, root) -> str:
     return (script.replace("/mnt/app-secret", f"{root}/mnt/app-secret")
             .replace("/etc/aziot", f"{root}/etc/aziot")
@@ -283,14 +293,17 @@ def test_cloudinit_scripts_in_fake_root(tmp_path):
     # GPU check: times out without devices, succeeds once /dev/kfd + a render node exist
     gpu = root / "gpu.sh"
     gpu.write_text(_fake_root_script(files["/usr/local/sbin/kvedge-gpu-check"], root))
+    (root / "boot_id").write_text("boot-A\n")
     r = subprocess.run(["sh", str(gpu), "1", "1"], capture_output=True)
     assert r.returncode == 1
+    assert json.loads((root / "var/lib/kvedge/gpu.json").read_text())["error"] == "timeout"
+    assert "gpu_missing" in (root / "var/lib/kvedge/boot-timing").read_text()
     (root / "dev/kfd").write_text("")
     (root / "dev/dri/renderD128").write_text("")
     r = subprocess.run(["sh", str(gpu), "1", "2"], capture_output=True)
     assert r.returncode == 0
     info = json.loads((root / "var/lib/kvedge/gpu.json").read_text())
-    assert info["kfd"] is True and info["render_nodes"] == 1
+    assert info["kfd"] is True and info["render_nodes"] == 1 and info["boot_id"] == "boot-A"
     stamps = (root / "var/lib/kvedge/boot-timing").read_text()
     assert "config_applied" in stamps and "gpu_ready" in stamps
 
@@ -471,7 +484,7 @@ def test_vmi_health_probes_and_heartbeat_script(tmp_path):
     from kvedge_amd.module.app import ModuleApp
     from kvedge_amd.module.transport import FakeTransport
 
-    _, objs = render()
+    _, objs = render(sets=["gpu.count=0"])  # CPU VM: the GPU evidence is the next test's
     spec = by_kind(objs, "VirtualMachine")[0]["spec"]["template"]["spec"]
     rp, lp = spec["readinessProbe"], spec["livenessProbe"]
     assert rp["exec"]["command"] == ["/usr/local/sbin/kvedge-health", "ready"]
@@ -518,7 +531,7 @@ def test_vmi_health_probes_and_heartbeat_script(tmp_path):
     app2.stop()
     assert probe("ready") == 0 and probe("live") == 0
     # module disabled: readiness = THIS boot's iotedge check passed
-    _, objs2 = render(sets=["module.enabled=false"])
+    _, objs2 = render(sets=["module.enabled=false", "gpu.count=0"])
     _, ci2 = _cloudinit(objs2)
     f2 = {f["path"]: f["content"] for f in ci2["write_files"]}
     sh.write_text(_fake_root_script(f2["/usr/local/sbin/kvedge-health"], tmp_path))
@@ -541,3 +554,79 @@ def test_vmi_health_probes_and_heartbeat_script(tmp_path):
     _, objs3 = render(sets=["health.enabled=false"])
     spec3 = by_kind(objs3, "VirtualMachine")[0]["spec"]["template"]["spec"]
     assert "readinessProbe" not in spec3 and "livenessProbe" not in spec3
+
+
+def test_health_requires_this_boots_gpu(tmp_path):
+    """VERDICT r5 next #2 (BASELINE config 5): with gpu.count > 0 a VMI is Ready only when
+    THIS boot's kvedge-gpu-check stamped gpu_ready and the module's heartbeat says it
+    serves on the GPU.  A module that fell back to the CPU, or a boot whose GPU never
+    showed up (failed re-attach), stays not-ready."""
+    import torch
+
+    from kvedge_amd.module.app import ModuleApp
+    from kvedge_amd.module.transport import FakeTransport
+
+    _, objs = render()  # gpu.count = 1 (default)
+    _, ci = _cloudinit(objs)
+    files = files_of(ci)
+    (tmp_path / "var/lib/kvedge").mkdir(parents=True)
+    (tmp_path / "dev/dri").mkdir(parents=True)
+    boot_id = tmp_path / "boot_id"
+    boot_id.write_text("boot-A\n")
+    for name, path in (("health.sh", "/usr/local/sbin/kvedge-health"),
+                       ("gpu.sh", "/usr/local/sbin/kvedge-gpu-check"),
+                       ("stamp", "/usr/local/sbin/kvedge-stamp")):
+        (tmp_path / name).write_text(_fake_root_script(files[path], tmp_path))
+        (tmp_path / name).chmod(0o755)
+    probe = lambda: subprocess.run(["sh", str(tmp_path / "health.sh"), "ready"]).returncode  # noqa
+    gpu_check = lambda: subprocess.run(["sh", str(tmp_path / "gpu.sh"), "1", "1"],  # noqa
+                                       capture_output=True).returncode
+    hb = tmp_path / "var/lib/kvedge/heartbeat"
+    app = ModuleApp(FakeTransport({"model": "simulated-temperature"}), device="cpu",
+                    heartbeat_path=str(hb), boot_id_path=str(boot_id)).start()
+    app.run(max_steps=1)
+    # (1) a fresh heartbeat of this boot from a module on the CPU: not ready, even with
+    # this boot's gpu_ready stamp
+    (tmp_path / "dev/kfd").write_text("")
+    (tmp_path / "dev/dri/renderD128").write_text("")
+    assert gpu_check() == 0
+    assert json.loads(hb.read_text())["device"] == "cpu"
+    assert probe() != 0
+    # (2) the module serves on the GPU (the heartbeat writer of a cuda-device module) and
+    # this boot's gpu_ready exists: ready
+    app.device, app.gpus = torch.device("cuda"), 1
+    app._heartbeat({})
+    beat = json.loads(hb.read_text())
+    assert beat["device"] == "cuda" and beat["gpus"] == 1
+    assert probe() == 0
+    # (3) the VMI restarted on another node and the GPU did not come back: the previous
+    # boot's gpu_ready does not count, this boot's check stamps gpu_missing
+    boot_id.write_text("boot-B\n")
+    (tmp_path / "dev/kfd").unlink()
+    app.boot_id = "boot-B"
+    app._heartbeat({})  # even a (hypothetical) heartbeat claiming cuda for this boot
+    assert gpu_check() == 1
+    assert probe() != 0
+    bt = (tmp_path / "var/lib/kvedge/boot-timing").read_text().splitlines()
+    assert bt[-1].split()[0] == "gpu_missing" and bt[-1].split()[2] == "boot-B"
+    # (4) the GPU appears within this boot: ready again
+    (tmp_path / "dev/kfd").write_text("")
+    assert gpu_check() == 0
+    assert probe() == 0
+    app.stop()
+    # module disabled, GPU VM: this boot's iotedge check AND this boot's gpu_ready
+    _, objs2 = render(sets=["module.enabled=false"])
+    f2 = files_of(_cloudinit(objs2)[1])
+    (tmp_path / "health.sh").write_text(_fake_root_script(f2["/usr/local/sbin/kvedge-health"], tmp_path))
+    boot_id.write_text("boot-C\n")
+    subprocess.run(["sh", str(tmp_path / "stamp"), "iotedge_check_pass"], check=True)
+    assert probe() != 0
+    assert gpu_check() == 0
+    assert probe() == 0
+    # the module manifest carries the GPU requirement (and not on a CPU VM)
+    def mod_env(objs_):
+        cm = [o for o in by_kind(objs_, "ConfigMap") if o["metadata"]["name"].endswith("module-deployment")][0]
+        dep = json.loads(cm["data"]["deployment.json"])
+        return dep["modulesContent"]["$edgeAgent"]["properties.desired"]["modules"]["kvedge"]["env"]
+    assert mod_env(objs)["KVEDGE_REQUIRE_GPU"]["value"] == "1"
+    assert "KVEDGE_REQUIRE_GPU" not in mod_env(render(sets=["gpu.count=0"])[1])

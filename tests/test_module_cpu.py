@@ -357,3 +357,34 @@ def test_refine_budget_config():
     ModuleConfig(refine_s=0.0).validate()
     with pytest.raises(ValueError):
         ModuleConfig(refine_s=-1.0).validate()
+
+
+def test_module_refuses_cpu_when_gpu_required(tmp_path, capsys, monkeypatch):
+    """a GPU VM whose MI355X did not come back must not serve on the CPU.
+    With KVEDGE_REQUIRE_GPU (the chart sets it from gpu.count) the module exits non-zero
+    with a clear error and writes no heartbeat; without it, the heartbeat names the
+    device it runs on, so kvedge-health can tell a CPU fallback apart."""
+    import json
+
+    import pytest
+
+    from kvedge_amd.module import __main__ as entry
+    from kvedge_amd.module.app import GpuUnavailableError, ModuleApp
+    from kvedge_amd.module.transport import FakeTransport
+
+    with pytest.raises(GpuUnavailableError, match="refusing to serve on the CPU"):
+        ModuleApp(FakeTransport({"model": "simulated-temperature"}), device="cpu", require_gpus=1)
+    hb = tmp_path / "heartbeat"
+    monkeypatch.setenv("KVEDGE_REQUIRE_GPU", "1")
+    rc = entry.main(["--transport", "fake", "--model", "simulated-temperature", "--steps", "1",
+                     "--heartbeat", str(hb), "--state", str(tmp_path / "s.json"),
+                     "--stamps", str(tmp_path / "bt"), "--tune-cache", ""])
+    assert rc == 3 and not hb.exists()
+    assert "refusing to serve on the CPU" in capsys.readouterr().err
+    monkeypatch.setenv("KVEDGE_REQUIRE_GPU", "0")
+    rc = entry.main(["--transport", "fake", "--model", "simulated-temperature", "--steps", "1",
+                     "--heartbeat", str(hb), "--state", str(tmp_path / "s.json"),
+                     "--stamps", str(tmp_path / "bt"), "--tune-cache", ""])
+    assert rc == 0
+    beat = json.loads(hb.read_text())
+    assert beat["device"] == "cpu" and beat["gpus"] == 0
