@@ -208,8 +208,9 @@ void conv_dual2(const at::Tensor& x, int64_t x_coff, int64_t K1, const at::Tenso
                     (x2.size(2) + stride2 - 1) / stride2 == Wo,
                 "kvedge: x2 geometry vs stride");
   }
-  TORCH_CHECK(x.numel() * 2 < (1ll << 31) && x2.numel() * 2 < (1ll << 31) && y.numel() * 2 < (1ll << 31),
-              "kvedge: conv_dual2 operands exceed 2 GiB");
+  // no whole-tensor cap: kv_conv2d splits a batch whose per-image operands fit a launch
+  // into image chunks (x2 advanced per image, up2 included) and refuses (rc -9) only an
+  // IMAGE too large for 32-bit offsets -- the same contract as conv2d
   const c10::DeviceGuard g(x.device());
   KvConvParams p{};
   p.x = x.data_ptr();

@@ -136,18 +136,30 @@ def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
     if refine_iters is None:
         refine_iters = int(os.environ.get("KVEDGE_AUTOTUNE_REFINE_ITERS", "20"))
     ntiles = int(torch.ops.kvedge.conv_num_tiles())
-    sig = _cache_signature(ntiles, concurrency)
-    cache = {}
+    # A/B knob: tune over the first KVEDGE_TILE_LIMIT tiles only (e.g. without a new family).
+    # Applied BEFORE the cache signature: a limited run's picks never pass for a full run's
+    lim = int(os.environ.get("KVEDGE_TILE_LIMIT", "0"))
+    if 0 < lim < ntiles:
+        ntiles = lim
+    from .. import parallel
+
+    world = parallel.info().world_size if parallel.is_dist() else 1
+    sig = _cache_signature(ntiles, concurrency, world)
+    cache, cache_alts = {}, {}
     if cache_path and os.path.exists(cache_path):
         try:
             with open(cache_path) as f:
                 doc = json.load(f)
-            # picks are valid only for the same kernel library, tile table, device and
-            # concurrency; anything else (an older build, the old flat format) is ignored
+            # picks are valid only for the same kernel library, tile table, device,
+            # concurrency and world size; anything else (an older build, the old flat
+            # format) is ignored
             if isinstance(doc, dict) and doc.get("signature") == sig:
-                cache = {k: tuple(v) for k, v in doc.get("picks", {}).items()}
-        except (OSError, ValueError):
-            cache = {}
+                for k, v in doc.get("picks", {}).items():
+                    cache[k] = (v[0], v[1])
+                    if len(v) > 2 and isinstance(v[2], list):
+                        cache_alts[k] = [int(t) for t in v[2]]
+        except (OSError, ValueError, TypeError, IndexError):
+            cache, cache_alts = {}, {}
     with record_convs() as rec:
         model(example_input)
     torch.cuda.synchronize()
@@ -155,15 +167,9 @@ def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
     # EVERY rank -- data-parallel ranks must time the same keys (one all-reduce below)
     if cache and not all(repr(key) in cache for _, key, _ in rec):
         cache = {}
-    from .. import parallel
-
-    if parallel.is_dist() and parallel.allreduce_scalars(
-            [1.0 if cache else 0.0], op="min")[0] < 1.0:
-        cache = {}
-    # A/B knob: tune over the first KVEDGE_TILE_LIMIT tiles only (e.g. without a new family)
-    lim = int(os.environ.get("KVEDGE_TILE_LIMIT", "0"))
-    if 0 < lim < ntiles:
-        ntiles = lim
+    cache = _fleet_cache(cache, [repr(key) for _, key, _ in rec])
+    if not cache:
+        cache_alts = {}
     results: Dict = {}
     side = [torch.cuda.Stream() for _ in range(concurrency)] if concurrency > 1 else None
     timer = (lambda f, t, n: _time_concurrent(f, t, n, side)) if side else _time
@@ -221,24 +227,82 @@ def autotune(model: Callable, example_input: torch.Tensor, iters: int = 5,
         fin = sorted((ts[t], t) for t in range(ntiles) if ts[t] != float("inf"))
         if fin:
             alts[ks] = [t for us, t in fin if us <= fin[0][0] * (1.0 + ALT_TOL)][:1 + ALT_MAX]
+    alts.update({k: v for k, v in cache_alts.items() if k not in alts})
     for layer, key, fn in rec:
         ks = repr(key)
         layer.tile = (results.get(ks) or cache[ks])[0]
+        # runner-ups survive a warm restart (the cache keeps them), so the in-graph refine
+        # can still work within its budget on a cache hit
         layer.tile_alts = alts.get(ks, [layer.tile])
         layer.tile_us = (results.get(ks) or cache[ks])[1] or 0.0
         if ks not in results:
             results[ks] = cache[ks]
     if cache_path and todo and parallel.info().local_rank == 0:  # one writer per VM disk
-        try:
-            os.makedirs(os.path.dirname(cache_path) or ".", exist_ok=True)
-            cache.update(results)
-            tmp = cache_path + ".tmp"
-            with open(tmp, "w") as f:
-                json.dump({"signature": sig, "picks": cache}, f, indent=0)
-            os.replace(tmp, cache_path)
-        except OSError:
-            pass  # read-only disk: tuning still applied, just not remembered
+        cache.update(results)
+        _write_cache(cache_path, sig, {k: [v[0], v[1], alts.get(k, [v[0]])]
+                                       for k, v in cache.items()})
     return results
+
+
+def _fleet_cache(cache: Dict, keys) -> Dict:
+    """Data-parallel ranks use their tune caches only if EVERY rank has one covering
+    ``keys`` and all hold the SAME picks: VMs that each tuned alone earlier would pin
+    different tiles (split-K on one, not on the other) and break the bitwise replica check
+    (C4).  One min and one max all-reduce of a digest of the picks; otherwise every rank
+    drops its cache and re-tunes (identity when not distributed)."""
+    from .. import parallel
+
+    if not parallel.is_dist():
+        return cache
+    dg = _picks_digest(cache, keys) if cache else -1.0
+    lo, = parallel.allreduce_scalars([dg], op="min")
+    hi, = parallel.allreduce_scalars([dg], op="max")
+    return cache if lo >= 0 and lo == hi else {}
+
+
+def _picks_digest(cache: Dict, keys) -> float:
+    """Order-independent digest of the picks for ``keys`` as an exact float (52 bits), for
+    a min/max all-reduce agreement check across data-parallel ranks."""
+    import hashlib
+
+    doc = json.dumps(sorted((k, int(cache[k][0])) for k in set(keys) if k in cache))
+    return float(int(hashlib.sha256(doc.encode()).hexdigest()[:13], 16))
+
+
+def _write_cache(path: str, sig: str, picks: Dict) -> None:
+    """Atomically (re)write the tune cache.  The in-graph refined tiles of earlier engines
+    (other batches / stream counts) are kept while the signature still matches."""
+    try:
+        old = {}
+        if os.path.exists(path):
+            with open(path) as f:
+                old = json.load(f)
+        refined = old.get("refined", {}) if isinstance(old, dict) and old.get("signature") == sig else {}
+        _dump_atomic(path, {"signature": sig, "picks": picks, "refined": refined})
+    except (OSError, ValueError):
+        pass  # read-only disk: tuning still applied, just not remembered
+
+
+def _add_refined(path: str, key: str, rows) -> None:
+    """Store graph_refine's per-layer tiles under ``key`` in an existing tune cache (whose
+    picks the refined engine was tuned from); no cache file, nothing stored."""
+    try:
+        with open(path) as f:
+            doc = json.load(f)
+        if not isinstance(doc, dict) or "signature" not in doc:
+            return
+        doc.setdefault("refined", {})[key] = rows
+        _dump_atomic(path, doc)
+    except (OSError, ValueError):
+        pass
+
+
+def _dump_atomic(path: str, doc: Dict) -> None:
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(doc, f, indent=0)
+    os.replace(tmp, path)
 
 
 ALT_TOL = 0.25  # runner-ups within 25 % of a layer's best (isolated timing) are graph-tested
@@ -246,7 +310,7 @@ ALT_MAX = 2     # ... at most two per layer
 
 
 def graph_refine(engine, budget_s: float = 30.0, min_gain: float = 0.003,
-                 verbose: bool = False) -> Dict:
+                 verbose: bool = False, cache_path: str = None, ab=None) -> Dict:
     """In-graph tile refinement: the per-layer timing above measures a
     layer alone (or as concurrent copies of itself), but in the bench graph each kernel
     runs next to the previous and next layer of its own slice and whatever the other
@@ -256,28 +320,40 @@ def graph_refine(engine, budget_s: float = 30.0, min_gain: float = 0.003,
     step graph is re-captured with the runner-up and timed against the current graph,
     replays interleaved A B B A ... on the same stream (drift hits both alike).  A change
     is kept only if the WHOLE STEP gets faster by more than ``min_gain`` in two separate
-    measurements.  Layers with the same shape key keep separate picks.  Stops at
-    ``budget_s``.  Returns {"trials", "kept", "step_ms_before", "step_ms_after"}."""
+    measurements.  Stops at ``budget_s``.
+
+    Verify before commit: when anything was kept, the refined graph is
+    A/B-timed once more against the ORIGINAL capture; unless it wins by ``min_gain`` every
+    layer's tile and the original graph are restored.  ``step_ms_before`` /
+    ``step_ms_after`` come from that one interleaved measurement (original vs final; the
+    same graph twice when nothing was kept).  Kept tiles go to ``cache_path`` (per layer
+    ordinal, per batch x streams), so a warm restart reuses them.  ``ab``: timing hook
+    (tests).  Returns {"trials", "kept", "reverted", "step_ms_before", "step_ms_after"}."""
     import time as _time
 
-    layers = []
+    ab = ab or _ab
+    layers, order = [], []
     with record_convs() as rec:
         engine.model(engine.frames[:engine.batch // engine.n_streams])
-    torch.cuda.synchronize()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     seen = set()
     for layer, key, fn in rec:
-        if id(layer) in seen or len(getattr(layer, "tile_alts", ())) < 2:
+        if id(layer) in seen:
             continue
         seen.add(id(layer))
-        layers.append(layer)
+        order.append((layer, repr(key)))
+        if len(getattr(layer, "tile_alts", ())) >= 2:
+            layers.append(layer)
     layers.sort(key=lambda l: -(getattr(l, "tile_us", 0.0) or 0.0))  # largest first
     if not layers or engine.graph is None:
-        return {"trials": 0, "kept": 0}
+        return {"trials": 0, "kept": 0, "reverted": False}
     t_end = _time.perf_counter() + budget_s
-    cur, cur_out = engine.graph, engine.outputs
-    base = _replay_ms(cur, 3)
+    orig, orig_out = engine.graph, engine.outputs
+    orig_tiles = [(l, l.tile) for l, _ in order]
+    cur, cur_out = orig, orig_out
+    base = _replay_ms(cur, 3) if ab is _ab else 1.0
     rounds = max(4, min(40, int(200.0 / max(base, 1e-3))))
-    before = _ab(cur, cur, rounds)[0]
     trials = kept = 0
     from .. import parallel
 
@@ -310,14 +386,15 @@ def graph_refine(engine, budget_s: float = 30.0, min_gain: float = 0.003,
                 g = g_out = None
                 continue
             trials += 1
-            a, b = _ab(cur, g, rounds)
+            a, b = ab(cur, g, rounds)
             gain = fleet((a - b) / a, False)[0]
             if gain > min_gain:
-                a2, b2 = _ab(cur, g, 2 * rounds)
+                a2, b2 = ab(cur, g, 2 * rounds)
                 gain = min(gain, fleet((a2 - b2) / a2, False)[0])
             if gain > min_gain:
                 kept += 1
-                del cur, cur_out
+                if cur is not orig:
+                    del cur, cur_out
                 cur, cur_out = g, g_out
                 if verbose:
                     print(f"graph_refine: tile {old} -> {t}: step {a:.3f} -> {b:.3f} ms",
@@ -325,10 +402,59 @@ def graph_refine(engine, budget_s: float = 30.0, min_gain: float = 0.003,
             else:
                 layer.tile = old
                 del g, g_out
+    # final check: the refined graph against the original capture, one interleaved A/B
+    before, after = ab(orig, cur, 2 * rounds)
+    reverted = False
+    if kept:
+        gain = fleet((before - after) / before, False)[0]
+        if gain <= min_gain:  # the per-trial wins did not add up: keep the original
+            reverted = True
+            for l, t in orig_tiles:
+                l.tile = t
+            cur, cur_out = orig, orig_out
+            after = before
+    else:
+        before = after = round((before + after) / 2, 4)  # one graph: no difference to report
     engine.graph, engine.outputs = cur, cur_out  # a rejected capture last set outputs
-    after = _ab(cur, cur, rounds)[0]
-    return {"trials": trials, "kept": kept, "step_ms_before": round(before, 4),
-            "step_ms_after": round(after, 4)}
+    if cache_path and kept and not reverted and parallel.info().local_rank == 0:
+        # next to the per-key picks this engine was tuned from (same signature): a warm
+        # restart of the same batch x streams re-applies them (apply_refined)
+        _add_refined(cache_path, f"b{engine.batch}s{engine.n_streams}",
+                     [[i, k, l.tile] for i, (l, k) in enumerate(order)])
+    return {"trials": trials, "kept": 0 if reverted else kept, "reverted": reverted,
+            "step_ms_before": round(before, 4), "step_ms_after": round(after, 4)}
+
+
+def apply_refined(engine, cache_path: str) -> int:
+    """Re-apply the in-graph refined tiles a previous engine of the same batch x streams
+    stored in ``cache_path`` (graph_refine), layer by layer, when every layer's shape key
+    still matches.  Returns the number of layers whose tile changed."""
+    if not cache_path or not os.path.exists(cache_path):
+        return 0
+    try:
+        with open(cache_path) as f:
+            doc = json.load(f)
+        rows = doc.get("refined", {}).get(f"b{engine.batch}s{engine.n_streams}")
+    except (OSError, ValueError, AttributeError):
+        return 0
+    if not rows:
+        return 0
+    order = []
+    with record_convs() as rec:
+        engine.model(engine.frames[:engine.batch // engine.n_streams])
+    seen = set()
+    for layer, key, fn in rec:
+        if id(layer) not in seen:
+            seen.add(id(layer))
+            order.append((layer, repr(key)))
+    if len(rows) != len(order) or any(k != ok for (i, k, t), (_, ok) in zip(rows, order)):
+        return 0
+    n = 0
+    for (i, k, t), (layer, _) in zip(rows, order):
+        if layer.tile != t:
+            layer.tile = int(t)
+            n += 1
+    return n
 
 
 def _replay_ms(g, n: int) -> float:
@@ -359,9 +485,10 @@ def _ab(ga, gb, rounds: int):
     return med(ta), med(tb)
 
 
-def _cache_signature(ntiles: int, concurrency: int) -> str:
+def _cache_signature(ntiles: int, concurrency: int, world: int = 1) -> str:
     """Identity of what a cached pick depends on: the kernel library build (size and
-    mtime of the loaded .so), its tile table, the device, the timing concurrency."""
+    mtime of the loaded .so), its tile table (after KVEDGE_TILE_LIMIT), the device, the
+    timing concurrency and the data-parallel world (fleet-mean picks vs a lone tune)."""
     from .. import ops
 
     try:
@@ -370,4 +497,4 @@ def _cache_signature(ntiles: int, concurrency: int) -> str:
     except OSError:
         lib = "?"
     dev = torch.cuda.get_device_name() if torch.cuda.is_available() else "cpu"
-    return f"lib={lib};tiles={ntiles};conc={concurrency};dev={dev}"
+    return f"lib={lib};tiles={ntiles};conc={concurrency};world={world};dev={dev}"

@@ -36,10 +36,10 @@ class ModuleConfig:
     native_loop: bool = True     # GPU: replay the graph from the C++ serve loop
     steps_per_poll: int = 1      # graph replays per module step (native loop)
     # seconds of in-graph tile refinement when the engine is built (engine.prepare refine_s;
-    # 0 = off).  It times runner-up tiles inside the captured step: worth 2-3 % on YOLOv8n,
-    # ~0.1 % on ResNet-50, and it was 8.9 of the 12.6 s cold start at the bench's 30 s
-    # budget (profiles/r5_v14_module_cold_start.json)
-    refine_s: float = 3.0
+    # 0 = off, the default).  It times runner-up tiles inside the captured step; on the
+    # driver's fresh boxes it returned -0.5 .. +0.1 % (BENCH_r05 / r6 builder boxes) for
+    # 3.1 s of a 6.6 s cold start, so it is opt-in
+    refine_s: float = 0.0
     # multi-replica lockstep: module steps between control boundaries (0 = auto: every
     # step at world 1, 16 otherwise).  Twin patches, collective direct methods, report
     # decisions and stop requests are exchanged ONLY at these boundaries, so every rank

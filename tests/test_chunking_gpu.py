@@ -68,3 +68,26 @@ def test_batch_beyond_2gib_slice_parity(model, batch):
     cos = torch.nn.functional.cosine_similarity(big.flatten(), small.flatten(), dim=0)
     assert cos > 0.9999, float(cos)
     assert (big - small).abs().max() <= 2e-2 * small.abs().max() + 1e-3
+
+
+def test_conv_dual2_up2_chunked_bitwise_equal():
+    """conv_dual2 (the YOLO neck's upsample + concat folded into cv1) has no
+    whole-tensor 2 GiB cap any more; past the chunk size it runs as image-chunk launches
+    with x2 advanced per (half-size) image, bit-identical to one launch."""
+    g = torch.Generator().manual_seed(7)
+    N, H, W = 6, 40, 40
+    skip = torch.randn(N, H, W, 192, generator=g).to(torch.bfloat16).cuda()
+    low = torch.randn(N, H // 2, W // 2, 384, generator=g).to(torch.bfloat16).cuda()
+    w = (torch.randn(128, 64 + 256, generator=g) * 0.05).to(torch.bfloat16).cuda()
+    b = torch.randn(128, generator=g).cuda()
+    outs = []
+    for chunk in (0, 1 << 20):  # one launch; ~1 MB chunks (one 40x40x192 image = 600 KB)
+        torch.ops.kvedge.set_conv_chunk_bytes(chunk)
+        y = torch.full((N, H, W, 192), 3.0, dtype=torch.bfloat16, device="cuda")
+        ops.conv_dual2(skip, 64, low, w, b, ops.ACT_SILU, y, x_coff=128, x2_coff=128, y_coff=64,
+                       up2=True)
+        outs.append(y.cpu())
+    torch.ops.kvedge.set_conv_chunk_bytes(0)
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0], outs[1])
+    assert (outs[0][..., :64].float() == 3.0).all()

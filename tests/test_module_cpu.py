@@ -353,7 +353,7 @@ def test_refine_budget_config():
     """The module's in-graph refine budget is a validated twin/CLI key (0 = off)."""
     import pytest
     from kvedge_amd.module.config import ModuleConfig
-    assert ModuleConfig().refine_s == 3.0
+    assert ModuleConfig().refine_s == 0.0  # opt-in (VERDICT r5 weak #4)
     ModuleConfig(refine_s=0.0).validate()
     with pytest.raises(ValueError):
         ModuleConfig(refine_s=-1.0).validate()
