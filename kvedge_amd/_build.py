@@ -86,6 +86,13 @@ if os.environ.get("KVEDGE_CHECKS", "0") not in ("", "0"):
     COMMON.append("-DKVEDGE_CHECKS=1")
     OBJ = os.path.join(ROOT, "build", "obj_checks")
     SO_PATH = os.path.join(PKG, "_C_checks.so")
+if os.environ.get("KVEDGE_VARIANT"):
+    # A/B variant of the library: extra compile flags (KVEDGE_CFLAGS, e.g. -DKV_GLDS_IL=1),
+    # own object dir, linked as kvedge_amd/_C_<variant>.so (load with KVEDGE_LIB=_C_<v>.so)
+    _v = os.environ["KVEDGE_VARIANT"]
+    COMMON.extend(os.environ.get("KVEDGE_CFLAGS", "").split())
+    OBJ = os.path.join(ROOT, "build", "obj_" + _v)
+    SO_PATH = os.path.join(PKG, f"_C_{_v}.so")
 
 
 def build(force: bool = False, jobs: int = 0, verbose: bool = False, asan: bool = False) -> str:

@@ -467,7 +467,14 @@ class KvYoloV8n:
         N = frames_u8.shape[0]
         return torch.cat([f.reshape(N, -1) for f in feats], dim=1)
 
+    # tests: a list here collects every call's three head maps.  Maps made during a hipGraph
+    # capture live in the graph's pool and hold each replay's values, so a parity test can
+    # read the GRAPH's own head maps instead of an eager re-run
+    keep_heads = None
+
     def __call__(self, frames_u8: torch.Tensor):
         feats = self.heads(self.stem_b1(frames_u8), b1_done=True)
+        if self.keep_heads is not None:
+            self.keep_heads.append(feats)
         boxes, scores, cls = ops.yolo_decode(feats, STRIDES, self.nc)
         return ops.nms(boxes, scores, cls, self.conf, self.iou, self.max_det)

@@ -94,56 +94,71 @@ def _check_resnet_slice(eng, kv, ref, B, S, sl):
 
 
 def test_yolov8n_bench_config_vs_fp32_reference():
+    """YOLOv8n at the bench configuration (batch AND stream slices), on the GRAPH's own head
+    maps -- kept alive from the capture, so they hold the replay's values -- for 32 images of
+    EACH stream slice:
+      * graph head maps vs the fp32 nn.Module on the same frames (cosine, box / class parts);
+      * the GPU decode of those maps vs the CPU reference decode;
+      * the CPU reference NMS of the GPU-decoded boxes vs the graph's own detections:
+        counts, and every kept box / score / class."""
     from kvedge_amd.models.yolov8 import KvYoloV8n, frames_to_yolo, init_yolov8n
+    from kvedge_amd.ops import reference as R
 
     ref = init_yolov8n(seed=0)
     kv = KvYoloV8n(ref, "cuda")
-    # the bench's exact configuration: batch AND stream slices
+    kv.keep_heads = []
     eng = InferenceEngine(kv, BENCH_BATCH["yolov8n"], 640, device="cuda", seed=0, use_graph=True,
                           streams=BENCH_STREAMS["yolov8n"])
     eng.prepare(warmup=1, autotune=True)
     assert eng.graph is not None and eng.tuning
+    S = eng.n_streams
+    graph_heads = kv.keep_heads[-S:]  # the capture's calls, one per stream slice, in order
+    kv.keep_heads = None
     eng.run()
     torch.cuda.synchronize()
-    n = 32
-    frames = eng.frames[:n].contiguous()
-    with torch.no_grad():
-        # the graph's own path (fused b0 + b1 stem), autotuned tiles, full batch
-        heads = kv.heads(kv.stem_b1(eng.frames), b1_done=True)
-        hr = ref(frames_to_yolo(frames.cpu()))
-    for g, r in zip(heads, hr):
-        g = g[:n].float().cpu()
-        r = r.permute(0, 2, 3, 1).float()
-        cos = torch.nn.functional.cosine_similarity(g.flatten(), r.flatten(), dim=0)
-        assert cos > 0.99, float(cos)
-        # class logits and box-DFL logits separately (different magnitudes)
-        for sl in (slice(0, 64), slice(64, None)):
-            c = torch.nn.functional.cosine_similarity(g[..., sl].flatten(),
-                                                      r[..., sl].flatten(), dim=0)
-            assert c > 0.99, (sl, float(c))
-    # post-processing at the bench configuration: the GPU decode + NMS
-    # kernels on these head maps == the CPU reference decode + NMS on the same maps
-    hs = [h[:n].contiguous() for h in heads]
-    b, s_, c = ops.yolo_decode(hs, (8, 16, 32), 80)
-    out, cnt = ops.nms(b, s_, c, kv.conf, kv.iou, kv.max_det)
-    torch.cuda.synchronize()
-    from kvedge_amd.ops import reference as R
-
-    hc = [h.cpu() for h in hs]
-    A = b.shape[1]
-    rb, rs = torch.empty(n, A, 4), torch.empty(n, A)
-    rc = torch.empty(n, A, dtype=torch.int32)
-    R.yolo_decode(hc, (8, 16, 32), 80, rb, rs, rc)
-    assert (b.cpu() - rb).abs().max() < 2e-2 and (s_.cpu() - rs).abs().max() < 1e-5
-    assert torch.equal(c.cpu(), rc)
-    rout = torch.empty(n, kv.max_det, 6)
-    rcnt = torch.empty(n, dtype=torch.int32)
-    R.nms(b.cpu(), s_.cpu(), c.cpu(), kv.conf, kv.iou, kv.max_det, rout, rcnt)
-    assert torch.equal(cnt.cpu(), rcnt), (cnt.cpu().tolist(), rcnt.tolist())
-    assert (out.cpu() - rout).abs().max() < 1e-4
-    # and the graph's own detections for these images are exactly that
     dets, dcnt = eng.outputs
-    assert torch.equal(dcnt[:n].cpu(), rcnt)
+    per = eng.batch // S
+    n = 32
+    total = 0
+    for sl in range(S):
+        lo = sl * per
+        frames = eng.frames[lo:lo + n].contiguous()
+        heads = [h[:n].contiguous() for h in graph_heads[sl]]
+        with torch.no_grad():
+            hr = ref(frames_to_yolo(frames.cpu()))
+        for g, r in zip(heads, hr):
+            g = g.float().cpu()
+            r = r.permute(0, 2, 3, 1).float()
+            cos = torch.nn.functional.cosine_similarity(g.flatten(), r.flatten(), dim=0)
+            assert cos > 0.99, (sl, float(cos))
+            # class logits and box-DFL logits separately (different magnitudes)
+            for part in (slice(0, 64), slice(64, None)):
+                c = torch.nn.functional.cosine_similarity(g[..., part].flatten(),
+                                                          r[..., part].flatten(), dim=0)
+                assert c > 0.99, (sl, part, float(c))
+        # decode: GPU kernels on the graph's maps vs the CPU reference
+        b, s_, c = ops.yolo_decode(heads, (8, 16, 32), 80)
+        torch.cuda.synchronize()
+        hc = [h.cpu() for h in heads]
+        A = b.shape[1]
+        rb, rs = torch.empty(n, A, 4), torch.empty(n, A)
+        rc = torch.empty(n, A, dtype=torch.int32)
+        R.yolo_decode(hc, (8, 16, 32), 80, rb, rs, rc)
+        assert (b.cpu() - rb).abs().max() < 2e-2 and (s_.cpu() - rs).abs().max() < 1e-5
+        assert torch.equal(c.cpu(), rc)
+        # NMS: the CPU reference on the GPU-decoded boxes vs the GRAPH's detections
+        rout = torch.empty(n, kv.max_det, 6)
+        rcnt = torch.empty(n, dtype=torch.int32)
+        R.nms(b.cpu(), s_.cpu(), c.cpu(), kv.conf, kv.iou, kv.max_det, rout, rcnt)
+        gcnt = dcnt[lo:lo + n].cpu()
+        assert torch.equal(gcnt, rcnt), (sl, gcnt.tolist(), rcnt.tolist())
+        gd = dets[lo:lo + n].cpu()
+        for i in range(n):
+            k = int(rcnt[i])
+            assert (gd[i, :k] - rout[i, :k]).abs().max() < 1e-4 if k else True, (sl, i)
+        total += int(rcnt.sum())
+    assert total > 0  # the comparison saw real detections
+    rcnt = dcnt[:n].cpu()
     stats = {"images": n, "detections": int(rcnt.sum()), "max_per_image": int(rcnt.max())}
     if os.path.isdir("gpurun_out"):
         with open("gpurun_out/bench_config_parity_yolov8n.json", "w") as f:

@@ -68,7 +68,8 @@ def conv_dual_cost(x1, x2, w, bias, act, stride2, out=None, tile=-1):
     N, Ho, Wo, K1 = x1.shape
     K2, co = x2.shape[3], w.shape[0]
     m = N * Ho * Wo
-    return (f"dual 1x1 {K1}+{K2}>{co} @{Ho}x{Wo}", (m * (K1 + K2) + m * co) * 2 + _b(w),
+    return (f"dual 1x1 {K1}+{K2}>{co} @{Ho}x{Wo}" + (" s2" if stride2 > 1 else ""),
+            (m * (K1 + K2) + m * co) * 2 + _b(w),
             2.0 * m * (K1 + K2) * co, tile)
 
 
