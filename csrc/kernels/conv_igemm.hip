@@ -349,6 +349,9 @@ int direct_de_launch(const KvConvParams* p, int tile, hipStream_t stream);
 // v12 skinny implicit GEMM for edge batches (conv_skinny.hip): indices after v10
 int skinny_num_tiles();
 int skinny_launch(const KvConvParams* p, int tile, hipStream_t stream);
+// v14 256x256 8-phase ping-pong implicit GEMM (conv_pp.hip): indices after v12
+int pp_num_tiles();
+int pp_launch(const KvConvParams* p, int tile, hipStream_t stream);
 // v9 bottleneck seam, conv3 + residual -> next conv1 (conv_seam.hip): tail calls only, tile
 // indices after the whole table above (kv_conv_num_tiles() + i)
 int seam_num_tiles();
@@ -363,7 +366,7 @@ extern "C" int kv_nloop_sched_check(void) { return kvedge::nloop_sched_check(); 
 extern "C" int kv_conv_num_tiles(void) {
   return kNumTiles + glds_num_tiles() + stream_num_tiles() + direct_num_tiles() +
          nloop_num_tiles() + xp_num_tiles() + sk_num_tiles() + direct_de_num_tiles() +
-         skinny_num_tiles();
+         skinny_num_tiles() + pp_num_tiles();
 }
 
 extern "C" int kv_conv_pick_tile(const KvConvParams* p) {
@@ -516,7 +519,9 @@ static int kv_conv2d_one(const KvConvParams* p, int tile, hipStream_t stream) {
   const int v8 = v7 + xp_num_tiles();
   const int v10 = v8 + sk_num_tiles();
   const int v12 = v10 + direct_de_num_tiles();
-  if (tile >= v12 + skinny_num_tiles()) return -6;
+  const int v14 = v12 + skinny_num_tiles();
+  if (tile >= v14 + pp_num_tiles()) return -6;
+  if (tile >= v14) return pp_launch(p, tile - v14, stream);
   if (tile >= v12) return skinny_launch(p, tile - v12, stream);
   if (tile >= v10) return direct_de_launch(p, tile - v10, stream);
   if (tile >= v8) return sk_launch(p, tile - v8, stream);
