@@ -103,8 +103,9 @@ def test_conv_residual_and_slices():
     assert err <= 0.02 * scale
 
 
-N_TILES = 118  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue / N-160 (68-85) + v8 split-K (86-104) + v10 (105-107) + v12 (108-116) + v14 (117)
-PP0 = 117  # v14: 256x256 8-phase ping-pong implicit GEMM (conv_pp.hip): modes 0 (Cin % 64), 1, 4
+N_TILES = 121  # v1 (0-5) + v2 (6-31) + v3 (32-53) + v4 (54-57) + v6 (58-67) + v7 BK32 MF16 / direct-epilogue / N-160 (68-85) + v8 split-K (86-104) + v10 (105-107) + v12 (108-116) + v14 (117-120)
+PP0 = 117  # v14: 8-phase ping-pong implicit GEMM (conv_pp.hip): 256x256, 512x128, then their
+# persistent forms (one workgroup per CU walking tiles); modes 0 (Cin % 64), 1, 4
 # + v6 A-resident N-loop 1x1 GEMM (58-67, conv_nloop.hip kNlTiles: one Kpad per tile;
 # 63-65 are the fused-downsample (dual) forms, 66-67 step 128 K at a time)
 NLOOP0 = 58
@@ -1009,7 +1010,7 @@ def test_c2f16_matches_four_launch_block():
 
 
 @pytest.mark.parametrize("tile", [-1] + list(range(6, DIRECT0)) + [NLOOP0, 63, 64] +
-                         list(range(XP0, DE0)) + [DE0, SKN0, SKN0 + 8, PP0])
+                         list(range(XP0, DE0)) + [DE0, SKN0, SKN0 + 8] + list(range(PP0, PP0 + 4)))
 @pytest.mark.parametrize("geom", [
     # (N, H, W, skip ld, skip coff, K1, low ld, low coff, K2, Cout, y ld, y coff): YOLO h15 / h12
     (2, 20, 20, 192, 128, 64, 192, 64, 128, 64, 96, 0),
@@ -1031,7 +1032,7 @@ def test_conv_dual2_up2(tile, geom):
     out = torch.full((N, H, W, ldy), 7.0, dtype=torch.bfloat16, device="cuda")
     args = (skip.cuda(), K1, low.cuda(), w.cuda(), b.cuda(), ops.ACT_SILU, out)
     kw = dict(x_coff=sc, x2_coff=lc, y_coff=yc, up2=True, tile=tile)
-    if not (tile == -1 or 6 <= tile < STREAM0 or XP0 <= tile < DE0 or tile == PP0):
+    if not (tile == -1 or 6 <= tile < STREAM0 or XP0 <= tile < DE0 or tile >= PP0):
         with pytest.raises(RuntimeError):
             ops.conv_dual2(*args, **kw)
         return
@@ -1044,9 +1045,12 @@ def test_conv_dual2_up2(tile, geom):
     _assert_close(got[..., yc:yc + cout], ref[..., yc:yc + cout], ("dual2 up2", tile, geom))
 
 
+@pytest.mark.parametrize("tile", list(range(PP0, PP0 + 4)))
 @pytest.mark.parametrize("case", [
     # (N, H, W, cin, cout, k, stride, pad, act, res, ldx_extra, x_coff, ldy_extra, y_coff)
     (4, 14, 14, 256, 256, 3, 1, 1, ops.ACT_RELU, False, 0, 0, 0, 0),     # s3 3x3 (36 K-tiles)
+    (3, 28, 28, 128, 128, 3, 1, 1, ops.ACT_RELU, False, 0, 0, 0, 0),     # s2 3x3 (the 512 x 128 form)
+    (3, 28, 28, 512, 128, 1, 1, 0, ops.ACT_RELU, False, 0, 0, 0, 0),     # s2 reduce
     (2, 7, 7, 512, 512, 3, 1, 1, ops.ACT_RELU, False, 0, 0, 0, 0),       # s4 3x3, M tail
     (3, 14, 14, 512, 512, 3, 2, 1, ops.ACT_RELU, False, 0, 0, 0, 0),     # s4 entry 3x3/2
     (2, 28, 28, 128, 128, 3, 2, 1, ops.ACT_RELU, False, 0, 0, 0, 0),     # K = 1152, 2 tiles of N
@@ -1054,16 +1058,20 @@ def test_conv_dual2_up2(tile, geom):
     (3, 7, 7, 512, 2048, 1, 1, 0, ops.ACT_RELU, True, 0, 0, 0, 0),       # s4 expand + res
     (2, 9, 11, 192, 136, 1, 1, 0, ops.ACT_NONE, False, 64, 32, 8, 8),    # K / N tails, slices
     (1, 3, 3, 64, 40, 1, 1, 0, ops.ACT_SILU, True, 0, 0, 0, 0),          # one K-tile, tiny M
+    # > 256 tiles: the persistent forms walk 2 tiles per workgroup (1x1 K = 256: 4 K-steps,
+    # the staging stream crosses a tile boundary every 4; 3x3 K = 2304 with a residual)
+    (256, 14, 14, 256, 512, 1, 1, 0, ops.ACT_RELU, True, 0, 0, 0, 0),
+    (200, 14, 14, 256, 512, 3, 1, 1, ops.ACT_RELU, False, 0, 0, 0, 0),
 ])
-def test_conv_pp(case):
+def test_conv_pp(tile, case):
     """v14 (conv_pp.hip): the 8-phase ping-pong loop at the ResNet-50 GEMM shapes and at K /
     M / N tails, vs the fp32 reference (channels outside the output slice untouched); then
     three launches into NaN-poisoned outputs must agree bitwise: a skipped half-tile, a
     stale LDS read or a restage race shows as NaN or as a launch-to-launch difference."""
     N, H, W, cin, cout, k, s, p, act, res, lx, xc, ly, yc = case
     err, scale = _conv_case(N, H, W, cin, cout, k, s, p, act, res=res, ldx_extra=lx, x_coff=xc,
-                            ldy_extra=ly, y_coff=yc, tile=PP0)
-    assert err <= 0.02 * scale, (case, err, scale)
+                            ldy_extra=ly, y_coff=yc, tile=tile)
+    assert err <= 0.02 * scale, (tile, case, err, scale)
     # a second launch on the same inputs is bitwise identical (no race in the schedule)
     spec = ConvSpec.auto(cin, cout, k, s, p, act)
     g = torch.Generator().manual_seed(11)
@@ -1074,7 +1082,7 @@ def test_conv_pp(case):
     for _ in range(3):
         o = torch.full((N,) + spec.out_hw(H, W) + (cout,), float("nan"), dtype=torch.bfloat16,
                        device="cuda")
-        ops.conv2d(x, spec, w, b, out=o, tile=PP0)
+        ops.conv2d(x, spec, w, b, out=o, tile=tile)
         outs.append(o)
     torch.cuda.synchronize()
     assert not torch.isnan(outs[0].float()).any()

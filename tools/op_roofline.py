@@ -25,7 +25,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 # kernel-family boundaries of kv_conv2d's tile index (csrc/kernels/conv_igemm.hip)
 FAMILIES = [(0, "v1"), (6, "glds"), (32, "stream"), (54, "direct"), (58, "nloop"),
             (68, "xp/bk32/de"), (86, "splitk"), (105, "direct-de"),
-            (108, "skinny"), (117, "pp")]
+            (108, "skinny"), (117, "pp")]  # pp 117: 256x256, 118: 512x128, 119-120: persistent
 
 
 def family(tile):
