@@ -642,6 +642,8 @@ void batchnorm_nhwc(const at::Tensor& x, at::Tensor& y, const at::Tensor& scale,
 }
 
 int64_t conv_num_tiles() { return kv_conv_num_tiles(); }
+int64_t conv_splitk_base() { return kv_conv_splitk_base(); }
+int64_t conv_splitk_num_tiles() { return kv_conv_splitk_num_tiles(); }
 int64_t nloop_sched_check() { return kv_nloop_sched_check(); }
 int64_t conv_seam_num_tiles() { return kv_conv_seam_num_tiles(); }
 int64_t set_conv_chunk_bytes(int64_t b) { return kv_set_conv_chunk_bytes(b); }
@@ -783,6 +785,8 @@ TORCH_LIBRARY(kvedge, m) {
   m.def("preprocess(Tensor x, Tensor(a!) y, float[] mean, float[] std) -> ()");
   m.def("batchnorm_nhwc(Tensor x, Tensor(a!) y, Tensor scale, Tensor shift, bool relu) -> ()");
   m.def("conv_num_tiles() -> int", conv_num_tiles);
+  m.def("conv_splitk_base() -> int", conv_splitk_base);
+  m.def("conv_splitk_num_tiles() -> int", conv_splitk_num_tiles);
   m.def("nloop_sched_check() -> int", nloop_sched_check);
   m.def("conv_seam_num_tiles() -> int", conv_seam_num_tiles);
   m.def("bneck_fused(Tensor x, Tensor w1, Tensor b1, Tensor w2, Tensor b2, Tensor w3, Tensor b3, "

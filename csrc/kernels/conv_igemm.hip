@@ -369,6 +369,15 @@ extern "C" int kv_conv_num_tiles(void) {
          skinny_num_tiles() + pp_num_tiles();
 }
 
+// first split-K (v8) tile index: ops.is_splitk() sizes a workspace for exactly these, so it
+// is read from here rather than re-derived from family sizes in Python (adding the v14 family
+// after the split-K one once shifted a derived base by four)
+extern "C" int kv_conv_splitk_base(void) {
+  return kNumTiles + glds_num_tiles() + stream_num_tiles() + direct_num_tiles() +
+         nloop_num_tiles() + xp_num_tiles();
+}
+extern "C" int kv_conv_splitk_num_tiles(void) { return sk_num_tiles(); }
+
 extern "C" int kv_conv_pick_tile(const KvConvParams* p) {
   // Heuristic: enough workgroups to cover 256 CUs x 2, largest tile otherwise.
   const long long M = p->M, N = p->Cout;

@@ -73,6 +73,8 @@ int kv_conv2d(const KvConvParams* p, int tile, hipStream_t stream);
 // image-chunk size of kv_conv2d launches (bytes per operand per launch); 0 = default
 long long kv_set_conv_chunk_bytes(long long bytes);
 int kv_conv_num_tiles(void);
+int kv_conv_splitk_base(void);       // split-K tiles: [base, base + splitk_num_tiles)
+int kv_conv_splitk_num_tiles(void);
 // host replay of the v6 (conv_nloop.hip) counted-wait schedules: 0 = every tile is safe
 int kv_nloop_sched_check(void);
 int kv_conv_pick_tile(const KvConvParams* p);

@@ -63,8 +63,10 @@ def load(build_if_missing: bool = False) -> bool:
         return False
     _check_single_hip_runtime()
     global SPLITK0
-    SPLITK0 = (int(torch.ops.kvedge.conv_num_tiles()) - N_SKINNY_TILES - N_DE_TILES -
-               N_SPLITK_TILES)
+    SPLITK0 = int(torch.ops.kvedge.conv_splitk_base())
+    if int(torch.ops.kvedge.conv_splitk_num_tiles()) != N_SPLITK_TILES:
+        _load_error = "split-K tile count differs from the native library (stale build?)"
+        return False
     _loaded = True
     return True
 
@@ -209,7 +211,7 @@ SPLITK_MAX_ELEMS = 32 << 20  # 128 MB of fp32 per stream at most
 SPLITK_MAX_SPLIT = 32        # largest split of conv_sk.hip kSkTiles
 N_SPLITK_TILES = 19          # conv_sk.hip kSkTiles
 N_DE_TILES = 3               # v10 direct-epilogue tiles (conv_direct.hip): after split-K
-N_SKINNY_TILES = 9           # v12 edge-batch tiles (conv_skinny.hip kSknTiles): last
+N_SKINNY_TILES = 9           # v12 edge-batch tiles (conv_skinny.hip kSknTiles): before v14
 SPLITK0 = 1 << 30            # first split-K tile index, set by load()
 
 

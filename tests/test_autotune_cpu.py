@@ -200,3 +200,19 @@ def test_dist_cache_agreement_gloo():
     for r in range(2):
         kept, differ, missing = res[r]
         assert kept == caches[0][r] and differ == {} and missing == {}
+
+
+def test_splitk_tile_range_from_native():
+    """ops.is_splitk() must cover exactly the native split-K family: it decides which tiles
+    get an fp32 slab workspace, and a derived base once drifted when a family was appended."""
+    from kvedge_amd import ops
+    if not ops.load():
+        pytest.skip("native library not built")
+    import torch
+    base = int(torch.ops.kvedge.conv_splitk_base())
+    assert ops.SPLITK0 == base
+    assert ops.is_splitk(base) and ops.is_splitk(base + ops.N_SPLITK_TILES - 1)
+    assert not ops.is_splitk(base - 1) and not ops.is_splitk(base + ops.N_SPLITK_TILES)
+    # split-K, direct-epilogue, skinny and v14 families follow in that order
+    assert base + ops.N_SPLITK_TILES + ops.N_DE_TILES + ops.N_SKINNY_TILES + 4 == \
+        int(torch.ops.kvedge.conv_num_tiles())
