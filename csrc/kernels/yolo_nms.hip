@@ -144,7 +144,7 @@ __device__ __forceinline__ bool iou_gt(float ax1, float ay1, float ax2, float ay
 }
 
 constexpr int kNmsWaves = 8;
-constexpr int kSel = 1024;     // top-set target size
+constexpr int kSel = 768;      // top-set target size (rank-sortable: <= kRankSortMax)
 constexpr int kSelMax = 2048;  // top-set capacity (a wider threshold bin -> full sort)
 constexpr int kBins = 2048;    // score-bit histogram bins
 constexpr int kRankSortMax = 1024;  // rank sort up to here (<= 2 keys per thread), bitonic above
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
                                                   float conf, float iou_thr, int max_det,
                                                   float* __restrict__ out,
                                                   int* __restrict__ count, int diag) {
-  __shared__ unsigned long long keys[kMaxCand];
+  __shared__ __attribute__((aligned(16))) unsigned long long keys[kMaxCand];
   __shared__ __attribute__((aligned(16))) float kept[4 * 320];
   __shared__ int kept_c[320];
   __shared__ unsigned long long supp[kNmsWaves];
@@ -167,8 +167,6 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   const int n = blockIdx.x;
   const int tid = threadIdx.x;
   const unsigned long long t_start = (diag & 4) ? __builtin_amdgcn_s_memrealtime() : 0ull;
-  if (tid == 0) ncand = 0;
-  __syncthreads();
   const float* sc = scores + (long long)n * A;
   // wave-aggregated compaction: one LDS atomic per wave and pass (popcount of the ballot)
   // instead of one per candidate -- with random-init heads nearly all 8400 anchors pass
@@ -176,7 +174,9 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   // All of this thread's scores are loaded up front (A <= kMaxCand: at most kIt per thread),
   // so the HBM latency is paid once, not once per pass of the ballot loop below.
   constexpr int kIt = kMaxCand / (64 * kNmsWaves);
-  {
+  auto compact = [&]() __attribute__((always_inline)) {
+    if (tid == 0) ncand = 0;
+    __syncthreads();
     const int ln = tid & 63;
     float sv[kIt];
 #pragma unroll
@@ -200,8 +200,9 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
           keys[slot] = ((unsigned long long)__float_as_uint(s) << 32) | (0xFFFFFFFFu - (unsigned)a);
       }
     }
-  }
-  __syncthreads();
+    __syncthreads();
+  };
+  compact();
   const int cnt = min(ncand, kMaxCand);
   // diag bit 2: per-phase wall-clock stamps (s_memrealtime, 100 MHz) -> the image's output rows
   unsigned long long t_ph[4] = {t_start, 0, 0, 0};
@@ -228,6 +229,20 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
       }
     }
   };
+  // rank sort: each thread counts the keys above its own with broadcast LDS reads and writes
+  // its key to that slot -- one pass, one barrier.  Keys are unique (the index is in the low
+  // word), so the ranks are a permutation.
+  auto rank_sort = [&](const unsigned long long* src, unsigned long long* dst, int n)
+      __attribute__((always_inline)) {
+    for (int i0 = 0; i0 < n; i0 += blockDim.x) {
+      const int i = i0 + tid;
+      const unsigned long long key = i < n ? src[i] : 0ull;
+      int r = 0;
+      for (int j = 0; j < n; ++j) r += src[j] > key;
+      if (i < n) dst[r] = key;
+    }
+    __syncthreads();
+  };
   // Top-set selection.  Greedy NMS reads candidates in score order and usually reaches
   // max_det long before the end of the list, so only the head needs sorting: a 2048-bin
   // histogram of the score bits gives the lowest bin T whose suffix holds >= kSel keys;
@@ -245,6 +260,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   unsigned long long* K = keys;
   int nsel = cnt;
   bool sorted = false;  // the top set already came out of its sort (bucket or fallback)
+  bool clobbered = false;  // keys[] now holds the sorted top set, not all candidates
   if (cnt > kSel) {
     int* hist = reinterpret_cast<int*>(sel);
     for (int i = tid; i < kBins; i += blockDim.x) hist[i] = 0;
@@ -369,7 +385,18 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
       __syncthreads();
       K = sel;
       nsel = s_n2;
-      if (!(diag & 2)) bitonic(K, nsel);
+      if (!(diag & 2)) {
+        if (nsel <= kRankSortMax) {
+          // one rank pass into keys[0, nsel) instead of the bitonic network's log^2
+          // barrier-separated stages (a 1382-candidate image: ~28 us of bitonic, r5 probe);
+          // keys[] is rebuilt from the scores if the top set runs out (fallback below)
+          rank_sort(sel, keys, nsel);
+          K = keys;
+          clobbered = true;
+        } else {
+          bitonic(K, nsel);
+        }
+      }
       sorted = true;
     }
   }
@@ -381,17 +408,9 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   // (the index is in the low word), so the ranks are a permutation.
   if (K == sel && cnt > kSel) sorted = true;  // the bucket sort above
   if (!(diag & 2) && !sorted) {
-    if (K == keys && nsel <= kRankSortMax) {  // (a top set in sel stays bitonic: the
-      unsigned long long* dst = sel;           // full-sort fallback below needs keys intact)
-      for (int i0 = 0; i0 < nsel; i0 += blockDim.x) {
-        const int i = i0 + tid;
-        const unsigned long long key = i < nsel ? K[i] : 0ull;
-        int r = 0;
-        for (int j = 0; j < nsel; ++j) r += K[j] > key;
-        if (i < nsel) dst[r] = key;
-      }
-      __syncthreads();
-      K = dst;
+    if (K == keys && nsel <= kRankSortMax) {
+      rank_sort(keys, sel, nsel);
+      K = sel;
     } else {
       bitonic(K, nsel);  // diag bit 1: no top-set sort (timing only)
     }
@@ -509,7 +528,10 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   else nk = max_det;
   if (nk < max_det && nsel < cnt) {
     // the top set ran out: sort everything (its first nsel keys are the top set again,
-    // in the same order) and continue after them
+    // in the same order) and continue after them; the rank-sorted top set overwrote the
+    // head of keys[], so the candidates are compacted from the scores again first (the
+    // same set: compaction order does not matter, the sort fixes it)
+    if (clobbered) compact();
     bitonic(keys, cnt);
     greedy(keys, nsel, cnt);
   }

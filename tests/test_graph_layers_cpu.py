@@ -87,3 +87,51 @@ def test_summarize_refuses_a_short_trace(tmp_path):
                                   "rows": [["a", 0, 0, None]] * 3, "kernels": [1, 2, 1]}))
     with pytest.raises(SystemExit):
         gl.summarize(str(trace), str(labels), 5, 6.0, 2.5, out=io.StringIO())
+
+
+def _trace_with_pass(reps):
+    """_trace, preceded by the labelled eager pass: bn_kernel before the pass and after every
+    op (op 1 = two kernels), plus an earlier unrelated bn_kernel and tuning kernels."""
+    pre = [("void kvedge::bn_kernel(...)", -90_000, -89_000), ("kA", -88_000, -87_000)]
+    t = -80_000
+    seq = [["bn"], ["kA", "bn"], ["kB_gemm", "kB_fin", "bn"], ["kC", "bn"]]
+    for grp in seq:
+        for nm in grp:
+            full = "void kvedge::bn_kernel(...)" if nm == "bn" else nm
+            pre.append((full, t, t + 500))
+            t += 1000
+    body = _trace(reps).splitlines()
+    buf = io.StringIO()
+    w = csv.writer(buf)
+    w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+    for r in pre:
+        w.writerow(r)
+    return buf.getvalue() + "\n".join(body[1:]) + "\n"
+
+
+def test_op_kernel_counts_from_separators():
+    names = ["bn_kernel", "x", "bn_kernel", "kA", "bn_kernel", "kB", "kB2",
+             "at::native::fill", "bn_kernel", "kC", "bn_kernel"]
+    assert gl.op_kernel_counts(names, 3) == [1, 2, 1]
+    assert gl.op_kernel_counts(names, 11) is None  # no full pass in the trace
+
+
+def test_summarize_counts_kernels_per_op_from_the_trace(tmp_path):
+    """Labels that claim one kernel per op (an op that splits its Cout over two launches, or
+    whose kernel count the run step could not know) still summarise: the separator pass in
+    the trace gives the real counts."""
+    reps = 2
+    trace = tmp_path / "k_kernel_trace.csv"
+    trace.write_text(_trace_with_pass(reps))
+    labels = tmp_path / "labels.json"
+    labels.write_text(json.dumps({
+        "model": "yolov8n", "batch": 4, "streams": 2,
+        "rows": [["op a", 6e9, 1e12, None], ["op b", 1e9, 1e12, None], ["op c", 1e9, 0.0, None]],
+        "kernels": [1, 1, 1]}))
+    out = io.StringIO()
+    gl.summarize(str(trace), str(labels), reps, 6.0, 2.5, out=out)
+    table = [ln for ln in out.getvalue().splitlines() if ln.startswith("| ") and ln[2].isdigit()]
+    cells = [[c.strip() for c in ln.strip("|").split("|")] for ln in table]
+    assert [float(c[4]) for c in cells] == pytest.approx([10.0, 25.0, 4.0], abs=0.05)
+    assert "(+1 kernel)" in cells[1][3]
+    assert all(float(c[5]) > 0 for c in cells)  # floors come from the op rows

@@ -52,8 +52,17 @@ def run(a):
     eng = InferenceEngine(model, batch, M.image_size, device="cuda", streams=streams)
     eng.prepare(warmup=2, autotune=not a.no_autotune)
     per = batch // streams
+    # the labelled eager pass: a separator kernel (bn_kernel: the deployed models fold every
+    # BatchNorm, so the forward never launches one) before the pass and after every op, so
+    # the summary counts each op's kernels from the trace instead of assuming them (a Cout
+    # split launches two, a split-K tile GEMM + finalize)
+    sx = torch.zeros(1, 1, 1, 8, dtype=torch.bfloat16, device="cuda")
+    sy, s1, s0 = torch.empty_like(sx), torch.ones(8, device="cuda"), torch.zeros(8, device="cuda")
+    sep = lambda: ops.batchnorm_nhwc(sx, s1, s0, out=sy)  # noqa: E731
+    torch.cuda.synchronize()
     with torch.no_grad():
-        rows = costs_only(model, eng.frames[:per], ops)
+        sep()
+        rows = costs_only(model, eng.frames[:per], ops, after=sep)
     torch.cuda.synchronize()
     # kernels per op: a split-K tile is its GEMM and its finalize launch
     nk = [2 if (t is not None and ops.is_splitk(t)) else 1 for _, _, _, t in rows]
@@ -107,16 +116,35 @@ def assign(kernels, op_of, n_slices):
     return out if all(p == n_pos for p in ptr) else None
 
 
+def _is_model_kernel(nm):
+    return not (nm.startswith(("at::", "__amd_rocclr")) or "synth_dev" in nm or
+                "bump_kernel" in nm)
+
+
+def op_kernel_counts(names, n_ops):
+    """Kernels per op of the labelled eager pass: ``names`` = kernel names in launch order up
+    to the replay marker; the pass is the last n_ops + 1 separators (bn_kernel) and the
+    model kernels between them.  None if the trace has no such pass (older labels)."""
+    sep = [i for i, nm in enumerate(names) if nm.split("::")[-1].startswith("bn_kernel")]
+    if len(sep) < n_ops + 1:
+        return None
+    sep = sep[-(n_ops + 1):]
+    return [sum(1 for nm in names[a + 1:b] if _is_model_kernel(nm))
+            for a, b in zip(sep, sep[1:])]
+
+
 def summarize(path, labels, reps, hbm, peak, out=sys.stdout):
     lab = json.load(open(labels))
     rows, n_sl = lab["rows"], lab["streams"]
     n_ops = len(rows)
-    nk = lab.get("kernels") or [1] * n_ops
-    op_of = [p for p in range(n_ops) for _ in range(nk[p])]
     recs = list(csv.DictReader(open(path)))
     recs.sort(key=lambda r: int(r["Start_Timestamp"]))
     idx = max(i for i, r in enumerate(recs) if "synth_kernel" in r["Kernel_Name"]
               and "synth_dev" not in r["Kernel_Name"])
+    nk = op_kernel_counts([_short(r["Kernel_Name"]) for r in recs[:idx]], n_ops)
+    if nk is None:
+        nk = lab.get("kernels") or [1] * n_ops
+    op_of = [p for p in range(n_ops) for _ in range(nk[p])]
     body = recs[idx + 1:]
     # steps start at the frame kernel (synth_dev_kernel) of each replay
     starts = [i for i, r in enumerate(body) if "synth_dev_kernel" in r["Kernel_Name"]]
@@ -135,8 +163,7 @@ def summarize(path, labels, reps, hbm, peak, out=sys.stdout):
         walls.append((t1 - t0) / 1e3)
         ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), _short(r["Kernel_Name"]))
               for r in step]
-        model_ks = [x for x in ks if not (x[2].startswith(("at::", "__amd_rocclr")) or
-                                          "synth_dev" in x[2] or "bump_kernel" in x[2])]
+        model_ks = [x for x in ks if _is_model_kernel(x[2])]
         other = [x for x in ks if x not in model_ks]
         if len(model_ks) != len(op_of) * n_sl:
             if k == 0 and len(model_ks) % n_sl == 0:
@@ -148,6 +175,7 @@ def summarize(path, labels, reps, hbm, peak, out=sys.stdout):
                       f"{dict(_c.Counter(x[2][:40] for x in model_ks))}", file=sys.stderr)
                 n_ops = len(model_ks) // n_sl
                 op_of = list(range(n_ops))
+                nk = [1] * n_ops
                 rows = [[f"kernel #{i}", 0, 0.0, None] for i in range(n_ops)]
             else:
                 raise SystemExit(f"step {k}: {len(model_ks)} model kernels, expected "
@@ -206,7 +234,9 @@ def summarize(path, labels, reps, hbm, peak, out=sys.stdout):
         fl = max(byts / (hbm * 1e12), flops / (peak * 1e15)) * 1e6
         sh = share[p] / nst
         tot_share += sh
-        print(f"| {p} | {nm} | {family(tile)} | {names[p][:60]} | {d:.1f} | {fl:.1f} | "
+        kname = names[p][:60] + (f" (+{nk[p] - 1} kernel{'s' if nk[p] > 2 else ''})"
+                                 if nk[p] > 1 else "")
+        print(f"| {p} | {nm} | {family(tile)} | {kname} | {d:.1f} | {fl:.1f} | "
               f"{fl / max(d, 1e-3):.2f} | {sh:.1f} | {100 * sh / wall:.1f} |", file=out)
     oth = sum(extra_share.values()) / nst
     print(f"\nModel layers: {tot_share:.1f} us of wall share; frames/concat/other kernels: "

@@ -73,6 +73,19 @@ def conv_dual_cost(x1, x2, w, bias, act, stride2, out=None, tile=-1):
             2.0 * m * (K1 + K2) * co, tile)
 
 
+def conv_dual2_cost(x, K1, x2, w, bias, act, out, x_coff=0, x2_coff=0, y_coff=0, stride2=1,
+                    up2=False, tile=-1):
+    N, Ho, Wo, _ = x.shape
+    co = w.shape[0]
+    K2 = w.shape[1] - K1
+    m = N * Ho * Wo
+    # x2 is read at its own resolution: the up2 form reads each half-resolution pixel once
+    m2 = m // 4 if up2 else m
+    tag = " up2" if up2 else (" s2" if stride2 > 1 else "")
+    return (f"dual 1x1 {K1}+{K2}>{co} @{Ho}x{Wo}{tag}", (m * K1 + m2 * K2 + m * co) * 2 + _b(w),
+            2.0 * m * (K1 + K2) * co, tile)
+
+
 def conv_tail_cost(x, w, bias, act, w1, b1, res=None, x2=None, stride2=1, out=None, z=None,
                    tile=-1):
     N, H, W, K1 = x.shape
@@ -159,7 +172,8 @@ def softmax_cost(x, out=None, argmax=None):
     return "softmax + top1", _b(x) + x.numel() * 4, 0.0, None
 
 
-COSTS = {"conv2d": conv2d_cost, "conv_dual": conv_dual_cost, "conv_tail": conv_tail_cost,
+COSTS = {"conv2d": conv2d_cost, "conv_dual": conv_dual_cost, "conv_dual2": conv_dual2_cost,
+         "conv_tail": conv_tail_cost,
          "conv_pair": conv_pair_cost, "bottleneck_fused": bneck_cost, "c2f16": c2f16_cost,
          "stem_from_frames": stem_from_frames_cost, "stem12_pool_frames": stem12_cost,
          "yolo_stem2": yolo_stem2_cost,
@@ -167,8 +181,10 @@ COSTS = {"conv2d": conv2d_cost, "conv_dual": conv_dual_cost, "conv_tail": conv_t
          "nms": nms_cost, "global_avgpool": avgpool_cost, "softmax_rows": softmax_cost}
 
 
-def costs_only(model, frames, ops):
-    """The op rows of one forward without timing (CPU works): [(name, bytes, flops, tile)]."""
+def costs_only(model, frames, ops, after=None):
+    """The op rows of one forward without timing (CPU works): [(name, bytes, flops, tile)].
+    ``after``: called after every recorded (outermost) op -- tools/graph_layers.py launches a
+    separator kernel there, so the trace shows how many kernels each op launched."""
     recs, saved = [], {}
     for fname, cost in COSTS.items():
         saved[fname] = fn = getattr(ops, fname)
@@ -180,6 +196,8 @@ def costs_only(model, frames, ops):
             r = _fn(*args, **kw)
             if len(recs) == n0:
                 recs.append(row)
+                if after is not None:
+                    after()
             return r
         setattr(ops, fname, w)
     try:
