@@ -648,52 +648,6 @@ int64_t nloop_sched_check() { return kv_nloop_sched_check(); }
 int64_t conv_seam_num_tiles() { return kv_conv_seam_num_tiles(); }
 int64_t set_conv_chunk_bytes(int64_t b) { return kv_set_conv_chunk_bytes(b); }
 
-// v11 fused identity bottleneck (csrc/kernels/bneck_fused.hip): y = ReLU(W3 . ReLU(conv3x3(
-// ReLU(W1 . x + b1)) + b2) + b3 + x) in one launch.  x, y: [N, H, W, 4C] bf16 contiguous.
-void bneck_fused(const at::Tensor& x, const at::Tensor& w1, const at::Tensor& b1,
-                 const at::Tensor& w2, const at::Tensor& b2, const at::Tensor& w3,
-                 const at::Tensor& b3, at::Tensor& y, int64_t dbg) {
-  check_bf16(x, "x");
-  check_bf16(y, "y");
-  check_bf16(w1, "w1");
-  check_bf16(w2, "w2");
-  check_bf16(w3, "w3");
-  for (const at::Tensor* b : {&b1, &b2, &b3}) {
-    check_dev(*b, "bias");
-    TORCH_CHECK(b->scalar_type() == at::kFloat, "kvedge: bneck_fused biases must be fp32");
-  }
-  TORCH_CHECK(x.dim() == 4 && y.sizes() == x.sizes(), "kvedge: bneck_fused x / y [N, H, W, 4C]");
-  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C4 = x.size(3), C = C4 / 4;
-  TORCH_CHECK(C4 % 4 == 0 && w1.dim() == 2 && w1.size(0) == C && w1.size(1) == C4,
-              "kvedge: bneck_fused w1 [C, 4C]");
-  TORCH_CHECK(w2.dim() == 2 && w2.size(0) == C && w2.size(1) == 9 * C, "kvedge: bneck_fused w2 [C, 9C]");
-  TORCH_CHECK(w3.dim() == 2 && w3.size(0) == C4 && w3.size(1) == C, "kvedge: bneck_fused w3 [4C, C]");
-  TORCH_CHECK(b1.numel() == C && b2.numel() == C && b3.numel() == C4, "kvedge: bneck_fused bias sizes");
-  TORCH_CHECK(kv_bneck_fused_supported((int)C, (int)H, (int)W), "kvedge: bneck_fused has no "
-              "instantiation for C=", C, " H=", H, " W=", W);
-  TORCH_CHECK(x.numel() * 2 < (1ll << 31) - (1 << 20), "kvedge: bneck_fused operands exceed 2 GiB");
-  TORCH_CHECK(x.data_ptr() != y.data_ptr(), "kvedge: bneck_fused cannot run in place");
-  const c10::DeviceGuard g(x.device());
-  KvBneckParams p{};
-  p.x = x.data_ptr();
-  p.y = y.data_ptr();
-  p.w1 = w1.data_ptr();
-  p.b1 = b1.data_ptr<float>();
-  p.w2 = w2.data_ptr();
-  p.b2 = b2.data_ptr<float>();
-  p.w3 = w3.data_ptr();
-  p.b3 = b3.data_ptr<float>();
-  p.N = (int)N; p.H = (int)H; p.W = (int)W; p.C = (int)C;
-  p.x_bytes = (int)(x.numel() * 2);
-  p.dbg = (int)dbg;
-  const int rc = kv_bneck_fused(&p, cur_stream(x));
-  TORCH_CHECK(rc == 0, "kvedge: bneck_fused failed rc=", rc);
-}
-
-int64_t bneck_fused_supported(int64_t C, int64_t H, int64_t W) {
-  return kv_bneck_fused_supported((int)C, (int)H, (int)W);
-}
-
 // v13 fused YOLOv8 C2f(32, 32, n=1, shortcut) (csrc/kernels/c2f_fused.hip): x [N, H, W, ldx]
 // channels x_coff .. x_coff + 31 -> y [N, H, W, ldy] channels y_coff .. y_coff + 31
 void c2f16_fused(const at::Tensor& x, int64_t x_coff, const at::Tensor& w1, const at::Tensor& b1,
@@ -789,9 +743,6 @@ TORCH_LIBRARY(kvedge, m) {
   m.def("conv_splitk_num_tiles() -> int", conv_splitk_num_tiles);
   m.def("nloop_sched_check() -> int", nloop_sched_check);
   m.def("conv_seam_num_tiles() -> int", conv_seam_num_tiles);
-  m.def("bneck_fused(Tensor x, Tensor w1, Tensor b1, Tensor w2, Tensor b2, Tensor w3, Tensor b3, "
-        "Tensor(a!) y, int dbg=0) -> ()");
-  m.def("bneck_fused_supported(int C, int H, int W) -> int", bneck_fused_supported);
   m.def("c2f16_fused(Tensor x, int x_coff, Tensor w1, Tensor b1, Tensor wm1, Tensor bm1, "
         "Tensor wm2, Tensor bm2, Tensor w2, Tensor b2, Tensor(a!) y, int y_coff, int S) -> ()");
   m.def("c2f16_supported(int H, int W, int S) -> int", c2f16_supported);
@@ -808,7 +759,6 @@ TORCH_LIBRARY_IMPL(kvedge, CUDA, m) {
   m.impl("conv_frames_s2d", conv_frames_s2d);
   m.impl("conv_tail", conv_tail);
   m.impl("conv_pair", conv_pair);
-  m.impl("bneck_fused", bneck_fused);
   m.impl("c2f16_fused", c2f16_fused);
   m.impl("conv_dual2", conv_dual2);
   m.impl("sppf_pool", sppf_pool);

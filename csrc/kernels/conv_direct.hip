@@ -829,10 +829,6 @@ static const DirectEntry kDirect[] = {
     // stage-2 conv2 and YOLO's 128-channel 3x3s, as v10 tile 0
     KV_DIRECT_DE4(128, 128, 1, 3, kActRelu), KV_DIRECT_DE4(128, 128, 1, 3, kActSilu),
     KV_DIRECT_DE4(128, 128, 2, 3, kActSilu),
-    // ResNet-50 stage-2 entry 3x3/2 128 -> 128 @56^2: the implicit GEMM re-gathers every
-    // input pixel ~2.25x (9 taps / stride 2^2) in 64-B pieces through L2, and runs at 0.33 of
-    // its HBM floor next to the other slice (profiles/r6_v3_graph_layers_rn_b1280_pp.md row 8)
-    KV_DIRECT_DE4(128, 128, 2, 3, kActRelu),
 };
 #undef KV_DIRECT2
 #undef KV_DIRECT_DE

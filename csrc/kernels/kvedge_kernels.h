@@ -154,27 +154,6 @@ int kv_batchnorm_nhwc(const void* x, void* y, const float* scale, const float* s
                       int64_t rows, int C, int relu, hipStream_t s);
 
 // ---------------------------------------------------------------------------
-// v11 fused identity bottleneck (bneck_fused.hip): y = ReLU(W3 . ReLU(conv3x3(ReLU(W1 . x +
-// b1)) + b2) + b3 + x), NHWC bf16, x / y [N, H, W, 4C] contiguous, packed weights
-// w1 [C][4C], w2 [C][9C] (tap-major, cin minor), w3 [4C][C]; fp32 biases.
-// ---------------------------------------------------------------------------
-typedef struct KvBneckParams {
-  const void* x;
-  void* y;
-  const void* w1;
-  const float* b1;
-  const void* w2;
-  const float* b2;
-  const void* w3;
-  const float* b3;
-  int N, H, W, C;
-  int x_bytes;  // N * H * W * 4C * 2 (also y's)
-  int dbg;      // debug (tests/tools only): 1 / 2 = write z1 / z2 into y[..., :C] and stop
-} KvBneckParams;
-int kv_bneck_fused_supported(int C, int H, int W);
-int kv_bneck_fused(const KvBneckParams* p, hipStream_t stream);
-
-// ---------------------------------------------------------------------------
 // v13 fused YOLOv8 C2f(32, 32, n=1, shortcut) (c2f_fused.hip): t = SiLU(W1 . x + b1) (a =
 // t[:16], s = t[16:]), u = SiLU(conv3x3(s) + bm1), v = s + SiLU(conv3x3(u) + bm2),
 // y = SiLU(W2 . [a, s, v] + b2); NHWC bf16, x [N, H, W, ldx] at x_coff (32 channels), y at

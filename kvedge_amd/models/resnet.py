@@ -143,23 +143,6 @@ class DeployedBottleneck:
         idt = x if self.down is None else self.down(x)
         return self.c3(y, res=idt, out=out)
 
-    def fused_ok(self, x_shape, on_gpu: bool) -> bool:
-        """The whole block as ONE v11 launch (ops.bottleneck_fused: conv1 -> 3x3 -> conv3 +
-        residual, z1 / z2 in LDS): identity blocks of the stage widths bneck_fused.hip is
-        instantiated for (ResNet-50 stages 2 and 3)."""
-        N, H, W, C4 = x_shape
-        c1 = self.c1.spec
-        return (on_gpu and ops.BNECK_ENABLED and self.down is None and self.dual is None and
-                self.c2.spec.stride == 1 and c1.cin == C4 and self.c3.spec.cout == C4 and
-                ops.bneck_supported(c1.cout, H, W))
-
-    def call_fused(self, x, out=None):
-        if getattr(self, "_frag", None) is None or self._frag[0].device != x.device:
-            # the kernel's fragment-major copies of the three weights, made once
-            self._frag = tuple(ops.mfma_frag_major(c.w) for c in (self.c1, self.c2, self.c3))
-        return ops.bottleneck_fused(x, self.c1.w, self.c1.b, self.c2.w, self.c2.b, self.c3.w,
-                                    self.c3.b, out=out, frag=self._frag)
-
     def can_tail(self, nxt: "DeployedBottleneck") -> bool:
         """conv3 (or the fused downsample GEMM) + the next block's conv1 as one fused tail.
         Stage 1 (Cout = 256): the v3 tail tile holds a whole y row and both weight slices in
@@ -298,15 +281,11 @@ class KvResNet50:
                     if last and full is None:
                         shp = b.out_shape(y.shape)
                         full = ops.empty((B,) + shp[1:], dtype=y.dtype, device=y.device)
-                    if z is None and b.fused_ok(y.shape, y.is_cuda):  # as the path below
-                        y = b.call_fused(y, out=full[i:i + mb] if last else None)
-                        continue
-                    nxt_fused = nxt.fused_ok(b.out_shape(y.shape), y.is_cuda)
                     # the same batch gate as the whole-batch path below, evaluated on the
                     # FULL batch B: a micro-batch-sized gate would fuse (or not) differently
                     # from the whole-batch path and change y's bf16 rounding
-                    fuse = (self.fuse_tail and y.is_cuda and not nxt_fused and
-                            b.can_tail(nxt) and b.tail_fits(y, batch=B))
+                    fuse = (self.fuse_tail and y.is_cuda and b.can_tail(nxt) and
+                            b.tail_fits(y, batch=B))
                     if last and full_t1 is None and fuse:
                         full_t1 = ops.empty(full.shape[:3] + (nxt.c1.spec.cout,),
                                             dtype=y.dtype, device=y.device)
@@ -325,14 +304,8 @@ class KvResNet50:
             rest = self.blocks
         for i, b in enumerate(rest):
             nxt = rest[i + 1] if i + 1 < len(rest) else None
-            if t1 is None and b.fused_ok(x.shape, x.is_cuda):
-                x = b.call_fused(x)  # whole block, one launch (its conv1 is its own)
-                continue
-            # a block followed by a fused one keeps its conv3 unfused: the fused block
-            # computes its own conv1
-            nxt_fused = nxt is not None and nxt.fused_ok(b.out_shape(x.shape), x.is_cuda)
-            if (self.fuse_tail and x.is_cuda and nxt is not None and not nxt_fused and
-                    b.can_tail(nxt) and b.tail_fits(x)):
+            if (self.fuse_tail and x.is_cuda and nxt is not None and b.can_tail(nxt) and
+                    b.tail_fits(x)):
                 x, t1 = b.call_tail(x, nxt, t1=t1)
             else:
                 x, t1 = b(x, t1=t1), None

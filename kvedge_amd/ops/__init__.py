@@ -355,61 +355,6 @@ SEAM_ENABLED = os.environ.get("KVEDGE_SEAM", "1") != "0"
 SEAM_MIN_WGS = int(os.environ.get("KVEDGE_SEAM_MIN_WGS", "256"))
 
 
-# v11 fused identity bottleneck (csrc/kernels/bneck_fused.hip): an identity block of stages
-# 2 / 3 as ONE launch, z1 / z2 kept in LDS.  Correct (tests/test_kernels_gpu.py::
-# test_bneck_fused*) but measured SLOWER in the bench graph (profiles/r5_v3_bneck_ab.md: 80.4
-# / 77.5k vs 87.0 / 86.3k img/s): the block re-reads x for its residual, so it moves more HBM
-# bytes than the 3x3 + seam pair it replaces, and its memory phases (conv1's x stream, the
-# residual + y stores) and its MFMA phase run in series.  Opt-in: KVEDGE_BNECK=1.
-BNECK_ENABLED = os.environ.get("KVEDGE_BNECK", "0") == "1"
-_BNECK_SHAPES = {(128, 28, 28), (256, 14, 14)}  # (width C, H, W) of bneck_fused.hip kBnTable
-
-
-def bneck_supported(C: int, H: int, W: int) -> bool:
-    return (C, H, W) in _BNECK_SHAPES
-
-
-def mfma_frag_major(w: torch.Tensor) -> torch.Tensor:
-    """Packed weight [N, K] (N % 32 == K % 16 == 0) -> the A-fragment order of
-    v_mfma_f32_32x32x16_bf16: [N/32][K/16][64 lanes][8], lane l holding row l % 32, K
-    elements 8 (l // 32) .. + 8 of its (32-row, 16-deep) fragment.  One kernel load
-    instruction then reads a whole 1 KB fragment."""
-    N, K = w.shape
-    assert N % 32 == 0 and K % 16 == 0, (N, K)
-    f = w.reshape(N // 32, 32, K // 16, 2, 8).permute(0, 2, 3, 1, 4)  # [cs][ks][h][r][8]
-    return f.reshape(N // 32, K // 16, 64, 8).contiguous().view(N, K)
-
-
-def bottleneck_fused(x: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor,
-                     b2: torch.Tensor, w3: torch.Tensor, b3: torch.Tensor,
-                     out: Optional[torch.Tensor] = None, frag=None,
-                     _dbg: int = 0) -> torch.Tensor:
-    """Identity bottleneck y = ReLU(W3 . ReLU(conv3x3(ReLU(W1 . x + b1)) + b2) + b3 + x).
-
-    x: [N, H, W, 4C] bf16 NHWC; w1 [C, 4C], w2 [C, 9C] (tap-major), w3 [4C, C]: the packed
-    bf16 weights of the three folded convs; fp32 biases; ``frag``: the same three weights in
-    :func:`mfma_frag_major` order (what the kernel reads; made here when not given).  GPU:
-    one launch, z1 / z2 never leave LDS.  CPU: the three reference convs, z1 and z2 rounded to bf16 in between (what the
-    kernel keeps in LDS)."""
-    N, H, W, C4 = x.shape
-    C = C4 // 4
-    if out is None:
-        out = empty(N, H, W, C4, dtype=torch.bfloat16, device=x.device)
-    if x.is_cuda:
-        f1, f2, f3 = frag if frag is not None else (mfma_frag_major(w) for w in (w1, w2, w3))
-        _native().bneck_fused(x, f1, b1, f2, b2, f3, b3, out, _dbg)
-        return out
-    s1 = ConvSpec.auto(C4, C, 1, 1, 0, ACT_RELU)
-    s2 = ConvSpec.auto(C, C, 3, 1, 1, ACT_RELU)
-    s3 = ConvSpec.auto(C, C4, 1, 1, 0, ACT_RELU)
-    z1 = torch.empty(N, H, W, C, dtype=torch.bfloat16)
-    z2 = torch.empty(N, H, W, C, dtype=torch.bfloat16)
-    _ref.conv2d(x, s1, w1, b1, None, z1, 0, 0, 0)
-    _ref.conv2d(z1, s2, w2, b2, None, z2, 0, 0, 0)
-    _ref.conv2d(z2, s3, w3, b3, x, out, 0, 0, 0)
-    return out
-
-
 # v13 fused YOLOv8 C2f(32, 32, n=1, shortcut) (csrc/kernels/c2f_fused.hip): the b2 block at
 # 160 x 160.  KVEDGE_C2F=0 = the four-launch path (A/B knob)
 C2F_ENABLED = os.environ.get("KVEDGE_C2F", "1") != "0"

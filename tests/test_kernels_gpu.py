@@ -843,60 +843,6 @@ def test_conv_seam(case):
     assert ran >= 2, "the default pick and at least one explicit seam tile must run"
 
 
-@pytest.mark.parametrize("N,C,H,W", [(2, 128, 28, 28), (5, 128, 28, 28), (1, 256, 14, 14),
-                                     (3, 256, 14, 14), (17, 256, 14, 14), (9, 128, 28, 28)])
-def test_bneck_fused(N, C, H, W):
-    """v11 fused identity bottleneck (ops.bottleneck_fused: conv1 -> 3x3 -> conv3 + residual
-    in one launch, z1 / z2 in LDS) vs the three reference convs with the same bf16
-    intermediates.  Odd batches (partial last XCD round), both instantiations; the output
-    is NaN-poisoned first, so a pixel or channel the kernel skips fails."""
-    C4 = 4 * C
-    g = torch.Generator().manual_seed(C + N)
-    x = torch.relu(_rand((N, H, W, C4), 31)).to(torch.bfloat16)  # post-ReLU like the model
-    s1 = ConvSpec.auto(C4, C, 1, 1, 0, ops.ACT_RELU)
-    s2 = ConvSpec.auto(C, C, 3, 1, 1, ops.ACT_RELU)
-    s3 = ConvSpec.auto(C, C4, 1, 1, 0, ops.ACT_RELU)
-    w1 = ops.pack_conv_weight(torch.randn(C, C4, 1, 1, generator=g) * (2.0 / C4) ** 0.5, s1)
-    w2 = ops.pack_conv_weight(torch.randn(C, C, 3, 3, generator=g) * (2.0 / (9 * C)) ** 0.5, s2)
-    w3 = ops.pack_conv_weight(torch.randn(C4, C, 1, 1, generator=g) * (1.0 / C) ** 0.5, s3)
-    b1, b2, b3 = (torch.randn(n, generator=g) * 0.1 for n in (C, C, C4))
-    assert w1.shape == (C, C4) and w2.shape == (C, 9 * C) and w3.shape == (C4, C)
-    ref = ops.bottleneck_fused(x, w1, b1, w2, b2, w3, b3)
-    out = torch.full((N, H, W, C4), float("nan"), dtype=torch.bfloat16, device="cuda")
-    ops.bottleneck_fused(x.cuda(), w1.cuda(), b1.cuda(), w2.cuda(), b2.cuda(), w3.cuda(),
-                         b3.cuda(), out=out)
-    torch.cuda.synchronize()
-    got = out.cpu()
-    assert not torch.isnan(got.float()).any()
-    _assert_close(got, ref, ("bneck", N, C, H, W))
-
-
-def test_bneck_fused_exact_small_integers():
-    """Layout check with exactly representable data (small integers, power-of-two weights):
-    any swapped tap, channel or pixel mapping changes the result by at least 1."""
-    N, C, H, W = 2, 128, 28, 28
-    C4 = 4 * C
-    g = torch.Generator().manual_seed(5)
-    x = torch.randint(0, 3, (N, H, W, C4), generator=g).to(torch.bfloat16)
-    s1 = ConvSpec.auto(C4, C, 1, 1, 0, ops.ACT_RELU)
-    s2 = ConvSpec.auto(C, C, 3, 1, 1, ops.ACT_RELU)
-    s3 = ConvSpec.auto(C, C4, 1, 1, 0, ops.ACT_RELU)
-    w1 = ops.pack_conv_weight(torch.randint(-1, 2, (C, C4, 1, 1), generator=g).float() / 16, s1)
-    w2 = ops.pack_conv_weight(torch.randint(-1, 2, (C, C, 3, 3), generator=g).float() / 16, s2)
-    w3 = ops.pack_conv_weight(torch.randint(-1, 2, (C4, C, 1, 1), generator=g).float() / 16, s3)
-    b1 = torch.randint(-2, 3, (C,), generator=g).float()
-    b2 = torch.randint(-2, 3, (C,), generator=g).float()
-    b3 = torch.randint(-2, 3, (C4,), generator=g).float()
-    ref = ops.bottleneck_fused(x, w1, b1, w2, b2, w3, b3)
-    got = ops.bottleneck_fused(x.cuda(), w1.cuda(), b1.cuda(), w2.cuda(), b2.cuda(), w3.cuda(),
-                               b3.cuda()).cpu()
-    torch.cuda.synchronize()
-    d = (got.float() - ref.float()).abs()
-    # bf16 rounding of the intermediates is identical on both sides up to summation order
-    assert d.max().item() <= 0.5 * ref.float().abs().max().item() * 2 ** -7 + 1e-6, d.max()
-    assert (d > 0).float().mean().item() < 0.01
-
-
 @pytest.mark.parametrize("tile", list(range(SKN0, N_TILES)))
 @pytest.mark.parametrize("case", [
     # (N, H, W, cin, cout, k, stride, pad, act, res): ResNet-50 edge-batch layers

@@ -129,23 +129,6 @@ def test_s2d_stem_equals_strided_conv():
         assert (y - ref.permute(0, 2, 3, 1)).abs().max() < 0.05 * ref.abs().max() + 0.05
 
 
-def test_mfma_frag_major_layout():
-    """ops.mfma_frag_major: fragment (cs, ks) lane l holds row 32 cs + l % 32, K elements
-    16 ks + 8 (l // 32) .. + 8 -- the A operand of v_mfma_f32_32x32x16_bf16 (bneck_fused.hip)."""
-    import torch
-    from kvedge_amd import ops
-
-    N, K = 96, 48
-    w = torch.arange(N * K, dtype=torch.float32).reshape(N, K)
-    f = ops.mfma_frag_major(w).reshape(N // 32, K // 16, 64, 8)
-    for cs in range(N // 32):
-        for ks in range(K // 16):
-            for lane in (0, 5, 31, 32, 47, 63):
-                r, h = lane % 32, lane // 32
-                want = w[32 * cs + r, 16 * ks + 8 * h:16 * ks + 8 * h + 8]
-                assert torch.equal(f[cs, ks, lane], want)
-
-
 def test_c2f16_reference_matches_block():
     """ops.c2f16's CPU reference is the DC2f four-conv path (same bf16 intermediates)."""
     import torch

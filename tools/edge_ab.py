@@ -3,9 +3,8 @@
 
 An arm is a set of knobs (``KEY=VAL,KEY=VAL``; arms separated by ``;``): environment variables
 read when the engine is built and tuned (``KVEDGE_TILE_LIMIT``: the tuner sees the first N
-tiles only, 0 = the whole table), ``KVEDGE_TAIL1_MIN_ROWS`` (models.resnet.TAIL1_MIN_ROWS,
-the stage-1 fused-tail gate) and ``KVEDGE_BNECK`` (ops.BNECK_ENABLED, the v11 fused identity
-bottleneck).  Per arm the engine of every batch is rebuilt and autotuned,
+tiles only, 0 = the whole table) and ``KVEDGE_TAIL1_MIN_ROWS`` (models.resnet.TAIL1_MIN_ROWS,
+the stage-1 fused-tail gate).  Per arm the engine of every batch is rebuilt and autotuned,
 then ``--steps`` synchronised replays give p50 / p99.  Arms alternate ``--rounds`` times so box drift hits both alike.  Prints one
 JSON line per (round, arm, batch) and a summary of the median p50 per arm.
 
@@ -50,7 +49,6 @@ def main():
                 else:
                     os.environ[k] = v
             resnet.TAIL1_MIN_ROWS = int(os.environ.get("KVEDGE_TAIL1_MIN_ROWS", tail0))
-            ops.BNECK_ENABLED = os.environ.get("KVEDGE_BNECK", "0") == "1"
             tag = ",".join(f"{k}={v}" for k, v in sorted(arm.items()))
             for row in edge_latency(model, KvResNet50.image_size, batches, steps=a.steps):
                 row.update(round=r, arm=tag)

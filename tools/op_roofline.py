@@ -127,15 +127,6 @@ def yolo_stem2_cost(frames, spec0, w0, b0, spec1, w1, b1, out=None):
             2.0 * (m0 * 27 * 16 + m1 * 144 * 32), None)
 
 
-def bneck_cost(x, w1, b1, w2, b2, w3, b3, out=None):
-    N, H, W, C4 = x.shape
-    C = C4 // 4
-    m = N * H * W
-    wb = _b(w1) + _b(w2) + _b(w3)
-    return (f"bneck fused {C4}>{C}>{C}>{C4} +res @{H}x{W}", 2 * m * C4 * 2 + wb,
-            2.0 * m * 17 * C * C, None)
-
-
 def c2f16_cost(x, w1, b1, wm1, bm1, wm2, bm2, w2, b2, out=None, x_coff=0, y_coff=0, S=0):
     N, H, W, _ = x.shape
     m = N * H * W
@@ -174,7 +165,7 @@ def softmax_cost(x, out=None, argmax=None):
 
 COSTS = {"conv2d": conv2d_cost, "conv_dual": conv_dual_cost, "conv_dual2": conv_dual2_cost,
          "conv_tail": conv_tail_cost,
-         "conv_pair": conv_pair_cost, "bottleneck_fused": bneck_cost, "c2f16": c2f16_cost,
+         "conv_pair": conv_pair_cost, "c2f16": c2f16_cost,
          "stem_from_frames": stem_from_frames_cost, "stem12_pool_frames": stem12_cost,
          "yolo_stem2": yolo_stem2_cost,
          "sppf_pool": sppf_cost, "upsample2x": upsample_cost, "yolo_decode": decode_cost,
