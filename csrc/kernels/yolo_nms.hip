@@ -13,9 +13,7 @@
 // NMS: one workgroup per image (latency-bound by nature):
 //   1. compaction of candidates with score > conf into an LDS key array
 //      key = score_bits << 32 | ~index  (descending key = score desc, index asc)
-//   2. sort, descending: up to 2048 keys one rank pass; above that a score-histogram top
-//      set (>= 768 keys) is rank-sorted alone, and the bitonic network over all keys (up
-//      to 16384 in LDS, 128 KiB of the CU's 160 KiB) runs only if greedy exhausts it
+//   2. bitonic sort of up to 16384 keys in LDS (128 KiB of the CU's 160 KiB)
 //   3. greedy suppression in chunks of 64 candidates, ONE WAVE64 LANE PER BOX:
 //      all 8 waves test the chunk against interleaved eighths of the kept list
 //      (ballot -> LDS), then wave 0 resolves the 64x64 in-chunk IoU matrix with
@@ -147,10 +145,9 @@ __device__ __forceinline__ bool iou_gt(float ax1, float ay1, float ax2, float ay
 
 constexpr int kNmsWaves = 8;
 constexpr int kSel = 768;      // top-set target size (rank-sortable: <= kRankSortMax)
-constexpr int kFullSort = 2048;  // up to here every candidate is rank-sorted, no top set
 constexpr int kSelMax = 2048;  // top-set capacity (a wider threshold bin -> full sort)
 constexpr int kBins = 2048;    // score-bit histogram bins
-constexpr int kRankSortMax = 2048;  // rank sort up to here (<= 4 keys per thread), bitonic above
+constexpr int kRankSortMax = 1024;  // rank sort up to here (<= 2 keys per thread), bitonic above
 
 __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __restrict__ boxes,
                                                   const float* __restrict__ scores,
@@ -163,7 +160,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   __shared__ int kept_c[320];
   __shared__ unsigned long long supp[kNmsWaves];
   __shared__ unsigned long long rowp[kNmsWaves][64];
-  __shared__ __attribute__((aligned(16))) unsigned long long sel[kSelMax];  // the top set; its first 8 KB hold the histogram first
+  __shared__ unsigned long long sel[kSelMax];  // the top set; its first 8 KB hold the histogram first
   __shared__ int s_nk;
   __shared__ int ncand;
   __shared__ int s_n2, s_T, s_nsel;
@@ -234,24 +231,14 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   };
   // rank sort: each thread counts the keys above its own with broadcast LDS reads and writes
   // its key to that slot -- one pass, one barrier.  Keys are unique (the index is in the low
-  // word), so the ranks are a permutation.  Two keys per 16-B read (an odd count is padded
-  // with key 0, which never ranks above a candidate), four reads in flight.
-  auto rank_sort = [&](unsigned long long* src, unsigned long long* dst, int n)
+  // word), so the ranks are a permutation.
+  auto rank_sort = [&](const unsigned long long* src, unsigned long long* dst, int n)
       __attribute__((always_inline)) {
-    if (tid == 0 && (n & 1)) src[n] = 0ull;
-    __syncthreads();
-    const int n2 = (n + 1) >> 1;
-    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-    const u64x2* s2 = reinterpret_cast<const u64x2*>(src);
     for (int i0 = 0; i0 < n; i0 += blockDim.x) {
       const int i = i0 + tid;
       const unsigned long long key = i < n ? src[i] : 0ull;
       int r = 0;
-#pragma unroll 4
-      for (int j = 0; j < n2; ++j) {
-        const u64x2 v = s2[j];
-        r += (int)(v.x > key) + (int)(v.y > key);
-      }
+      for (int j = 0; j < n; ++j) r += src[j] > key;
       if (i < n) dst[r] = key;
     }
     __syncthreads();
@@ -274,7 +261,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   int nsel = cnt;
   bool sorted = false;  // the top set already came out of its sort (bucket or fallback)
   bool clobbered = false;  // keys[] now holds the sorted top set, not all candidates
-  if (cnt > kFullSort) {  // (up to kFullSort: one rank sort of all of them, below)
+  if (cnt > kSel) {
     int* hist = reinterpret_cast<int*>(sel);
     for (int i = tid; i < kBins; i += blockDim.x) hist[i] = 0;
     if (tid == 0) s_n2 = 0;
@@ -419,7 +406,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   // one pass and one barrier instead of the bitonic network's log^2 barrier-separated stages
   // (28 at 128 keys, 42 us per image measured: profiles/r4_v5_nms_probe.txt).  Keys are unique
   // (the index is in the low word), so the ranks are a permutation.
-  if (K == sel && cnt > kFullSort) sorted = true;  // the bucket sort above
+  if (K == sel && cnt > kSel) sorted = true;  // the bucket sort above
   if (!(diag & 2) && !sorted) {
     if (K == keys && nsel <= kRankSortMax) {
       rank_sort(keys, sel, nsel);

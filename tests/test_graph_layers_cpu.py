@@ -110,8 +110,8 @@ def _trace_with_pass(reps):
 
 
 def test_op_kernel_counts_from_separators():
-    names = ["bn_kernel", "x", "bn_kernel", "kA", "bn_kernel", "kB", "kB2",
-             "at::native::fill", "bn_kernel", "kC", "bn_kernel"]
+    names = ["bn_kernel", "x", "bn_kernel", "kA", "_ZN6kvedge12_GLOBAL__N_19bn_kernelEPKv", "kB",
+             "kB2", "at::native::fill", "kvedge::bn_kernel", "kC", "bn_kernel"]
     assert gl.op_kernel_counts(names, 3) == [1, 2, 1]
     assert gl.op_kernel_counts(names, 11) is None  # no full pass in the trace
 

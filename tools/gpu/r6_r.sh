@@ -11,3 +11,6 @@ grep -E "max over|diag 0" gpurun_out/${T}_nms$b.txt
 done
 timeout -k 10 900 python -u bench.py --steps 20 --warmup 5 > gpurun_out/${T}_bench.txt 2>gpurun_out/${T}_bench.err || { tail -20 gpurun_out/${T}_bench.err; exit 1; }
 python tools/bench_line.py gpurun_out/${T}_bench.txt
+# stem12 PMC (three counter passes, each its own run) -- VERDICT r5 next 6: VALU- or DMA-bound?
+timeout -k 10 400 bash tools/pmc_cmd.sh gpurun_out/${T}_stem_pmc tools/stem_probe.py --batch 640 --reps 3 > /dev/null 2>&1 || { echo "stem pmc failed"; exit 1; }
+grep -E "stem12|kernel" gpurun_out/${T}_stem_pmc/summary.txt | head -5

@@ -30,6 +30,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -125,7 +126,8 @@ def op_kernel_counts(names, n_ops):
     """Kernels per op of the labelled eager pass: ``names`` = kernel names in launch order up
     to the replay marker; the pass is the last n_ops + 1 separators (bn_kernel) and the
     model kernels between them.  None if the trace has no such pass (older labels)."""
-    sep = [i for i, nm in enumerate(names) if nm.split("::")[-1].startswith("bn_kernel")]
+    # demangled ("...::bn_kernel") or not ("_ZN6kvedge12_GLOBAL__N_19bn_kernelE...")
+    sep = [i for i, nm in enumerate(names) if re.search(r"(^|::|\d)bn_kernel", nm)]
     if len(sep) < n_ops + 1:
         return None
     sep = sep[-(n_ops + 1):]
