@@ -68,6 +68,18 @@ __device__ __forceinline__ unsigned pk_max_i16(unsigned a, unsigned b) {
 
 __device__ __forceinline__ int ring6(int Y) { return (Y + 6 * 4) % kRing; }  // Y >= -24
 
+// two floats -> one dword of two bf16 (one v_cvt_pk_bf16_f32; a in the low half)
+typedef __bf16 stem_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float stem_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned stem_pk2(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((stem_f2){a, b}, stem_bf16x2));
+}
+// byte B (compile-time, 0..11) of a 12-B raw load as float: one v_cvt_f32_ubyteN
+template <int B>
+__device__ __forceinline__ float stem_ub(const u32x3& r) {
+  return (float)((r[B >> 2] >> (8 * (B & 3))) & 0xffu);
+}
+
 __global__ __launch_bounds__(kNT, 2) void stem12_pool_kernel(
     const unsigned char* __restrict__ frames, const bf16* __restrict__ w,
     const float* __restrict__ bias, bf16* __restrict__ y, int N, int Hs, int Ws, int Hp, int Wp,
@@ -87,19 +99,25 @@ __global__ __launch_bounds__(kNT, 2) void stem12_pool_kernel(
 #pragma unroll
     for (int t = 0; t < kKs; ++t)
       wreg[cb][t] = *reinterpret_cast<const bf16x8*>(w + (cb * 32 + fr) * kK + t * 16 + fh * 8);
-  float4 bv[2][4];
+  // the folded-BN bias as the C operand of each block's first MFMA (accumulator layout:
+  // element 4g + e = channel g * 8 + fh * 4 + e): no per-block seeding moves
+  floatx16 bias16[2];
 #pragma unroll
   for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
-      bv[cb][g] = *reinterpret_cast<const float4*>(bias + cb * 32 + g * 8 + fh * 4);
+    for (int g = 0; g < 4; ++g) {
+      float4 v = *reinterpret_cast<const float4*>(bias + cb * 32 + g * 8 + fh * 4);
+      kv_settle(v);  // loaded once: no waits for it inside the band loop
+      bias16[cb][4 * g + 0] = v.x;
+      bias16[cb][4 * g + 1] = v.y;
+      bias16[cb][4 * g + 2] = v.z;
+      bias16[cb][4 * g + 3] = v.w;
+    }
   // loaded once: no waits for them inside the band loop (which has the raw prefetch in flight)
 #pragma unroll
   for (int cb = 0; cb < 2; ++cb) {
 #pragma unroll
     for (int t = 0; t < kKs; ++t) kv_settle(wreg[cb][t]);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) kv_settle(bv[cb][g]);
   }
 
   // ---- zero columns of every ring row (s2d X = -2, -1 and Ws, Ws + 1): written once
@@ -119,62 +137,69 @@ __global__ __launch_bounds__(kNT, 2) void stem12_pool_kernel(
   const int pairs = Ws / 2;     // 12-B loads per input row
   const int per_row = 2 * pairs;  // loads per s2d row (two input rows)
 
+  // Band-invariant load geometry (computed once, not per band): load i of this thread
+  // covers s2d row ld_j of a fetch, input-row parity ld_dy, s2d pixel pair k of that row --
+  // global byte offset ld_g within the s2d row, LDS byte offset ld_l within the ring row
+  int ld_j[kMaxLoads], ld_g[kMaxLoads], ld_l[kMaxLoads];
+  bool ld_dy[kMaxLoads];
+#pragma unroll
+  for (int i = 0; i < kMaxLoads; ++i) {
+    const int q = tid + kNT * i;
+    const int j = q / per_row, rem = q - j * per_row;
+    const int dy = rem / pairs, k = rem - dy * pairs;
+    ld_j[i] = j;
+    ld_dy[i] = dy != 0;
+    ld_g[i] = (dy * W0 + 4 * k) * 3;
+    ld_l[i] = (2 * k + 2) * 24 + dy * 12;
+  }
+  const int srow_bytes = 2 * W0 * 3;  // one s2d row = two input rows
+
   // Raw prefetch of s2d rows [Ylo, Ylo + nrows) of image n (rows outside the image and
-  // loads past the row count read nothing and commit zeros).
+  // loads past the row count read nothing: the out-of-range offset returns zeros).
   u32x3 raw[kMaxLoads];
   unsigned okm = 0;
   auto fetch = [&](int n, int Ylo, int nrows) __attribute__((always_inline)) {
     okm = 0;
+    const int base = (n * Hs + Ylo) * srow_bytes;
 #pragma unroll
     for (int i = 0; i < kMaxLoads; ++i) {
-      const int q = tid + kNT * i;
-      const int j = q / per_row, rem = q - j * per_row;
-      const int dy = rem / pairs, k = rem - dy * pairs;
-      const int Y = Ylo + j;
-      const bool ok = j < nrows && (unsigned)Y < (unsigned)Hs;
-      const int off = ok ? (((n * Hs + Y) * 2 + dy) * W0 + 4 * k) * 3 : 0x7ffffff0;
-      raw[i] = __builtin_amdgcn_raw_buffer_load_b96(rf, off, 0, 0);
+      const int Y = Ylo + ld_j[i];
+      const bool ok = ld_j[i] < nrows && (unsigned)Y < (unsigned)Hs;
+      raw[i] = __builtin_amdgcn_raw_buffer_load_b96(rf, ok ? base + ld_j[i] * srow_bytes + ld_g[i]
+                                                             : 0x7ffffff0, 0, 0);
       okm |= ok ? 1u << i : 0u;
     }
   };
-  // normalised bf16 of 6 bytes (2 input pixels x rgb) starting at byte `sh` of (lo | hi<<32)
-  auto six = [&](unsigned lo, unsigned hi, int sh, bool ok, unsigned out[3]) __attribute__((always_inline)) {
-    const unsigned long long v = ((unsigned long long)hi << 32 | lo) >> (8 * sh);
-    float f[6];
-#pragma unroll
-    for (int e = 0; e < 6; ++e)
-      f[e] = ok ? (float)((unsigned)(v >> (8 * e)) & 0xffu) * nrm.a[e % 3] + nrm.b[e % 3] : 0.f;
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      bf16 p[2] = {f2bf(f[2 * e]), f2bf(f[2 * e + 1])};
-      out[e] = __builtin_bit_cast(unsigned, p);
-    }
-  };
-  // write the fetched rows (and zeros for the rows that are outside the image)
+  // write the fetched rows (and zeros for the rows that are outside the image).  Byte b of
+  // the 12 is colour b % 3 of input pixel 4k + b / 3: v = byte * a[c] + b[c], with b[c]
+  // zeroed for a load that read nothing (its bytes are 0), so out-of-image pixels are 0, not
+  // -mean / std (the conv padding stays exact) -- no per-element select
   auto commit = [&](int Ylo, int nrows) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < kMaxLoads; ++i) {
-      const int q = tid + kNT * i;
-      const int j = q / per_row, rem = q - j * per_row;
-      if (j >= nrows) continue;
-      const int dy = rem / pairs, k = rem - dy * pairs;
+      if (ld_j[i] >= nrows) continue;
       const bool ok = (okm >> i) & 1u;
-      unsigned char* row = ring + ring6(Ylo + j) * RP;
-      unsigned px0[3], px1[3];
-      six(raw[i][0], raw[i][1], 0, ok, px0);  // s2d pixel 2k   (input pixels 4k, 4k+1)
-      six(raw[i][1], raw[i][2], 2, ok, px1);  // s2d pixel 2k+1 (input pixels 4k+2, 4k+3)
-      unsigned char* p0 = row + (2 * k + 2) * 24 + dy * 12;
-      unsigned char* p1 = p0 + 24;
-      if (dy == 0) {
-        *reinterpret_cast<uint2*>(p0) = make_uint2(px0[0], px0[1]);
-        *reinterpret_cast<unsigned*>(p0 + 8) = px0[2];
-        *reinterpret_cast<uint2*>(p1) = make_uint2(px1[0], px1[1]);
-        *reinterpret_cast<unsigned*>(p1 + 8) = px1[2];
+      const float a0 = nrm.a[0], a1 = nrm.a[1], a2 = nrm.a[2];
+      const float c0 = ok ? nrm.b[0] : 0.f, c1 = ok ? nrm.b[1] : 0.f, c2 = ok ? nrm.b[2] : 0.f;
+      const u32x3 r = raw[i];
+      unsigned char* p0 = ring + ring6(Ylo + ld_j[i]) * RP + ld_l[i];  // s2d pixel 2k
+      unsigned char* p1 = p0 + 24;                                       // s2d pixel 2k + 1
+      const unsigned d0 = stem_pk2(stem_ub<0>(r) * a0 + c0, stem_ub<1>(r) * a1 + c1);
+      const unsigned d1 = stem_pk2(stem_ub<2>(r) * a2 + c2, stem_ub<3>(r) * a0 + c0);
+      const unsigned d2 = stem_pk2(stem_ub<4>(r) * a1 + c1, stem_ub<5>(r) * a2 + c2);
+      const unsigned e0 = stem_pk2(stem_ub<6>(r) * a0 + c0, stem_ub<7>(r) * a1 + c1);
+      const unsigned e1 = stem_pk2(stem_ub<8>(r) * a2 + c2, stem_ub<9>(r) * a0 + c0);
+      const unsigned e2 = stem_pk2(stem_ub<10>(r) * a1 + c1, stem_ub<11>(r) * a2 + c2);
+      if (!ld_dy[i]) {
+        *reinterpret_cast<uint2*>(p0) = make_uint2(d0, d1);
+        *reinterpret_cast<unsigned*>(p0 + 8) = d2;
+        *reinterpret_cast<uint2*>(p1) = make_uint2(e0, e1);
+        *reinterpret_cast<unsigned*>(p1 + 8) = e2;
       } else {
-        *reinterpret_cast<unsigned*>(p0) = px0[0];
-        *reinterpret_cast<uint2*>(p0 + 4) = make_uint2(px0[1], px0[2]);
-        *reinterpret_cast<unsigned*>(p1) = px1[0];
-        *reinterpret_cast<uint2*>(p1 + 4) = make_uint2(px1[1], px1[2]);
+        *reinterpret_cast<unsigned*>(p0) = d0;
+        *reinterpret_cast<uint2*>(p0 + 4) = make_uint2(d1, d2);
+        *reinterpret_cast<unsigned*>(p1) = e0;
+        *reinterpret_cast<uint2*>(p1 + 4) = make_uint2(e1, e2);
       }
     }
   };
@@ -192,15 +217,6 @@ __global__ __launch_bounds__(kNT, 2) void stem12_pool_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) ra[r] = ring6(yr - 2 + r) * RP + x * 24 + fh * 16;
       floatx16 acc[2];
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          acc[cb][4 * g + 0] = bv[cb][g].x;
-          acc[cb][4 * g + 1] = bv[cb][g].y;
-          acc[cb][4 * g + 2] = bv[cb][g].z;
-          acc[cb][4 * g + 3] = bv[cb][g].w;
-        }
       bf16x8 af[3];
       auto load = [&](int buf, int t) __attribute__((always_inline)) {
         const unsigned char* pa = ring + ra[t / 3] + (t % 3) * 32;
@@ -213,8 +229,10 @@ __global__ __launch_bounds__(kNT, 2) void stem12_pool_kernel(
 #pragma unroll
       for (int t = 0; t < kKs; ++t) {
         if (t + 2 < kKs) load((t + 2) % 3, t + 2);
-        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wreg[0][t], af[t % 3], acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wreg[1][t], af[t % 3], acc[1], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wreg[0][t], af[t % 3],
+                                                         t == 0 ? bias16[0] : acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wreg[1][t], af[t % 3],
+                                                         t == 0 ? bias16[1] : acc[1], 0, 0, 0);
       }
       // keep the reads two k-steps ahead of the MFMAs
       __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
@@ -228,14 +246,10 @@ __global__ __launch_bounds__(kNT, 2) void stem12_pool_kernel(
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            bf16x4 o;
-            o[0] = f2bf(acc[cb][4 * g + 0]);
-            o[1] = f2bf(acc[cb][4 * g + 1]);
-            o[2] = f2bf(acc[cb][4 * g + 2]);
-            o[3] = f2bf(acc[cb][4 * g + 3]);
-            *reinterpret_cast<bf16x4*>(dst + (cb * 32 + g * 8 + fh * 4) * 2) = o;
-          }
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<uint2*>(dst + (cb * 32 + g * 8 + fh * 4) * 2) =
+                make_uint2(stem_pk2(acc[cb][4 * g + 0], acc[cb][4 * g + 1]),
+                           stem_pk2(acc[cb][4 * g + 2], acc[cb][4 * g + 3]));
       }
     }
   };
