@@ -143,7 +143,7 @@ __device__ __forceinline__ bool iou_gt(float ax1, float ay1, float ax2, float ay
   return inter > thr * fmaxf(aa + ab - inter, 1e-9f);
 }
 
-constexpr int kNmsWaves = 8;
+constexpr int kNmsWaves = 16;  // 1024 threads: the slowest image sets the kernel time (one workgroup per image)
 constexpr int kSel = 768;      // top-set target size (rank-sortable: <= kRankSortMax)
 constexpr int kSelMax = 2048;  // top-set capacity (a wider threshold bin -> full sort)
 constexpr int kBins = 2048;    // score-bit histogram bins
