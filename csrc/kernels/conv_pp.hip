@@ -36,6 +36,8 @@
 //        reading wave's lgkmcnt(0) before a barrier the restaging wave passes first.
 // Steps past the last K-tile are staged out of range (zero fill, into halves already
 // consumed), so every phase issues the same two DMA ops and the counted waits stay exact.
+#include <stdlib.h>
+
 #include "conv_glds_kernel.inc"
 
 #ifndef KV_PP_DMA
@@ -60,7 +62,11 @@ namespace {
 // launch per tile.  The A and B staging descriptors switch tiles at the first A / B half
 // staged for the new tile (every later stage of the old tile precedes it).  Bias: two LDS
 // slots by tile parity (kLdsBias forms), the next tile's written at the end of an epilogue.
-template <int BM, int BN, int MODE, bool PT>
+// ABL (ablation instantiations, timing only -- outputs are wrong; KVEDGE_PP_ABL, tile 117,
+// MODE 0 and 1): bit 0 drops the MFMA clusters, bit 1 the fragment reads, bit 2 the LDS-DMA
+// staging, bit 3 the lgkmcnt(0) before each phase's first barrier, bit 4 both barriers of
+// every phase.  What is left of the phase period says what bounds it (tools/pp_abl.sh).
+template <int BM, int BN, int MODE, bool PT, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const KvConvParams p) {
   constexpr int kHA = BM / 2 * 64, kHB = BN / 2 * 64;  // bf16 elements per A / B half-tile
   constexpr int kStage = (BM + BN) * 64;               // one K-tile: A0 A1 B0 B1
@@ -184,6 +190,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const KvConvParams p) {
   // stage half h (0 A0, 1 A1, 2 B0, 3 B1) of K-step T: AO or BO DMA ops per wave, always
   // issued (out of range past the last K-step)
   auto stage = [&](int h, int T) __attribute__((always_inline)) {
+    if constexpr ((ABL & 4) != 0) return;
     bf16* dst = smem + (T & 1) * kStage + half_off(h) + wid * (h < 2 ? AO : BO) * 512;
     const bool live = T < nsteps;  // wave-uniform
     if (h == 0) a_next();
@@ -279,18 +286,19 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const KvConvParams p) {
   auto phase = [&](const bf16* st, int qm, int qn, auto RA, auto RB, int sh, int sT, bool tile_end)
       __attribute__((always_inline)) {
     if (KV_PP_DMA == 0) stage(sh, sT);
-    if constexpr (decltype(RA)::value) read_a(st, qm);
-    if constexpr (decltype(RB)::value) read_b(st, qn);
+    if constexpr (decltype(RA)::value && (ABL & 2) == 0) read_a(st, qm);
+    if constexpr (decltype(RB)::value && (ABL & 2) == 0) read_b(st, qn);
     if (KV_PP_DMA == 1) stage(sh, sT);
     // tile kt+1 landed (this wave's part): 3 half-tiles stay in flight (2 when this phase's
     // DMA is issued later, inside its MFMA cluster)
     if (tile_end) wait_vm<KV_PP_DMA == 2 ? AO + BO : 2 * AO + BO>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if constexpr ((ABL & 8) == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr ((ABL & 16) == 0) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     if (KV_PP_PRIO) __builtin_amdgcn_s_setprio(1);
-    if (KV_PP_DMA == 2) {
+    if constexpr ((ABL & 1) != 0) {
+    } else if (KV_PP_DMA == 2) {
       mma_half(qm, qn, 0);
       __builtin_amdgcn_sched_barrier(0);
       stage(sh, sT);
@@ -301,7 +309,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const KvConvParams p) {
     }
     if (KV_PP_PRIO) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
+    if constexpr ((ABL & 16) == 0) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
 
@@ -466,6 +474,21 @@ int pp_launch(const KvConvParams* p, int tile, hipStream_t stream) {
   ConvKernelFn fn = wide ? (pt ? KV_PP_FN(256, 256, true) : KV_PP_FN(256, 256, false))
                          : (pt ? KV_PP_FN(512, 128, true) : KV_PP_FN(512, 128, false));
 #undef KV_PP_FN
+  static const int abl = getenv("KVEDGE_PP_ABL") ? atoi(getenv("KVEDGE_PP_ABL")) : 0;
+  if (abl && wide && !pt && (mode == 0 || mode == 1)) {
+#define KV_PP_ABL(a) (mode == 0 ? conv_pp_kernel<256, 256, 0, false, a> : conv_pp_kernel<256, 256, 1, false, a>)
+    switch (abl) {
+      case 1: fn = KV_PP_ABL(1); break;
+      case 2: fn = KV_PP_ABL(2); break;
+      case 4: fn = KV_PP_ABL(4); break;
+      case 6: fn = KV_PP_ABL(6); break;
+      case 8: fn = KV_PP_ABL(8); break;
+      case 16: fn = KV_PP_ABL(16); break;
+      case 22: fn = KV_PP_ABL(22); break;
+      default: return -6;
+    }
+#undef KV_PP_ABL
+  }
   hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(512), 0, stream, *p);
   return hipGetLastError() == hipSuccess ? 0 : -7;
 }
