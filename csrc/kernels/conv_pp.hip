@@ -66,7 +66,6 @@ namespace {
 // MODE 0 and 1): bit 0 drops the MFMA clusters, bit 1 the fragment reads, bit 2 the LDS-DMA
 // staging, bit 3 the lgkmcnt(0) before each phase's first barrier, bit 4 both barriers of
 // every phase.  What is left of the phase period says what bounds it (tools/pp_abl.sh).
-// Bits 5 / 6 (policy experiments, outputs correct): the A / B staging DMAs non-temporal.
 template <int BM, int BN, int MODE, bool PT, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const KvConvParams p) {
   constexpr int kHA = BM / 2 * 64, kHB = BN / 2 * 64;  // bf16 elements per A / B half-tile
@@ -200,14 +199,14 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const KvConvParams p) {
     if (h >= 2) {
 #pragma unroll
       for (int j = 0; j < BO; ++j)
-        glds16<(ABL & 64) ? 2 : 0>(rw, dst + j * 512, live ? b_off[h - 2][j] : kOOB, live ? kbase * 2 : 0);
+        glds16(rw, dst + j * 512, live ? b_off[h - 2][j] : kOOB, live ? kbase * 2 : 0);
       return;
     }
     if (MODE == 1) {
 #pragma unroll
       for (int j = 0; j < AO; ++j) {
         const int v = (live && kbase + a_lc[h][j] * 8 < p.Cin) ? a_off[h][j] : kOOB;
-        glds16<(ABL & 32) ? 2 : 0>(rx, dst + j * 512, v, live ? kbase * 2 : 0);
+        glds16(rx, dst + j * 512, v, live ? kbase * 2 : 0);
       }
     } else if (MODE == 4) {
       // both sources are read here for the last time: non-temporal (de:80 policy)
@@ -225,7 +224,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const KvConvParams p) {
 #pragma unroll
       for (int j = 0; j < AO; ++j) {
         const bool ok = live && tap < p.KH * p.KW && ((a_msk[h][j] >> tap) & 1u);
-        glds16<(ABL & 32) ? 2 : 0>(rx, dst + j * 512, ok ? (a_off[h][j] + toff) * 2 : kOOB, 0);
+        glds16(rx, dst + j * 512, ok ? (a_off[h][j] + toff) * 2 : kOOB, 0);
       }
     }
   };
@@ -486,9 +485,6 @@ int pp_launch(const KvConvParams* p, int tile, hipStream_t stream) {
       case 8: fn = KV_PP_ABL(8); break;
       case 16: fn = KV_PP_ABL(16); break;
       case 22: fn = KV_PP_ABL(22); break;
-      case 32: fn = KV_PP_ABL(32); break;
-      case 64: fn = KV_PP_ABL(64); break;
-      case 96: fn = KV_PP_ABL(96); break;
       default: return -6;
     }
 #undef KV_PP_ABL

@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out; export TMPDIR=/tmp
 T=${TAG:-r6x}
 for A in 0 2 4; do
-  OUT=gpurun_out/${T}_pmc_$A
+  OUT=gpurun_out/${T}_pmc_$A; mkdir -p $OUT
   i=0
   for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS" \
              "TA_BUSY_avr TA_BUSY_max TD_BUSY_avr TD_BUSY_max TCP_PENDING_STALL_CYCLES_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES" \
