@@ -32,8 +32,17 @@ def test_resnet50_bench_config_vs_fp32_reference():
     assert eng.graph is not None and eng.tuning  # the timed configuration
     eng.run()
     torch.cuda.synchronize()
-    for sl in range(S):  # every stream slice of the timed graph
-        _check_resnet_slice(eng, kv, ref, B, S, sl)
+    per = [_check_resnet_slice(eng, kv, ref, B, S, sl)  # every stream slice
+           for sl in range(S)]
+    # the slices run the same kernels on different frames: their agreement with fp32 must be
+    # statistically the same -- a slice-dependent fault (an offset, a stream-ordering race)
+    # that still clears the absolute bounds shows up as a gap between them
+    cos0, pi0 = per[0]
+    for cos, pi in per[1:]:
+        assert abs(cos - cos0) < 3e-3, (cos, cos0)
+        assert abs(float(pi.median()) - float(pi0.median())) < 3e-3, (float(pi.median()),
+                                                                      float(pi0.median()))
+        assert abs(float(pi.min()) - float(pi0.min())) < 0.01, (float(pi.min()), float(pi0.min()))
 
 
 def _check_resnet_slice(eng, kv, ref, B, S, sl):
@@ -91,6 +100,7 @@ def _check_resnet_slice(eng, kv, ref, B, S, sl):
     tie = max(0.25 * float(lg_ref.std()), 4 * noise,
               max([margins[i] for i in flips_t], default=0.0))
     assert all(margins[i] < tie for i in flips), stats
+    return float(cos), per_img
 
 
 def test_yolov8n_bench_config_vs_fp32_reference():
