@@ -3,8 +3,8 @@
 
 An arm is a set of knobs (``KEY=VAL,KEY=VAL``; arms separated by ``;``): environment variables
 read when the engine is built and tuned (``KVEDGE_TILE_LIMIT``: the tuner sees the first N
-tiles only, 0 = the whole table) and ``KVEDGE_TAIL1_MIN_ROWS`` (models.resnet.TAIL1_MIN_ROWS,
-the stage-1 fused-tail gate).  Per arm the engine of every batch is rebuilt and autotuned,
+tiles only, 0 = the whole table), ``KVEDGE_TAIL1_MIN_ROWS`` (models.resnet.TAIL1_MIN_ROWS,
+the stage-1 fused-tail gate) and ``KVEDGE_SEAM_MIN_WGS`` (ops.SEAM_MIN_WGS, the v9 seam gate).  Per arm the engine of every batch is rebuilt and autotuned,
 then ``--steps`` synchronised replays give p50 / p99.  Arms alternate ``--rounds`` times so box drift hits both alike.  Prints one
 JSON line per (round, arm, batch) and a summary of the median p50 per arm.
 
@@ -39,6 +39,7 @@ def main():
     keys = sorted({k for arm in arms for k in arm})
     base = {k: os.environ.get(k) for k in keys}
     tail0 = resnet.TAIL1_MIN_ROWS
+    seam0 = ops.SEAM_MIN_WGS
     res = {}
     for r in range(a.rounds):
         for arm in arms:
@@ -49,6 +50,7 @@ def main():
                 else:
                     os.environ[k] = v
             resnet.TAIL1_MIN_ROWS = int(os.environ.get("KVEDGE_TAIL1_MIN_ROWS", tail0))
+            ops.SEAM_MIN_WGS = int(os.environ.get("KVEDGE_SEAM_MIN_WGS", seam0))
             tag = ",".join(f"{k}={v}" for k, v in sorted(arm.items()))
             for row in edge_latency(model, KvResNet50.image_size, batches, steps=a.steps):
                 row.update(round=r, arm=tag)
