@@ -261,6 +261,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
   int nsel = cnt;
   bool sorted = false;  // the top set already came out of its sort (bucket or fallback)
   bool clobbered = false;  // keys[] now holds the sorted top set, not all candidates
+  int rest_T = -1;         // threshold bin of the top set (the rest = keys below it)
   if (cnt > kSel) {
     int* hist = reinterpret_cast<int*>(sel);
     for (int i = tid; i < kBins; i += blockDim.x) hist[i] = 0;
@@ -369,6 +370,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
     }
     if (s_nsel <= kSelMax && K == keys) {
       const int T = s_T;
+      rest_T = T;
       const int ln = tid & 63;
       if (tid == 0) s_n2 = 0;
       __syncthreads();
@@ -532,8 +534,32 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(const float* __rest
     // head of keys[], so the candidates are compacted from the scores again first (the
     // same set: compaction order does not matter, the sort fixes it)
     if (clobbered) compact();
-    bitonic(keys, cnt);
-    greedy(keys, nsel, cnt);
+    const int nrest = cnt - nsel;
+    if (rest_T >= 0 && nrest <= kRankSortMax && !(diag & 2)) {
+      // only the keys BELOW the top set still need an order: compact them (bin < T) into
+      // sel, rank-sort them into keys[0, nrest) and continue the greedy there -- they all
+      // rank below every top-set key, so this is the full sort's tail (the crowded image's
+      // bitonic network over every candidate was ~25 us of the slowest image, r6 probe)
+      const int ln = tid & 63;
+      if (tid == 0) s_n2 = 0;
+      __syncthreads();
+      for (int i0 = 0; i0 < cnt; i0 += blockDim.x) {
+        const int i = i0 + tid;
+        const unsigned long long key = i < cnt ? keys[i] : 0ull;
+        const bool take = i < cnt && bin_of(key) < rest_T;
+        const unsigned long long m = __ballot(take);
+        int base = 0;
+        if (ln == 0 && m) base = atomicAdd(&s_n2, (int)__popcll(m));
+        base = __shfl(base, 0);
+        if (take) sel[base + (int)__popcll(m & ((1ull << ln) - 1ull))] = key;
+      }
+      __syncthreads();
+      rank_sort(sel, keys, nrest);
+      greedy(keys, 0, nrest);
+    } else {
+      bitonic(keys, cnt);
+      greedy(keys, nsel, cnt);
+    }
   }
   for (int i = nk * 6 + tid; i < max_det * 6; i += blockDim.x) o[i] = 0.f;
   if (tid == 0) count[n] = nk;
