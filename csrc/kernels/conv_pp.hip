@@ -66,6 +66,7 @@ namespace {
 // MODE 0 and 1): bit 0 drops the MFMA clusters, bit 1 the fragment reads, bit 2 the LDS-DMA
 // staging, bit 3 the lgkmcnt(0) before each phase's first barrier, bit 4 both barriers of
 // every phase.  What is left of the phase period says what bounds it (tools/pp_abl.sh).
+// Bits 5 / 6: drop only the B (weight) / only the A (activation) staging DMAs.
 template <int BM, int BN, int MODE, bool PT, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const KvConvParams p) {
   constexpr int kHA = BM / 2 * 64, kHB = BN / 2 * 64;  // bf16 elements per A / B half-tile
@@ -191,6 +192,8 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const KvConvParams p) {
   // issued (out of range past the last K-step)
   auto stage = [&](int h, int T) __attribute__((always_inline)) {
     if constexpr ((ABL & 4) != 0) return;
+    if ((ABL & 32) != 0 && h >= 2) return;
+    if ((ABL & 64) != 0 && h < 2) return;
     bf16* dst = smem + (T & 1) * kStage + half_off(h) + wid * (h < 2 ? AO : BO) * 512;
     const bool live = T < nsteps;  // wave-uniform
     if (h == 0) a_next();
@@ -485,6 +488,10 @@ int pp_launch(const KvConvParams* p, int tile, hipStream_t stream) {
       case 8: fn = KV_PP_ABL(8); break;
       case 16: fn = KV_PP_ABL(16); break;
       case 22: fn = KV_PP_ABL(22); break;
+      case 32: fn = KV_PP_ABL(32); break;
+      case 64: fn = KV_PP_ABL(64); break;
+      case 34: fn = KV_PP_ABL(34); break;
+      case 66: fn = KV_PP_ABL(66); break;
       default: return -6;
     }
 #undef KV_PP_ABL
