@@ -46,6 +46,9 @@
 #ifndef KV_PP_PRIO
 #define KV_PP_PRIO 1
 #endif
+#ifndef KV_PP_KEEPB
+#define KV_PP_KEEPB 1
+#endif
 
 namespace kvedge {
 namespace {
@@ -243,7 +246,10 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const KvConvParams p) {
       for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int d = 0; d < 4; ++d) acc[a][b][c][d] = floatx4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 afr[2][4], bfr[2][2];  // [ks][block]
+  // B fragments per N half (KV_PP_KEEPB: B0's stay in registers from phase 0 to phase 3, so
+  // the K-step reads 24 fragments instead of 28 -- the ablation puts the cost of the staging
+  // in its contention with these LDS reads, profiles/r6_v10_pp_ablation_pmc.md)
+  bf16x8 afr[2][4], bfrq[2][2][2];  // [ks][block] / [qn][ks][block]
   auto read_a = [&](const bf16* st, int qm) __attribute__((always_inline)) {
     const bf16* As = st + half_off(qm);
 #pragma unroll
@@ -261,8 +267,13 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const KvConvParams p) {
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const int row = wn * 32 + b * 16 + fr;
-        bfr[ks][b] = *reinterpret_cast<const bf16x8*>(Bs + row * 64 + (((ks * 4 + fh) ^ sw(row)) << 3));
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(Bs + row * 64 + (((ks * 4 + fh) ^ sw(row)) << 3));
+        if (KV_PP_KEEPB && qn == 1) bfrq[1][ks][b] = v;
+        else bfrq[0][ks][b] = v;
       }
+  };
+  auto bfr_of = [&](int qn, int ks, int b) __attribute__((always_inline)) -> const bf16x8& {
+    return (KV_PP_KEEPB && qn == 1) ? bfrq[1][ks][b] : bfrq[0][ks][b];
   };
   auto mma = [&](int qm, int qn) __attribute__((always_inline)) {
 #pragma unroll
@@ -272,7 +283,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const KvConvParams p) {
 #pragma unroll
         for (int tm = 0; tm < 4; ++tm)
           acc[qn][tn][qm][tm] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ks][tn], afr[ks][tm], acc[qn][tn][qm][tm], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr_of(qn, ks, tn), afr[ks][tm], acc[qn][tn][qm][tm], 0, 0, 0);
   };
   // one phase: reads + staging (+ the per-tile counted wait), barrier, MFMAs, barrier.
   // KV_PP_DMA (A/B knob): 1 = the two DMA ops after the fragment reads (default), 0 = before
@@ -284,7 +295,7 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const KvConvParams p) {
 #pragma unroll
       for (int tm = 0; tm < 4; ++tm)
         acc[qn][tn][qm][tm] =
-            __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[ks][tn], afr[ks][tm], acc[qn][tn][qm][tm], 0, 0, 0);
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr_of(qn, ks, tn), afr[ks][tm], acc[qn][tn][qm][tm], 0, 0, 0);
   };
   auto phase = [&](const bf16* st, int qm, int qn, auto RA, auto RB, int sh, int sT, bool tile_end)
       __attribute__((always_inline)) {
@@ -412,7 +423,9 @@ __global__ __launch_bounds__(512, 1) void conv_pp_kernel(const KvConvParams p) {
     phase(st, 0, 0, T1{}, T1{}, 2, T + 1, false);  // B0 of K-step T+1
     phase(st, 0, 1, T0{}, T1{}, 0, T + 2, false);  // A0 of K-step T+2
     phase(st, 1, 1, T1{}, T0{}, 3, T + 2, false);  // B1 of K-step T+2
-    phase(st, 1, 0, T0{}, T1{}, 1, T + 2, true);   // A1 of K-step T+2; wait: K-step T+1
+    // (KV_PP_KEEPB: B0 is still in registers from phase 0, no reads in this phase)
+    if constexpr (KV_PP_KEEPB) phase(st, 1, 0, T0{}, T0{}, 1, T + 2, true);
+    else phase(st, 1, 0, T0{}, T1{}, 1, T + 2, true);   // A1 of K-step T+2; wait: K-step T+1
     if (PT && ++c_kt == nk) {  // the tile's last K-step: epilogue, fresh accumulators
       epilogue(c_i);
       c_kt = 0;
