@@ -17,9 +17,10 @@ import torch
 
 from .. import ops
 
-_OPS = ("conv2d", "conv_dual", "conv_tail", "conv_pair", "bottleneck_fused", "c2f16", "stem_pool", "stem_pool_frames", "stem_from_frames", "maxpool2d", "sppf_pool", "global_avgpool",
-        "softmax_rows", "upsample2x", "yolo_decode", "nms", "synth_frames", "preprocess",
-        "batchnorm_nhwc")
+_OPS = ("conv2d", "conv_dual", "conv_dual2", "conv_tail", "conv_pair", "c2f16", "stem_pool",
+        "stem_pool_frames", "stem12_pool_frames", "stem_from_frames", "yolo_stem2", "maxpool2d",
+        "sppf_pool", "global_avgpool", "pooled_fc", "softmax_rows", "upsample2x", "yolo_decode",
+        "nms", "synth_frames", "preprocess", "batchnorm_nhwc")
 
 
 def _shape_of(out):
